@@ -1,0 +1,199 @@
+// SPDX-License-Identifier: MIT
+// CPU backend: OpenMP implementation of every backend op.  It is both the `backend = "CPU"`
+// solver (reference: Simulation_CPU.jl:14-133, Threads.@threads over z) and the golden
+// model the gfx950 kernels are tested against.  Same Philox noise stream as the GPU.
+#include <omp.h>
+#include <string.h>
+
+#include <algorithm>
+#include <stdexcept>
+
+#include "gs/capi_impl.h"
+
+namespace {
+
+using gs::Box;
+using gs::Geom;
+
+template <typename T>
+class CpuBackend final : public gs::Backend {
+ public:
+  CpuBackend(const Geom& g, const gs::Params& p, void* b0, void* b1, void* send, void* recv)
+      : g_(g), p_(p) {
+    buf_[0] = (T*)b0;
+    buf_[1] = (T*)b1;
+    send_ = (T*)send;
+    recv_ = (T*)recv;
+    if (!b0 || !b1) throw std::runtime_error("null field buffer");
+  }
+
+  void fill_box(int b, const Box& bx, double u, double v) override {
+    T* d = buf_[b];
+    const T uu = (T)u, vv = (T)v;
+#pragma omp parallel for collapse(2) schedule(static)
+    for (int z = bx.z0; z < bx.z0 + bx.nz; ++z)
+      for (int y = bx.y0; y < bx.y0 + bx.ny; ++y) {
+        T* row = d + 2 * gs::lin(g_, 0, y, z);
+        for (int x = bx.x0; x < bx.x0 + bx.nx; ++x) {
+          row[2 * x] = uu;
+          row[2 * x + 1] = vv;
+        }
+      }
+  }
+
+  void seed(int b) override {
+    // global cube [L/2-6, L/2+6]^3 (0-based, inclusive), clipped to this rank.
+    // The reference only defines it for a cubic domain; use each axis' own extent.
+    T* d = buf_[b];
+    int64_t lo[3], hi[3];
+    const int64_t L[3] = {g_.Lx, g_.Ly, g_.Lz};
+    const int64_t o[3] = {g_.ox, g_.oy, g_.oz};
+    const int n[3] = {g_.nx, g_.ny, g_.nz};
+    for (int a = 0; a < 3; ++a) {
+      const int64_t mn = L[a] / 2 - 6, mx = L[a] / 2 + 6;
+      lo[a] = std::max<int64_t>(mn, o[a]) - o[a];
+      hi[a] = std::min<int64_t>(mx + 1, o[a] + n[a]) - o[a];
+    }
+    for (int64_t z = lo[2]; z < hi[2]; ++z)
+      for (int64_t y = lo[1]; y < hi[1]; ++y)
+        for (int64_t x = lo[0]; x < hi[0]; ++x) {
+          T* c = d + 2 * gs::lin(g_, (int)x, (int)y, (int)z);
+          c[0] = (T)0.25;
+          c[1] = (T)0.33;
+        }
+  }
+
+  void step(int src, int dst, const Box& R, int64_t t) override {
+    const T* s = buf_[src];
+    T* d = buf_[dst];
+    const gs::Coef<T> c = gs::make_coef<T>(p_);
+    const bool noise = p_.noise != 0.0;
+    const int64_t sx = 2, sy = 2 * (int64_t)g_.px, sz = 2 * gs::plane_elems(g_);
+    const Geom g = g_;
+    const uint64_t seed = p_.seed;
+#pragma omp parallel
+    {
+      gs::U4* cache = new gs::U4[R.nx > 0 ? R.nx : 1];
+#pragma omp for schedule(static)
+      for (int y = R.y0; y < R.y0 + R.ny; ++y) {
+        int64_t gy = g.oy + y;
+        if (gy < 0) gy += g.Ly; else if (gy >= g.Ly) gy -= g.Ly;
+        for (int z = R.z0; z < R.z0 + R.nz; ++z) {
+          int64_t gz = g.oz + z;
+          if (gz < 0) gz += g.Lz; else if (gz >= g.Lz) gz -= g.Lz;
+          if (noise && (z == R.z0 || (gz & 3) == 0)) {
+            for (int x = R.x0; x < R.x0 + R.nx; ++x) {
+              int64_t gx = g.ox + x;
+              if (gx < 0) gx += g.Lx; else if (gx >= g.Lx) gx -= g.Lx;
+              cache[x - R.x0] = gs::noise_block(gx, gy, gz >> 2, g.Lx, g.Ly, (uint64_t)t, seed);
+            }
+          }
+          const int64_t base = 2 * gs::lin(g, 0, y, z);
+          for (int x = R.x0; x < R.x0 + R.nx; ++x) {
+            const int64_t i = base + 2 * (int64_t)x;
+            const T u = s[i], v = s[i + 1];
+            const T su = s[i - sx] + s[i + sx] + s[i - sy] + s[i + sy] + s[i - sz] + s[i + sz];
+            const T sv = s[i - sx + 1] + s[i + sx + 1] + s[i - sy + 1] + s[i + sy + 1] +
+                         s[i - sz + 1] + s[i + sz + 1];
+            T r = (T)0;
+            if (noise) r = gs::uniform_pm1<T>(gs::u4_get(cache[x - R.x0], (int)(gz & 3)));
+            T uo, vo;
+            gs::gs_update<T>(c, u, v, su, sv, r, uo, vo);
+            d[i] = uo;
+            d[i + 1] = vo;
+          }
+        }
+      }
+      delete[] cache;
+    }
+  }
+
+  template <bool PACK>
+  void pack_impl(int b, const gs::HaloMsg* msgs, int n, T* pk) {
+    T* f = buf_[b];
+    for (int m = 0; m < n; ++m) {
+      const Box& bx = msgs[m].box;
+      T* out = pk + 2 * msgs[m].offset;
+#pragma omp parallel for collapse(2) schedule(static)
+      for (int z = 0; z < bx.nz; ++z)
+        for (int y = 0; y < bx.ny; ++y) {
+          T* row = f + 2 * gs::lin(g_, bx.x0, bx.y0 + y, bx.z0 + z);
+          T* p = out + 2 * ((int64_t)z * bx.ny + y) * bx.nx;
+          if (PACK) memcpy(p, row, sizeof(T) * 2 * bx.nx);
+          else memcpy(row, p, sizeof(T) * 2 * bx.nx);
+        }
+    }
+  }
+  void pack(int b, const gs::HaloPlan& p) override { pack_impl<true>(b, p.send, p.nsend, send_); }
+  void unpack(int b, const gs::HaloPlan& p) override { pack_impl<false>(b, p.recv, p.nrecv, recv_); }
+  void self_copy(int64_t so, int64_t d, int64_t n) override {
+    memcpy(recv_ + 2 * d, send_ + 2 * so, sizeof(T) * 2 * n);
+  }
+
+  void extract(int b, void* uo, void* vo) override {
+    const T* f = buf_[b];
+    T* u = (T*)uo;
+    T* v = (T*)vo;
+#pragma omp parallel for collapse(2) schedule(static)
+    for (int z = 0; z < g_.nz; ++z)
+      for (int y = 0; y < g_.ny; ++y) {
+        const T* row = f + 2 * gs::lin(g_, 0, y, z);
+        const int64_t o = ((int64_t)z * g_.ny + y) * g_.nx;
+        for (int x = 0; x < g_.nx; ++x) {
+          if (u) u[o + x] = row[2 * x];
+          if (v) v[o + x] = row[2 * x + 1];
+        }
+      }
+  }
+
+  void insert(int b, const void* ui, const void* vi) override {
+    T* f = buf_[b];
+    const T* u = (const T*)ui;
+    const T* v = (const T*)vi;
+#pragma omp parallel for collapse(2) schedule(static)
+    for (int z = 0; z < g_.nz; ++z)
+      for (int y = 0; y < g_.ny; ++y) {
+        T* row = f + 2 * gs::lin(g_, 0, y, z);
+        const int64_t o = ((int64_t)z * g_.ny + y) * g_.nx;
+        for (int x = 0; x < g_.nx; ++x) {
+          row[2 * x] = u[o + x];
+          row[2 * x + 1] = v[o + x];
+        }
+      }
+  }
+
+  void stats(int b, double* out) override {
+    const T* f = buf_[b];
+    double su = 0, sv = 0, mnu = 1e300, mxu = -1e300, mnv = 1e300, mxv = -1e300;
+#pragma omp parallel for collapse(2) reduction(+ : su, sv) reduction(min : mnu, mnv) \
+    reduction(max : mxu, mxv) schedule(static)
+    for (int z = 0; z < g_.nz; ++z)
+      for (int y = 0; y < g_.ny; ++y) {
+        const T* row = f + 2 * gs::lin(g_, 0, y, z);
+        for (int x = 0; x < g_.nx; ++x) {
+          const double u = row[2 * x], v = row[2 * x + 1];
+          su += u; sv += v;
+          mnu = std::min(mnu, u); mxu = std::max(mxu, u);
+          mnv = std::min(mnv, v); mxv = std::max(mxv, v);
+        }
+      }
+    out[0] = su; out[1] = mnu; out[2] = mxu; out[3] = sv; out[4] = mnv; out[5] = mxv;
+  }
+
+ private:
+  Geom g_;
+  gs::Params p_;
+  T* buf_[2];
+  T* send_;
+  T* recv_;
+};
+
+}  // namespace
+
+gs::Backend* gs_make_backend(int32_t dtype, const gs::Geom& g, const gs::Params& p, void* b0,
+                             void* b1, void* send, void* recv, void* stream) {
+  (void)stream;
+  if (dtype == gs::kF32) return new CpuBackend<float>(g, p, b0, b1, send, recv);
+  if (dtype == gs::kF64) return new CpuBackend<double>(g, p, b0, b1, send, recv);
+  throw std::runtime_error("unsupported dtype");
+}

@@ -1,0 +1,266 @@
+// SPDX-License-Identifier: MIT
+// gfx950 kernels for the Gray-Scott engine (included by backend_hip.hip only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "gs/common.h"
+
+namespace gsk {
+
+using gs::Box;
+using gs::Geom;
+
+template <typename T> struct Vec2;
+template <> struct Vec2<float> { using type = float2; };
+template <> struct Vec2<double> { using type = double2; };
+
+__device__ __forceinline__ int64_t wrap(int64_t a, int64_t L) {
+  return a < 0 ? a + L : (a >= L ? a - L : a);
+}
+
+// ------------------------------------------------------------------------------------------
+// fills / seed
+// ------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void k_fill(typename Vec2<T>::type* __restrict__ f, Geom g, Box b,
+                                              T u, T v) {
+  const int64_t n = gs::box_cells(b);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int x = (int)(i % b.nx);
+    const int64_t r = i / b.nx;
+    const int y = (int)(r % b.ny);
+    const int z = (int)(r / b.ny);
+    typename Vec2<T>::type c;
+    c.x = u;
+    c.y = v;
+    f[gs::lin(g, b.x0 + x, b.y0 + y, b.z0 + z)] = c;
+  }
+}
+
+template <typename T>
+void launch_fill(typename Vec2<T>::type* f, const Geom& g, const Box& b, T u, T v, hipStream_t s) {
+  const int64_t n = gs::box_cells(b);
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 8192);
+  k_fill<T><<<blocks, 256, 0, s>>>(f, g, b, u, v);
+}
+
+template <typename T>
+void launch_seed(typename Vec2<T>::type* f, const Geom& g, hipStream_t s) {
+  // global cube [L/2-6, L/2+6]^3 clipped to this rank
+  const int64_t L[3] = {g.Lx, g.Ly, g.Lz};
+  const int64_t o[3] = {g.ox, g.oy, g.oz};
+  const int n[3] = {g.nx, g.ny, g.nz};
+  int lo[3], cnt[3];
+  for (int a = 0; a < 3; ++a) {
+    const int64_t mn = L[a] / 2 - 6, mx = L[a] / 2 + 6;
+    const int64_t l = std::max<int64_t>(mn, o[a]) - o[a];
+    const int64_t h = std::min<int64_t>(mx + 1, o[a] + n[a]) - o[a];
+    lo[a] = (int)l;
+    cnt[a] = h > l ? (int)(h - l) : 0;
+  }
+  Box b{lo[0], lo[1], lo[2], cnt[0], cnt[1], cnt[2]};
+  if (gs::box_cells(b) == 0) return;
+  launch_fill<T>(f, g, b, (T)0.25, (T)0.33, s);
+}
+
+// ------------------------------------------------------------------------------------------
+// Single fused step (7-point Laplacian + reaction + Philox noise + Euler) over a region.
+// Lanes run along x (coalesced 8/16-B loads of interleaved (u,v)); each thread marches in z
+// keeping planes z-1, z, z+1 in registers, so every cell is fetched from HBM once and the
+// x/y neighbours are L1/L2 hits.  One Philox block per thread feeds four z-planes.
+// ------------------------------------------------------------------------------------------
+struct StepArgs {
+  Geom g;
+  Box r;
+  int32_t zchunk;
+  int32_t _pad;
+  int64_t t;
+};
+
+template <typename T, bool NOISE>
+__global__ __launch_bounds__(256) void k_step1(const typename Vec2<T>::type* __restrict__ s,
+                                               typename Vec2<T>::type* __restrict__ d,
+                                               StepArgs a, gs::Coef<T> c, uint64_t seed) {
+  using V2 = typename Vec2<T>::type;
+  const Geom& g = a.g;
+  const int x = a.r.x0 + blockIdx.x * 64 + threadIdx.x;
+  const int y = a.r.y0 + blockIdx.y * 4 + threadIdx.y;
+  const int z0 = a.r.z0 + blockIdx.z * a.zchunk;
+  const int z1 = min(z0 + a.zchunk, a.r.z0 + a.r.nz);
+  if (x >= a.r.x0 + a.r.nx || y >= a.r.y0 + a.r.ny || z0 >= z1) return;
+  const int64_t PX = g.px;
+  const int64_t PZ = gs::plane_elems(g);
+  int64_t i = gs::lin(g, x, y, z0);
+  const int64_t gx = wrap(g.ox + x, g.Lx);
+  const int64_t gy = wrap(g.oy + y, g.Ly);
+  V2 cm = s[i - PZ];
+  V2 c0 = s[i];
+  gs::U4 blk{0, 0, 0, 0};
+  for (int z = z0; z < z1; ++z) {
+    const V2 cp = s[i + PZ];
+    const V2 xm = s[i - 1], xp = s[i + 1], ym = s[i - PX], yp = s[i + PX];
+    const T su = (xm.x + xp.x) + (ym.x + yp.x) + (cm.x + cp.x);
+    const T sv = (xm.y + xp.y) + (ym.y + yp.y) + (cm.y + cp.y);
+    T r = (T)0;
+    if (NOISE) {
+      const int64_t gz = wrap(g.oz + z, g.Lz);
+      if (z == z0 || (gz & 3) == 0) blk = gs::noise_block(gx, gy, gz >> 2, g.Lx, g.Ly, (uint64_t)a.t, seed);
+      r = gs::uniform_pm1<T>(gs::u4_get(blk, (int)(gz & 3)));
+    }
+    V2 o;
+    gs::gs_update<T>(c, c0.x, c0.y, su, sv, r, o.x, o.y);
+    d[i] = o;
+    cm = c0;
+    c0 = cp;
+    i += PZ;
+  }
+}
+
+template <typename T>
+void launch_step1(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, const Geom& g,
+                  const gs::Params& p, const Box& r, int64_t t, hipStream_t st) {
+  StepArgs a;
+  a.g = g;
+  a.r = r;
+  a.t = t;
+  const int bx = (r.nx + 63) / 64, by = (r.ny + 3) / 4;
+  const int64_t xy = (int64_t)bx * by;
+  int nzc = (int)std::max<int64_t>(1, (2048 + xy - 1) / xy);
+  int zc = (r.nz + nzc - 1) / nzc;
+  zc = std::max(zc, std::min(r.nz, 8));
+  nzc = (r.nz + zc - 1) / zc;
+  a.zchunk = zc;
+  dim3 grid(bx, by, nzc), block(64, 4, 1);
+  const gs::Coef<T> c = gs::make_coef<T>(p);
+  if (p.noise != 0.0) k_step1<T, true><<<grid, block, 0, st>>>(s, d, a, c, p.seed);
+  else k_step1<T, false><<<grid, block, 0, st>>>(s, d, a, c, p.seed);
+}
+
+template <typename T>
+bool launch_fused(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, const Geom& g,
+                  const gs::Params& p, int n, int64_t t, hipStream_t st) {
+  (void)s; (void)d; (void)g; (void)p; (void)n; (void)t; (void)st;
+  return false;
+}
+
+// ------------------------------------------------------------------------------------------
+// halo pack / unpack: all messages in one launch (blockIdx.y = message)
+// ------------------------------------------------------------------------------------------
+struct PackArgs {
+  Box box[gs::kMaxMsgs];
+  int64_t off[gs::kMaxMsgs];
+};
+
+template <typename T, bool PACK>
+__global__ __launch_bounds__(256) void k_pack(typename Vec2<T>::type* __restrict__ f,
+                                              typename Vec2<T>::type* __restrict__ buf, Geom g,
+                                              PackArgs a) {
+  const Box b = a.box[blockIdx.y];
+  typename Vec2<T>::type* p = buf + a.off[blockIdx.y];
+  const int64_t n = gs::box_cells(b);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int x = (int)(i % b.nx);
+    const int64_t r = i / b.nx;
+    const int y = (int)(r % b.ny);
+    const int z = (int)(r / b.ny);
+    const int64_t j = gs::lin(g, b.x0 + x, b.y0 + y, b.z0 + z);
+    if (PACK) p[i] = f[j];
+    else f[j] = p[i];
+  }
+}
+
+template <typename T, bool PACK>
+void launch_pack(typename Vec2<T>::type* f, typename Vec2<T>::type* buf, const Geom& g,
+                 const gs::HaloMsg* msgs, int n, hipStream_t st) {
+  PackArgs a;
+  int64_t mx = 0;
+  for (int i = 0; i < n; ++i) {
+    a.box[i] = msgs[i].box;
+    a.off[i] = msgs[i].offset;
+    mx = std::max<int64_t>(mx, gs::box_cells(msgs[i].box));
+  }
+  const int bx = (int)std::max<int64_t>(1, std::min<int64_t>((mx + 255) / 256, 1024));
+  k_pack<T, PACK><<<dim3(bx, n, 1), 256, 0, st>>>(f, buf, g, a);
+}
+
+// ------------------------------------------------------------------------------------------
+// ghost-stripped interior <-> contiguous (z,y,x) arrays (get_fields, Simulation_CPU.jl:125)
+// ------------------------------------------------------------------------------------------
+template <typename T, bool EXTRACT>
+__global__ __launch_bounds__(256) void k_interior(typename Vec2<T>::type* __restrict__ f,
+                                                  T* __restrict__ u, T* __restrict__ v, Geom g) {
+  const int x = blockIdx.x * 256 + threadIdx.x;
+  const int y = blockIdx.y;
+  const int z = blockIdx.z;
+  if (x >= g.nx) return;
+  const int64_t j = gs::lin(g, x, y, z);
+  const int64_t o = ((int64_t)z * g.ny + y) * g.nx + x;
+  if (EXTRACT) {
+    const typename Vec2<T>::type c = f[j];
+    if (u) u[o] = c.x;
+    if (v) v[o] = c.y;
+  } else {
+    typename Vec2<T>::type c;
+    c.x = u[o];
+    c.y = v[o];
+    f[j] = c;
+  }
+}
+
+template <typename T>
+void launch_extract(const typename Vec2<T>::type* f, T* u, T* v, const Geom& g, hipStream_t st) {
+  dim3 grid((g.nx + 255) / 256, g.ny, g.nz);
+  k_interior<T, true><<<grid, 256, 0, st>>>(const_cast<typename Vec2<T>::type*>(f), u, v, g);
+}
+template <typename T>
+void launch_insert(typename Vec2<T>::type* f, const T* u, const T* v, const Geom& g, hipStream_t st) {
+  dim3 grid((g.nx + 255) / 256, g.ny, g.nz);
+  k_interior<T, false><<<grid, 256, 0, st>>>(f, const_cast<T*>(u), const_cast<T*>(v), g);
+}
+
+// ------------------------------------------------------------------------------------------
+// diagnostics: per-block partial sum/min/max of u and v (off the hot path)
+// ------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void k_stats(const typename Vec2<T>::type* __restrict__ f, Geom g,
+                                               double* __restrict__ out) {
+  __shared__ double sh[6][256];
+  double su = 0, sv = 0, mnu = 1e300, mxu = -1e300, mnv = 1e300, mxv = -1e300;
+  const int64_t n = (int64_t)g.nx * g.ny * g.nz;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int x = (int)(i % g.nx);
+    const int64_t r = i / g.nx;
+    const typename Vec2<T>::type c = f[gs::lin(g, x, (int)(r % g.ny), (int)(r / g.ny))];
+    const double u = c.x, v = c.y;
+    su += u; sv += v;
+    mnu = fmin(mnu, u); mxu = fmax(mxu, u);
+    mnv = fmin(mnv, v); mxv = fmax(mxv, v);
+  }
+  const int t = threadIdx.x;
+  sh[0][t] = su; sh[1][t] = mnu; sh[2][t] = mxu; sh[3][t] = sv; sh[4][t] = mnv; sh[5][t] = mxv;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (t < w) {
+      sh[0][t] += sh[0][t + w];
+      sh[3][t] += sh[3][t + w];
+      sh[1][t] = fmin(sh[1][t], sh[1][t + w]);
+      sh[4][t] = fmin(sh[4][t], sh[4][t + w]);
+      sh[2][t] = fmax(sh[2][t], sh[2][t + w]);
+      sh[5][t] = fmax(sh[5][t], sh[5][t + w]);
+    }
+    __syncthreads();
+  }
+  if (t < 6) out[6 * blockIdx.x + t] = sh[t][0];
+}
+
+template <typename T>
+void launch_stats(const typename Vec2<T>::type* f, const Geom& g, double* ws, int blocks, hipStream_t st) {
+  k_stats<T><<<blocks, 256, 0, st>>>(f, g, ws);
+}
+
+}  // namespace gsk

@@ -1,0 +1,45 @@
+// SPDX-License-Identifier: MIT
+// C ABI shared by libgs_core.so (CPU/OpenMP backend) and libgs_hip.so (gfx950 backend).
+// Python binds both through ctypes (grayscott_amd/ops/native.py); the CLI tools link them.
+#pragma once
+
+#include <stdint.h>
+#include "gs/common.h"
+
+extern "C" {
+
+typedef struct gs_engine gs_engine;
+
+// Create an engine over caller-owned buffers.  buf0/buf1: the two (u,v) state buffers
+// (gs::total_elems(g) pairs each).  sendbuf/recvbuf: packed halo buffers (plan sizes, may
+// be NULL when the rank has no neighbour).  stream: hipStream_t for the HIP backend.
+gs_engine* gs_create(int32_t dtype, const gs::Geom* g, const gs::Params* p, const int32_t* nbr27,
+                     int32_t rank, int32_t fuse, int32_t use_fused, void* buf0, void* buf1,
+                     void* sendbuf, void* recvbuf, void* stream);
+void gs_destroy(gs_engine* e);
+const char* gs_last_error(void);
+
+int gs_init_fields(gs_engine* e);
+int gs_advance(gs_engine* e, int64_t nsteps);
+int gs_exchange(gs_engine* e);
+int64_t gs_get_step(gs_engine* e);
+int gs_set_step(gs_engine* e, int64_t t);
+int gs_current_buffer(gs_engine* e);
+int gs_sync(gs_engine* e);
+int gs_extract(gs_engine* e, void* u, void* v);
+int gs_insert(gs_engine* e, const void* u, const void* v);
+int gs_stats(gs_engine* e, double* out6);
+int gs_set_transport(gs_engine* e, int (*fn)(void*), void* user);
+// halo plan introspection: counts and per-message (dir, peer, offset, cells)
+int gs_plan_info(gs_engine* e, int64_t* send_cells, int64_t* recv_cells, int32_t* nsend, int32_t* nrecv);
+int gs_plan_msg(gs_engine* e, int32_t which, int32_t i, int64_t* out4);
+
+// helpers usable without an engine
+int64_t gs_geom_total_elems(const gs::Geom* g);
+void gs_make_geom(gs::Geom* out, int nx, int ny, int nz, int H, int64_t ox, int64_t oy, int64_t oz,
+                  int64_t Lx, int64_t Ly, int64_t Lz, int periodic);
+void gs_noise_block(int64_t gx, int64_t gy, int64_t gz4, int64_t Lx, int64_t Ly, uint64_t step,
+                    uint64_t seed, uint32_t* out4);
+int gs_plan_sizes(const gs::Geom* g, const int32_t* nbr27, int32_t diagonals, int64_t* send_cells,
+                  int64_t* recv_cells);
+}

@@ -1,0 +1,118 @@
+// SPDX-License-Identifier: MIT
+// Implementation of the C ABI in capi.h.  Included exactly once by each backend library,
+// which must define:
+//   gs::Backend* gs_make_backend(int32_t dtype, const gs::Geom& g, const gs::Params& p,
+//                                void* b0, void* b1, void* send, void* recv, void* stream);
+//   void gs_backend_post_create(gs::Engine* e);   // optional hook (may be empty)
+#pragma once
+
+#include <exception>
+#include <string>
+
+#include "gs/capi.h"
+#include "gs/engine.h"
+
+gs::Backend* gs_make_backend(int32_t dtype, const gs::Geom& g, const gs::Params& p, void* b0,
+                             void* b1, void* send, void* recv, void* stream);
+
+struct gs_engine {
+  gs::Engine* eng;
+};
+
+static thread_local std::string g_gs_err;
+
+#define GS_TRY(body)                          \
+  try {                                       \
+    body;                                     \
+    return 0;                                 \
+  } catch (const std::exception& ex) {        \
+    g_gs_err = ex.what();                     \
+    return -1;                                \
+  }
+
+extern "C" {
+
+const char* gs_last_error(void) { return g_gs_err.c_str(); }
+
+gs_engine* gs_create(int32_t dtype, const gs::Geom* g, const gs::Params* p, const int32_t* nbr27,
+                     int32_t rank, int32_t fuse, int32_t use_fused, void* buf0, void* buf1,
+                     void* sendbuf, void* recvbuf, void* stream) {
+  try {
+    gs::EngineConfig c{};
+    c.g = *g;
+    c.p = *p;
+    for (int i = 0; i < 27; ++i) c.nbr[i] = nbr27[i];
+    c.rank = rank;
+    c.fuse = fuse;
+    c.use_fused = use_fused;
+    gs::Backend* be = gs_make_backend(dtype, *g, *p, buf0, buf1, sendbuf, recvbuf, stream);
+    gs_engine* e = new gs_engine;
+    e->eng = new gs::Engine(c, be);
+    return e;
+  } catch (const std::exception& ex) {
+    g_gs_err = ex.what();
+    return nullptr;
+  }
+}
+
+void gs_destroy(gs_engine* e) {
+  if (!e) return;
+  delete e->eng;
+  delete e;
+}
+
+int gs_init_fields(gs_engine* e) { GS_TRY(e->eng->init_fields()) }
+int gs_advance(gs_engine* e, int64_t n) { GS_TRY(e->eng->advance(n)) }
+int gs_exchange(gs_engine* e) { GS_TRY(e->eng->exchange()) }
+int64_t gs_get_step(gs_engine* e) { return e->eng->step(); }
+int gs_set_step(gs_engine* e, int64_t t) { GS_TRY(e->eng->set_step(t)) }
+int gs_current_buffer(gs_engine* e) { return e->eng->cur(); }
+int gs_sync(gs_engine* e) { GS_TRY(e->eng->backend()->host_sync()) }
+int gs_extract(gs_engine* e, void* u, void* v) {
+  GS_TRY(e->eng->backend()->extract(e->eng->cur(), u, v))
+}
+int gs_insert(gs_engine* e, const void* u, const void* v) {
+  GS_TRY(e->eng->backend()->insert(e->eng->cur(), u, v))
+}
+int gs_stats(gs_engine* e, double* out6) { GS_TRY(e->eng->backend()->stats(e->eng->cur(), out6)) }
+int gs_set_transport(gs_engine* e, int (*fn)(void*), void* user) {
+  GS_TRY(e->eng->set_transport(fn, user))
+}
+
+int gs_plan_info(gs_engine* e, int64_t* sc, int64_t* rc, int32_t* ns, int32_t* nr) {
+  const gs::HaloPlan& p = e->eng->plan();
+  *sc = p.send_cells; *rc = p.recv_cells; *ns = p.nsend; *nr = p.nrecv;
+  return 0;
+}
+
+int gs_plan_msg(gs_engine* e, int32_t which, int32_t i, int64_t* out4) {
+  const gs::HaloPlan& p = e->eng->plan();
+  const gs::HaloMsg* m = which == 0 ? p.send : p.recv;
+  const int n = which == 0 ? p.nsend : p.nrecv;
+  if (i < 0 || i >= n) return -1;
+  out4[0] = m[i].dir; out4[1] = m[i].peer; out4[2] = m[i].offset; out4[3] = gs::box_cells(m[i].box);
+  return 0;
+}
+
+int64_t gs_geom_total_elems(const gs::Geom* g) { return gs::total_elems(*g); }
+
+void gs_make_geom(gs::Geom* out, int nx, int ny, int nz, int H, int64_t ox, int64_t oy,
+                  int64_t oz, int64_t Lx, int64_t Ly, int64_t Lz, int periodic) {
+  *out = gs::make_geom(nx, ny, nz, H, ox, oy, oz, Lx, Ly, Lz, periodic);
+}
+
+void gs_noise_block(int64_t gx, int64_t gy, int64_t gz4, int64_t Lx, int64_t Ly, uint64_t step,
+                    uint64_t seed, uint32_t* out4) {
+  gs::U4 r = gs::noise_block(gx, gy, gz4, Lx, Ly, step, seed);
+  out4[0] = r.x; out4[1] = r.y; out4[2] = r.z; out4[3] = r.w;
+}
+
+int gs_plan_sizes(const gs::Geom* g, const int32_t* nbr27, int32_t diagonals, int64_t* sc,
+                  int64_t* rc) {
+  gs::HaloPlan p = gs::make_halo_plan(*g, nbr27, diagonals != 0);
+  *sc = p.send_cells;
+  *rc = p.recv_cells;
+  return 0;
+}
+
+}  // extern "C"

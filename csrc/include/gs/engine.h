@@ -1,0 +1,186 @@
+// SPDX-License-Identifier: MIT
+// Backend-independent time-stepping scheduler (the native runtime around the kernels).
+//
+// Reference call stack being replaced: public.jl:45 iterate! ->
+// exchange! (communication.jl:138-199, host-staged blocking Sendrecv) -> calculate! ->
+// swap (public.jl:67-68).  Here one "pass" fuses up to H steps per halo exchange:
+//   pack -> transport (RCCL / callback / self-copy) -> unpack -> k steps -> swap.
+// The outer-boundary ghost values of each buffer are kept at the parity the reference's
+// init + swap pattern implies by `ensure_bc`, so the stencil kernels never
+// need per-cell boundary predicates on level-0 data.
+#pragma once
+
+#include <stdint.h>
+#include <string.h>
+#include <stdexcept>
+#include <string>
+
+#include "gs/common.h"
+
+namespace gs {
+
+enum DType : int32_t { kF32 = 0, kF64 = 1 };
+
+// Transport callback: exchange the packed send buffer into the receive buffer.
+// Returns 0 on success.
+typedef int (*TransportFn)(void* user);
+
+class Backend {
+ public:
+  virtual ~Backend() {}
+  // fill box of buffer b with a constant (u,v) pair
+  virtual void fill_box(int b, const Box& box, double u, double v) = 0;
+  // one explicit Euler step over `region`, reading buffer src at time t, writing dst
+  virtual void step(int src, int dst, const Box& region, int64_t t) = 0;
+  // temporally blocked kernel: n steps over the interior, src at time t -> dst at t+n.
+  // Returns false if unsupported for this n (the scheduler then falls back to step()).
+  virtual bool fused(int src, int dst, int n, int64_t t) { (void)src; (void)dst; (void)n; (void)t; return false; }
+  virtual void pack(int b, const HaloPlan& p) = 0;
+  virtual void unpack(int b, const HaloPlan& p) = 0;
+  // copy send-buffer cells [src_off, +n) to recv-buffer cells [dst_off, +n)
+  virtual void self_copy(int64_t src_off, int64_t dst_off, int64_t n) = 0;
+  // native transport (RCCL); returns false if not configured
+  virtual bool native_exchange(const HaloPlan& p) { (void)p; return false; }
+  virtual void host_sync() {}
+  virtual void extract(int b, void* u, void* v) = 0;
+  virtual void insert(int b, const void* u, const void* v) = 0;
+  // seed cube into buffer b
+  virtual void seed(int b) = 0;
+  // sum / min / max of u and v over the interior: out[6]
+  virtual void stats(int b, double* out) = 0;
+};
+
+struct EngineConfig {
+  Geom g;
+  Params p;
+  int32_t nbr[27];
+  int32_t rank;
+  int32_t fuse;        // max steps per halo exchange (<= g.H)
+  int32_t use_fused;   // allow the temporally-blocked kernel
+};
+
+class Engine {
+ public:
+  Engine(const EngineConfig& c, Backend* be) : cfg_(c), be_(be) {
+    if (c.fuse < 1 || c.fuse > c.g.H) throw std::runtime_error("fuse must be in [1, H]");
+    int nb = 0;
+    for (int d = 0; d < 27; ++d) if (d != 13 && c.nbr[d] >= 0) ++nb;
+    has_nbr_ = nb > 0;
+    plan_ = make_halo_plan(c.g, c.nbr, c.g.H > 1 || c.fuse > 1);
+    bc_parity_[0] = bc_parity_[1] = -1;
+  }
+  ~Engine() { delete be_; }
+
+  const HaloPlan& plan() const { return plan_; }
+  Backend* backend() { return be_; }
+  int cur() const { return cur_; }
+  int64_t step() const { return t_; }
+  void set_step(int64_t t) { t_ = t; bc_parity_[0] = bc_parity_[1] = -1; }
+  void set_transport(TransportFn fn, void* user) { tfn_ = fn; tuser_ = user; }
+  double comm_calls() const { return (double)ncomm_; }
+
+  // Reference init (Simulation_CPU.jl:14-65): u = 1 everywhere (ghosts included), v = 0,
+  // u_temp = v_temp = 0, then the 13^3 seed cube.
+  void init_fields() {
+    const Geom& g = cfg_.g;
+    Box all{-g.H, -g.H, -g.H, g.nx + 2 * g.H, g.ny + 2 * g.H, g.nz + 2 * g.H};
+    be_->fill_box(0, all, 1.0, 0.0);
+    be_->fill_box(1, all, 0.0, 0.0);
+    be_->seed(0);
+    cur_ = 0;
+    t_ = 0;
+    bc_parity_[0] = 0;  // u ghosts = 1 -> even time
+    bc_parity_[1] = 1;  // u_temp ghosts = 0 -> odd time
+  }
+
+  void exchange() {
+    if (!has_nbr_) return;
+    be_->pack(cur_, plan_);
+    // self messages (periodic wrap onto the same rank)
+    bool remote = false;
+    for (int i = 0; i < plan_.nrecv; ++i) {
+      const HaloMsg& r = plan_.recv[i];
+      if (r.peer == cfg_.rank) {
+        const int sd = 26 - r.dir;  // my send towards -d lands in my ghost d
+        for (int j = 0; j < plan_.nsend; ++j)
+          if (plan_.send[j].dir == sd && plan_.send[j].peer == cfg_.rank)
+            be_->self_copy(plan_.send[j].offset, r.offset, box_cells(r.box));
+      } else {
+        remote = true;
+      }
+    }
+    if (remote) {
+      ++ncomm_;
+      if (!be_->native_exchange(plan_)) {
+        if (!tfn_) throw std::runtime_error("halo exchange needs a transport (RCCL or callback)");
+        be_->host_sync();
+        if (tfn_(tuser_) != 0) throw std::runtime_error("transport callback failed");
+      }
+    }
+    be_->unpack(cur_, plan_);
+  }
+
+  // Fill the outer (global-boundary) ghost shells of buffer b with the boundary value of
+  // time t.  Faces cover the full ghost-extended range so edges/corners are covered too.
+  void ensure_bc(int b, int64_t t) {
+    const Geom& g = cfg_.g;
+    if (g.periodic) return;
+    const int par = (int)(t & 1);
+    if (bc_parity_[b] == par) return;
+    const double u = bc_u(t);
+    const int H = g.H;
+    for (int a = 0; a < 3; ++a)
+      for (int s = -1; s <= 1; s += 2) {
+        int dd[3] = {0, 0, 0};
+        dd[a] = s;
+        if (cfg_.nbr[dir_index(dd[0], dd[1], dd[2])] >= 0) continue;
+        Box bx{-H, -H, -H, g.nx + 2 * H, g.ny + 2 * H, g.nz + 2 * H};
+        int32_t* o = a == 0 ? &bx.x0 : (a == 1 ? &bx.y0 : &bx.z0);
+        int32_t* c = a == 0 ? &bx.nx : (a == 1 ? &bx.ny : &bx.nz);
+        const int n = a == 0 ? g.nx : (a == 1 ? g.ny : g.nz);
+        *o = s < 0 ? -H : n;
+        *c = H;
+        be_->fill_box(b, bx, u, 0.0);
+      }
+    bc_parity_[b] = par;
+  }
+
+  void advance(int64_t nsteps) {
+    while (nsteps > 0) {
+      const int k = (int)(nsteps < cfg_.fuse ? nsteps : cfg_.fuse);
+      exchange();
+      const int oth = 1 - cur_;
+      if (k > 1 && cfg_.use_fused) {
+        ensure_bc(cur_, t_);
+        if (be_->fused(cur_, oth, k, t_)) {
+          cur_ = oth;
+          t_ += k;
+          nsteps -= k;
+          continue;
+        }
+      }
+      for (int s = 0; s < k; ++s) {
+        ensure_bc(cur_, t_);
+        const Box r = pass_region(cfg_.g, cfg_.nbr, k, s);
+        be_->step(cur_, 1 - cur_, r, t_);
+        cur_ = 1 - cur_;
+        ++t_;
+      }
+      nsteps -= k;
+    }
+  }
+
+ private:
+  EngineConfig cfg_;
+  Backend* be_;
+  HaloPlan plan_;
+  bool has_nbr_ = false;
+  int cur_ = 0;
+  int64_t t_ = 0;
+  int bc_parity_[2];
+  TransportFn tfn_ = nullptr;
+  void* tuser_ = nullptr;
+  int64_t ncomm_ = 0;
+};
+
+}  // namespace gs

@@ -1,0 +1,185 @@
+"""The Gray-Scott model: fields + native engine for one rank.
+
+Reference façade being replaced:
+  * ``init_fields(settings, mcd, T)``      -- public.jl:18-25 and the per-backend inits
+                                              (Simulation_CPU.jl:14-65, ext/*Ext.jl populate!)
+  * ``iterate!(fields, settings, mcd)``    -- public.jl:45-71 (exchange! -> calculate! -> swap)
+  * ``get_fields(backend, fields)``        -- Simulation_CPU.jl:125-133, ext/CUDAExt.jl:199-209
+  * ``Fields{T,N,A}``                      -- Structs.jl:82-93
+
+Fields live in one interleaved (u, v) buffer pair per rank, allocated as torch tensors (device
+memory on MI355X, host memory for the CPU backend) and updated in place by the native engine.
+"""
+from __future__ import annotations
+
+import math
+import os
+from dataclasses import dataclass
+from typing import Optional, Tuple
+
+import numpy as np
+import torch
+
+from ..ops import native
+from ..parallel.decomp import CartDomain
+from ..parallel.dist import DistContext
+from ..parallel.halo import TorchTransport
+from ..utils.config import Settings, load_backend_and_lang, parse_precision
+
+_TORCH_DTYPES = {"float32": torch.float32, "float64": torch.float64}
+_NP_DTYPES = {"float32": np.float32, "float64": np.float64}
+
+
+def default_fuse(backend: str, domain: CartDomain) -> int:
+    """Steps fused per halo exchange when ``fuse_steps = 0`` (auto)."""
+    if backend != "hip":
+        return 1
+    # The temporally blocked kernel halves HBM traffic per step; a deeper halo also halves
+    # the number of RCCL round trips.  Limited by the smallest local extent.
+    return max(1, min(2, min(domain.proc_sizes)))
+
+
+class GrayScott:
+    """One rank's Gray-Scott state and stepping engine."""
+
+    def __init__(self, settings: Settings, domain: CartDomain, ctx: Optional[DistContext] = None,
+                 fuse: Optional[int] = None, transport: Optional[str] = None,
+                 use_fused: bool = True):
+        self.settings = settings
+        self.domain = domain
+        self.ctx = ctx or DistContext()
+        self.backend, self.kernel_language = load_backend_and_lang(settings)
+        self.dtype = parse_precision(settings.precision)
+        if self.backend == "hip":
+            if not torch.cuda.is_available():
+                raise RuntimeError("backend requests the MI355X HIP path but no GPU is visible")
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        else:
+            self.device = torch.device("cpu")
+        if fuse is None or fuse <= 0:
+            fuse = settings.fuse_steps if settings.fuse_steps > 0 else default_fuse(self.backend, domain)
+        fuse = int(max(1, min(fuse, min(domain.proc_sizes))))
+        self.fuse = fuse
+        self.H = fuse
+        nx, ny, nz = domain.proc_sizes
+        ox, oy, oz = domain.proc_offsets
+        Lx, Ly, Lz = domain.L
+        self.geom = native.make_geom(nx, ny, nz, self.H, ox, oy, oz, Lx, Ly, Lz, domain.periodic)
+        n = native.total_elems(self.geom)
+        tdt = _TORCH_DTYPES[self.dtype]
+        self.buffers = [torch.empty(2 * n, dtype=tdt, device=self.device) for _ in range(2)]
+        scells, rcells = native.plan_sizes(self.geom, domain.nbr27, self.H > 1)
+        self.sendbuf = torch.empty(max(2 * scells, 2), dtype=tdt, device=self.device)
+        self.recvbuf = torch.empty(max(2 * rcells, 2), dtype=tdt, device=self.device)
+        stream = torch.cuda.current_stream(self.device).cuda_stream if self.backend == "hip" else 0
+        p = native.Params()
+        p.F, p.k, p.dt = settings.F, settings.k, settings.dt
+        p.Du, p.Dv, p.noise = settings.Du, settings.Dv, settings.noise
+        p.seed = int(settings.seed) & 0xFFFFFFFFFFFFFFFF
+        self.params = p
+        self.engine = native.Engine(self.backend, self.dtype, self.geom, p, domain.nbr27,
+                                    domain.rank, fuse, use_fused, self.buffers[0].data_ptr(),
+                                    self.buffers[1].data_ptr(), self.sendbuf.data_ptr(),
+                                    self.recvbuf.data_ptr(), stream)
+        self.transport = "none"
+        if domain.has_neighbors and any(r != domain.rank for i, r in enumerate(domain.nbr27)
+                                        if i != 13 and r >= 0):
+            self._setup_transport(transport or settings.transport)
+
+    # ------------------------------------------------------------------------------------
+    def _setup_transport(self, kind: str) -> None:
+        kind = (kind or "auto").lower()
+        if kind == "auto":
+            kind = "rccl" if self.backend == "hip" else "torch"
+        if kind == "rccl":
+            if self.backend != "hip":
+                raise ValueError("the rccl transport needs backend = AMDGPU/HIP")
+            uid = native.rccl_unique_id() if self.ctx.rank == 0 else None
+            uid = self.ctx.broadcast_object(uid, src=0)
+            self.engine.rccl_init(uid, self.ctx.world_size, self.ctx.rank)
+        elif kind == "torch":
+            group = self.ctx.nccl_group() if self.backend == "hip" else None
+            self._torch_transport = TorchTransport(self.engine.plan(), self.sendbuf, self.recvbuf,
+                                                   self.domain.rank, group)
+            self.engine.set_transport(self._torch_transport)
+        else:
+            raise ValueError(f"unknown transport {kind!r}")
+        self.transport = kind
+
+    # ------------------------------------------------------------------------------------
+    def init_fields(self) -> None:
+        self.engine.init_fields()
+
+    def iterate(self, nsteps: int = 1) -> None:
+        """Advance ``nsteps`` steps (each = exchange! + calculate! + swap in the reference)."""
+        if nsteps > 0:
+            self.engine.advance(nsteps)
+
+    @property
+    def step(self) -> int:
+        return self.engine.step
+
+    def set_step(self, t: int) -> None:
+        self.engine.set_step(t)
+
+    def synchronize(self) -> None:
+        self.engine.sync()
+
+    def exchange(self) -> None:
+        self.engine.exchange()
+
+    # ------------------------------------------------------------------------------------
+    @property
+    def local_shape(self) -> Tuple[int, int, int]:
+        """(nz, ny, nx): C-order shape of ghost-free local arrays (= Julia (x,y,z) column-major)."""
+        nx, ny, nz = self.domain.proc_sizes
+        return (nz, ny, nx)
+
+    def get_fields_device(self) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Ghost-stripped copies of u, v on the field device (interior compaction kernel)."""
+        tdt = _TORCH_DTYPES[self.dtype]
+        u = torch.empty(self.local_shape, dtype=tdt, device=self.device)
+        v = torch.empty(self.local_shape, dtype=tdt, device=self.device)
+        self.engine.extract(u.data_ptr(), v.data_ptr())
+        return u, v
+
+    def get_fields(self) -> Tuple[np.ndarray, np.ndarray]:
+        """Ghost-stripped host copies of u, v as (nz, ny, nx) numpy arrays."""
+        u, v = self.get_fields_device()
+        if self.backend == "hip":
+            return u.cpu().numpy(), v.cpu().numpy()
+        return u.numpy(), v.numpy()
+
+    def set_fields(self, u, v) -> None:
+        """Overwrite the interior of the current state (restart)."""
+        tdt = _TORCH_DTYPES[self.dtype]
+        tu = torch.as_tensor(np.ascontiguousarray(u)).to(device=self.device, dtype=tdt).contiguous()
+        tv = torch.as_tensor(np.ascontiguousarray(v)).to(device=self.device, dtype=tdt).contiguous()
+        if tuple(tu.shape) != self.local_shape or tuple(tv.shape) != self.local_shape:
+            raise ValueError(f"expected local arrays of shape {self.local_shape}")
+        self.engine.insert(tu.data_ptr(), tv.data_ptr())
+        self.engine.sync()
+
+    def full_state(self, which: Optional[int] = None) -> torch.Tensor:
+        """View of a raw state buffer as (pz, py, px, 2) including ghosts and padding."""
+        g = self.geom
+        b = self.buffers[self.engine.current if which is None else which]
+        return b.view(g.pz, g.py, g.px, 2)
+
+    def stats(self):
+        """Local [sum_u, min_u, max_u, sum_v, min_v, max_v]."""
+        return self.engine.stats()
+
+    def global_stats(self):
+        s = self.stats()
+        tot = self.ctx.allreduce_array([s[0], s[3]], "sum")
+        mn = self.ctx.allreduce_array([s[1], s[4]], "min")
+        mx = self.ctx.allreduce_array([s[2], s[5]], "max")
+        n = float(np.prod(self.domain.L))
+        return {"mean_u": tot[0] / n, "min_u": mn[0], "max_u": mx[0],
+                "mean_v": tot[1] / n, "min_v": mn[1], "max_v": mx[1]}
+
+    def close(self) -> None:
+        if getattr(self, "engine", None) is not None:
+            self.engine.close()
+            self.engine = None

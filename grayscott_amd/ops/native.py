@@ -1,0 +1,266 @@
+"""ctypes bindings to the native libraries built from ``csrc/``.
+
+* ``libgs_core.so`` -- CPU/OpenMP backend (golden model) + shared scheduler
+* ``libgs_hip.so``  -- gfx950 HIP kernels + RCCL halo transport + the same scheduler
+
+Both export the C ABI of ``csrc/include/gs/capi.h``.  There is deliberately no silent
+fallback: asking for the HIP backend when ``libgs_hip.so`` is missing raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from ctypes import (CFUNCTYPE, POINTER, Structure, c_char_p, c_double, c_int, c_int32, c_int64,
+                    c_uint32, c_uint64, c_void_p)
+from typing import Optional
+
+_LIB_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_lib")
+
+DTYPE_CODES = {"float32": 0, "float64": 1}
+
+
+class Geom(Structure):
+    _fields_ = [
+        ("nx", c_int32), ("ny", c_int32), ("nz", c_int32), ("H", c_int32),
+        ("xo", c_int32), ("px", c_int32), ("py", c_int32), ("pz", c_int32),
+        ("ox", c_int64), ("oy", c_int64), ("oz", c_int64),
+        ("Lx", c_int64), ("Ly", c_int64), ("Lz", c_int64),
+        ("periodic", c_int32), ("_pad", c_int32),
+    ]
+
+
+class Params(Structure):
+    _fields_ = [
+        ("F", c_double), ("k", c_double), ("dt", c_double), ("Du", c_double), ("Dv", c_double),
+        ("noise", c_double), ("seed", c_uint64),
+    ]
+
+
+TRANSPORT_FN = CFUNCTYPE(c_int, c_void_p)
+
+_libs = {}
+_lock = threading.Lock()
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+def lib_path(name: str) -> str:
+    return os.path.join(_LIB_DIR, f"libgs_{name}.so")
+
+
+def _declare(lib) -> None:
+    lib.gs_create.restype = c_void_p
+    lib.gs_create.argtypes = [c_int32, POINTER(Geom), POINTER(Params), POINTER(c_int32), c_int32,
+                              c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
+    lib.gs_destroy.argtypes = [c_void_p]
+    lib.gs_destroy.restype = None
+    lib.gs_last_error.restype = c_char_p
+    for name in ("gs_init_fields", "gs_exchange", "gs_current_buffer", "gs_sync"):
+        getattr(lib, name).argtypes = [c_void_p]
+        getattr(lib, name).restype = c_int
+    lib.gs_advance.argtypes = [c_void_p, c_int64]
+    lib.gs_advance.restype = c_int
+    lib.gs_get_step.argtypes = [c_void_p]
+    lib.gs_get_step.restype = c_int64
+    lib.gs_set_step.argtypes = [c_void_p, c_int64]
+    lib.gs_set_step.restype = c_int
+    lib.gs_extract.argtypes = [c_void_p, c_void_p, c_void_p]
+    lib.gs_extract.restype = c_int
+    lib.gs_insert.argtypes = [c_void_p, c_void_p, c_void_p]
+    lib.gs_insert.restype = c_int
+    lib.gs_stats.argtypes = [c_void_p, POINTER(c_double)]
+    lib.gs_stats.restype = c_int
+    lib.gs_set_transport.argtypes = [c_void_p, TRANSPORT_FN, c_void_p]
+    lib.gs_set_transport.restype = c_int
+    lib.gs_plan_info.argtypes = [c_void_p, POINTER(c_int64), POINTER(c_int64), POINTER(c_int32),
+                                 POINTER(c_int32)]
+    lib.gs_plan_info.restype = c_int
+    lib.gs_plan_msg.argtypes = [c_void_p, c_int32, c_int32, POINTER(c_int64)]
+    lib.gs_plan_msg.restype = c_int
+    lib.gs_geom_total_elems.argtypes = [POINTER(Geom)]
+    lib.gs_geom_total_elems.restype = c_int64
+    lib.gs_make_geom.argtypes = [POINTER(Geom), c_int, c_int, c_int, c_int, c_int64, c_int64,
+                                 c_int64, c_int64, c_int64, c_int64, c_int]
+    lib.gs_make_geom.restype = None
+    lib.gs_noise_block.argtypes = [c_int64, c_int64, c_int64, c_int64, c_int64, c_uint64, c_uint64,
+                                   POINTER(c_uint32)]
+    lib.gs_noise_block.restype = None
+    lib.gs_plan_sizes.argtypes = [POINTER(Geom), POINTER(c_int32), c_int32, POINTER(c_int64),
+                                  POINTER(c_int64)]
+    lib.gs_plan_sizes.restype = c_int
+    if hasattr(lib, "gs_rccl_unique_id"):
+        lib.gs_rccl_unique_id.argtypes = [ctypes.c_char_p, c_int32]
+        lib.gs_rccl_unique_id.restype = c_int
+        lib.gs_rccl_init.argtypes = [c_void_p, ctypes.c_char_p, c_int32, c_int32, c_int32]
+        lib.gs_rccl_init.restype = c_int
+    if hasattr(lib, "gs_bp_version"):
+        pass
+
+
+def load(name: str):
+    """Load ``libgs_<name>.so`` ("core" or "hip"); raise if it was not built."""
+    with _lock:
+        if name in _libs:
+            return _libs[name]
+        path = lib_path(name)
+        if not os.path.exists(path):
+            raise NativeLibraryMissing(
+                f"{path} not found: build the native libraries first (`make` or "
+                f"`python -c 'import __graft_entry__ as g; g.build()'`)")
+        lib = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
+        _declare(lib)
+        _libs[name] = lib
+        return lib
+
+
+def last_error(lib) -> str:
+    msg = lib.gs_last_error()
+    return msg.decode() if msg else "unknown error"
+
+
+def check(lib, rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{what} failed: {last_error(lib)}")
+
+
+def make_geom(nx, ny, nz, H, ox, oy, oz, Lx, Ly, Lz, periodic) -> Geom:
+    g = Geom()
+    load("core").gs_make_geom(ctypes.byref(g), nx, ny, nz, H, ox, oy, oz, Lx, Ly, Lz,
+                              1 if periodic else 0)
+    return g
+
+
+def total_elems(g: Geom) -> int:
+    return int(load("core").gs_geom_total_elems(ctypes.byref(g)))
+
+
+def plan_sizes(g: Geom, nbr27, diagonals: bool):
+    arr = (c_int32 * 27)(*nbr27)
+    s, r = c_int64(), c_int64()
+    load("core").gs_plan_sizes(ctypes.byref(g), arr, 1 if diagonals else 0, ctypes.byref(s),
+                               ctypes.byref(r))
+    return int(s.value), int(r.value)
+
+
+def noise_block(gx, gy, gz4, Lx, Ly, step, seed):
+    out = (c_uint32 * 4)()
+    load("core").gs_noise_block(gx, gy, gz4, Lx, Ly, step, seed, out)
+    return [int(v) for v in out]
+
+
+class Engine:
+    """Thin owner of a native ``gs_engine`` handle."""
+
+    def __init__(self, backend: str, dtype: str, geom: Geom, params: Params, nbr27, rank: int,
+                 fuse: int, use_fused: bool, buf0: int, buf1: int, send: int, recv: int,
+                 stream: int = 0):
+        self.lib = load("hip" if backend == "hip" else "core")
+        self.backend = backend
+        self.dtype = dtype
+        self._nbr = (c_int32 * 27)(*nbr27)
+        self._geom = geom
+        self._params = params
+        h = self.lib.gs_create(DTYPE_CODES[dtype], ctypes.byref(geom), ctypes.byref(params),
+                               self._nbr, rank, fuse, 1 if use_fused else 0, c_void_p(buf0),
+                               c_void_p(buf1), c_void_p(send or None), c_void_p(recv or None),
+                               c_void_p(stream or None))
+        if not h:
+            raise RuntimeError(f"gs_create failed: {last_error(self.lib)}")
+        self.h = c_void_p(h)
+        self._cb = None
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.gs_destroy(self.h)
+            self.h = None
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown order
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, rc, what):
+        check(self.lib, rc, what)
+
+    def init_fields(self):
+        self._chk(self.lib.gs_init_fields(self.h), "init_fields")
+
+    def advance(self, n: int):
+        self._chk(self.lib.gs_advance(self.h, int(n)), "advance")
+
+    def exchange(self):
+        self._chk(self.lib.gs_exchange(self.h), "exchange")
+
+    @property
+    def step(self) -> int:
+        return int(self.lib.gs_get_step(self.h))
+
+    def set_step(self, t: int):
+        self._chk(self.lib.gs_set_step(self.h, int(t)), "set_step")
+
+    @property
+    def current(self) -> int:
+        return int(self.lib.gs_current_buffer(self.h))
+
+    def sync(self):
+        self._chk(self.lib.gs_sync(self.h), "sync")
+
+    def extract(self, u_ptr: int, v_ptr: int):
+        self._chk(self.lib.gs_extract(self.h, c_void_p(u_ptr or None), c_void_p(v_ptr or None)),
+                  "extract")
+
+    def insert(self, u_ptr: int, v_ptr: int):
+        self._chk(self.lib.gs_insert(self.h, c_void_p(u_ptr), c_void_p(v_ptr)), "insert")
+
+    def stats(self):
+        out = (c_double * 6)()
+        self._chk(self.lib.gs_stats(self.h, out), "stats")
+        return list(out)
+
+    def set_transport(self, fn):
+        """``fn()`` -> None; exchanges send buffer into receive buffer (exceptions -> failure)."""
+
+        def _tramp(_user):
+            try:
+                fn()
+                return 0
+            except Exception as ex:  # pragma: no cover - surfaced through last_error
+                import traceback
+                traceback.print_exc()
+                return 1
+
+        self._cb = TRANSPORT_FN(_tramp)
+        self._chk(self.lib.gs_set_transport(self.h, self._cb, None), "set_transport")
+
+    def plan(self):
+        sc, rc = c_int64(), c_int64()
+        ns, nr = c_int32(), c_int32()
+        self.lib.gs_plan_info(self.h, ctypes.byref(sc), ctypes.byref(rc), ctypes.byref(ns),
+                              ctypes.byref(nr))
+        out = {"send_cells": sc.value, "recv_cells": rc.value, "send": [], "recv": []}
+        buf = (c_int64 * 4)()
+        for which, key, n in ((0, "send", ns.value), (1, "recv", nr.value)):
+            for i in range(n):
+                self.lib.gs_plan_msg(self.h, which, i, buf)
+                out[key].append({"dir": int(buf[0]), "peer": int(buf[1]), "offset": int(buf[2]),
+                                 "cells": int(buf[3])})
+        return out
+
+    def rccl_init(self, uid: bytes, nranks: int, rank: int):
+        if not hasattr(self.lib, "gs_rccl_init"):
+            raise RuntimeError("RCCL transport needs the HIP backend")
+        self._chk(self.lib.gs_rccl_init(self.h, uid, nranks, rank, DTYPE_CODES[self.dtype]),
+                  "rccl_init")
+
+
+def rccl_unique_id() -> bytes:
+    lib = load("hip")
+    buf = ctypes.create_string_buffer(256)
+    n = lib.gs_rccl_unique_id(buf, 256)
+    if n < 0:
+        raise RuntimeError(f"ncclGetUniqueId failed: {last_error(lib)}")
+    return buf.raw[:n]

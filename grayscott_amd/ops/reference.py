@@ -1,0 +1,145 @@
+"""Independent pure-Python (numpy + PyTorch) golden model.
+
+Used only as a test oracle: the native CPU backend and the gfx950 kernels are checked against
+it.  It re-implements, without sharing code with ``csrc/``:
+  * the Philox4x32-10 noise stream (rocrand_philox4x32_10.h semantics, counter mode)
+  * the reference initial condition (Simulation_CPU.jl:14-65)
+  * one explicit Euler step of the Gray-Scott system (Simulation_CPU.jl:77-113, Common.jl:13-18)
+  * the reference boundary behaviour: outer u ghost = 1 at even t, 0 at odd t.
+Arrays are C-ordered (z, y, x), i.e. the same memory order as the Julia (x, y, z) arrays.
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+
+M0 = np.uint64(0xD2511F53)
+M1 = np.uint64(0xCD9E8D57)
+W0 = 0x9E3779B9
+W1 = 0xBB67AE85
+MASK32 = np.uint64(0xFFFFFFFF)
+
+
+def philox4x32_10(c0, c1, c2, c3, seed: int):
+    """Vectorised Philox4x32-10 on uint32 counters; returns 4 uint32 arrays."""
+    c0 = np.asarray(c0, dtype=np.uint64) & MASK32
+    c1 = np.asarray(c1, dtype=np.uint64) & MASK32
+    c2 = np.asarray(c2, dtype=np.uint64) & MASK32
+    c3 = np.asarray(c3, dtype=np.uint64) & MASK32
+    k0 = seed & 0xFFFFFFFF
+    k1 = (seed >> 32) & 0xFFFFFFFF
+    for _ in range(10):
+        p0 = M0 * c0
+        p1 = M1 * c2
+        hi0, lo0 = p0 >> np.uint64(32), p0 & MASK32
+        hi1, lo1 = p1 >> np.uint64(32), p1 & MASK32
+        n0 = hi1 ^ c1 ^ np.uint64(k0)
+        n2 = hi0 ^ c3 ^ np.uint64(k1)
+        c0, c1, c2, c3 = n0, lo1, n2, lo0
+        k0 = (k0 + W0) & 0xFFFFFFFF
+        k1 = (k1 + W1) & 0xFFFFFFFF
+    return (c0.astype(np.uint32), c1.astype(np.uint32), c2.astype(np.uint32), c3.astype(np.uint32))
+
+
+def noise(L: Sequence[int], offsets: Sequence[int], sizes: Sequence[int], step: int,
+          seed: int, dtype=np.float64) -> np.ndarray:
+    """Uniform[-1,1) draws for the cells of a sub-domain at ``step`` -> (nz, ny, nx)."""
+    Lx, Ly, _ = (int(v) for v in L)
+    nx, ny, nz = (int(v) for v in sizes)
+    gx = np.arange(offsets[0], offsets[0] + nx, dtype=np.uint64)
+    gy = np.arange(offsets[1], offsets[1] + ny, dtype=np.uint64)
+    gz = np.arange(offsets[2], offsets[2] + nz, dtype=np.uint64)
+    Z, Y, X = np.meshgrid(gz, gy, gx, indexing="ij")
+    q = X + np.uint64(Lx) * (Y + np.uint64(Ly) * (Z >> np.uint64(2)))
+    st = np.uint64(step)
+    r = philox4x32_10(q & MASK32, q >> np.uint64(32), st & MASK32, st >> np.uint64(32), seed)
+    sel = (Z & np.uint64(3)).astype(np.int64)
+    words = np.choose(sel, r)
+    dt = np.dtype(dtype).type
+    return words.view(np.int32).astype(dt) * dt(2.0 ** -31)
+
+
+def init_fields(L: Sequence[int], offsets=(0, 0, 0), sizes=None, dtype=np.float64):
+    """Interior of u, v after the reference init (13^3 seed cube at L/2 +- 6)."""
+    L = [int(v) for v in L]
+    sizes = list(sizes) if sizes is not None else list(L)
+    u = np.ones((sizes[2], sizes[1], sizes[0]), dtype=dtype)
+    v = np.zeros_like(u)
+    sl = []
+    for a in (2, 1, 0):
+        lo = max(L[a] // 2 - 6, offsets[a]) - offsets[a]
+        hi = min(L[a] // 2 + 7, offsets[a] + sizes[a]) - offsets[a]
+        sl.append(slice(max(lo, 0), max(hi, 0)))
+    u[tuple(sl)] = 0.25
+    v[tuple(sl)] = 0.33
+    return u, v
+
+
+def bc_u(t: int) -> float:
+    return 0.0 if (t & 1) else 1.0
+
+
+def step(u: np.ndarray, v: np.ndarray, t: int, F: float, k: float, dt: float, Du: float,
+         Dv: float, noise_amp: float, seed: int, periodic: bool = False, backend: str = "numpy"):
+    """One global step (single rank, whole domain) of the reference update at time ``t``."""
+    L = (u.shape[2], u.shape[1], u.shape[0])
+    if backend == "torch":
+        return _step_torch(u, v, t, F, k, dt, Du, Dv, noise_amp, seed, periodic, L)
+    dtype = u.dtype.type
+    if periodic:
+        up = np.pad(u, 1, mode="wrap")
+        vp = np.pad(v, 1, mode="wrap")
+    else:
+        up = np.pad(u, 1, mode="constant", constant_values=bc_u(t))
+        vp = np.pad(v, 1, mode="constant", constant_values=0.0)
+
+    def nsum(a):
+        return (a[1:-1, 1:-1, :-2] + a[1:-1, 1:-1, 2:]) + (a[1:-1, :-2, 1:-1] + a[1:-1, 2:, 1:-1]) + \
+            (a[:-2, 1:-1, 1:-1] + a[2:, 1:-1, 1:-1])
+
+    su, sv = nsum(up), nsum(vp)
+    r = noise(L, (0, 0, 0), L, t, seed, dtype=u.dtype) if noise_amp != 0 else 0.0
+    uvv = u * v * v
+    du = dtype(Du / 6.0) * su - dtype(Du) * u - uvv + dtype(F) * (dtype(1) - u) + dtype(noise_amp) * r
+    dv = dtype(Dv / 6.0) * sv - dtype(Dv) * v + uvv - dtype(F + k) * v
+    return (u + du * dtype(dt)).astype(u.dtype), (v + dv * dtype(dt)).astype(v.dtype)
+
+
+def _step_torch(u, v, t, F, k, dt, Du, Dv, noise_amp, seed, periodic, L):
+    """Same update with a torch conv3d Laplacian (the "plain PyTorch reference")."""
+    import torch
+    import torch.nn.functional as Fn
+
+    tu = torch.as_tensor(u)
+    tv = torch.as_tensor(v)
+    dtype = tu.dtype
+    kern = torch.zeros((1, 1, 3, 3, 3), dtype=dtype, device=tu.device)
+    for (a, b, c) in ((0, 1, 1), (2, 1, 1), (1, 0, 1), (1, 2, 1), (1, 1, 0), (1, 1, 2)):
+        kern[0, 0, a, b, c] = 1.0
+    if periodic:
+        pu = Fn.pad(tu[None, None], (1, 1, 1, 1, 1, 1), mode="circular")
+        pv = Fn.pad(tv[None, None], (1, 1, 1, 1, 1, 1), mode="circular")
+    else:
+        pu = Fn.pad(tu[None, None], (1, 1, 1, 1, 1, 1), mode="constant", value=bc_u(t))
+        pv = Fn.pad(tv[None, None], (1, 1, 1, 1, 1, 1), mode="constant", value=0.0)
+    su = Fn.conv3d(pu, kern)[0, 0]
+    sv = Fn.conv3d(pv, kern)[0, 0]
+    if noise_amp != 0:
+        r = torch.as_tensor(noise(L, (0, 0, 0), L, t, seed, dtype=np.float64)).to(dtype)
+    else:
+        r = torch.zeros_like(tu)
+    uvv = tu * tv * tv
+    du = (Du / 6.0) * su - Du * tu - uvv + F * (1 - tu) + noise_amp * r
+    dv = (Dv / 6.0) * sv - Dv * tv + uvv - (F + k) * tv
+    return (tu + du * dt).numpy(), (tv + dv * dt).numpy()
+
+
+def run(L, nsteps: int, F=0.02, k=0.048, dt=1.0, Du=0.2, Dv=0.1, noise_amp=0.0, seed=0,
+        periodic=False, dtype=np.float64, backend="numpy"):
+    if isinstance(L, int):
+        L = (L, L, L)
+    u, v = init_fields(L, dtype=dtype)
+    for t in range(nsteps):
+        u, v = step(u, v, t, F, k, dt, Du, Dv, noise_amp, seed, periodic, backend)
+    return u, v

@@ -1,0 +1,166 @@
+"""3D Cartesian domain decomposition (one rank per MI355X).
+
+Parity with the reference ``init_domain`` (src/simulation/communication.jl:59-96):
+  * ``dims_create``    -- MPI.Dims_create(nprocs, [0,0,0]) (:64): balanced, non-increasing
+  * rank <-> coords    -- MPI.Cart_create / Cart_coords, row-major, no reorder (:65-69)
+  * sizes / offsets    -- L/dims plus one extra cell on the low coords absorbing L % dims
+                          (:73-87).  The reference only works for divisible L (defect D5);
+                          the remainder distribution here is the intended one.
+  * neighbours         -- Cart_shift on each axis (:90-92), non-periodic -> -1 (PROC_NULL)
+                          west/east = -/+x, down/up = -/+y, south/north = -/+z.
+
+Extension: ``periodic=True`` wraps the topology (the ADIOS2-Examples C++ behaviour), and the
+26-neighbour table (faces + edges + corners) used by multi-step halo exchanges.
+"""
+from __future__ import annotations
+
+import itertools
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+NEIGHBOR_NAMES = {
+    "west": (-1, 0, 0), "east": (1, 0, 0),
+    "down": (0, -1, 0), "up": (0, 1, 0),
+    "south": (0, 0, -1), "north": (0, 0, 1),
+}
+
+
+def _factor_triples(n: int):
+    for a in range(1, n + 1):
+        if n % a:
+            continue
+        m = n // a
+        for b in range(1, m + 1):
+            if m % b:
+                continue
+            yield (a, b, m // b)
+
+
+def dims_create(nnodes: int, dims: Optional[Sequence[int]] = None) -> List[int]:
+    """Equivalent of ``MPI_Dims_create`` for 3 dimensions.
+
+    Non-zero entries of ``dims`` are kept fixed; the free entries are filled with the most
+    balanced factorisation (smallest max/min spread), in non-increasing order.
+    """
+    if nnodes < 1:
+        raise ValueError("nnodes must be >= 1")
+    dims = list(dims) if dims is not None else [0, 0, 0]
+    if len(dims) != 3:
+        raise ValueError("only 3D decompositions are supported")
+    fixed = 1
+    free_idx = []
+    for i, d in enumerate(dims):
+        if d < 0:
+            raise ValueError("dims entries must be >= 0")
+        if d > 0:
+            fixed *= d
+        else:
+            free_idx.append(i)
+    if nnodes % fixed:
+        raise ValueError(f"cannot decompose {nnodes} with fixed dims {dims}")
+    rest = nnodes // fixed
+    k = len(free_idx)
+    if k == 0:
+        if rest != 1:
+            raise ValueError(f"dims {dims} do not multiply to {nnodes}")
+        return dims
+    best = None
+    for t in _factor_triples(rest):
+        cand = tuple(sorted([t[0], t[1], t[2]], reverse=True))
+        if k < 3:
+            # only k free slots: the remaining factors must be 1
+            if any(c != 1 for c in cand[k:]):
+                continue
+            cand = cand[:k]
+        key = (max(cand) - min(cand), cand)
+        if best is None or key < best[0]:
+            best = (key, cand)
+    assert best is not None
+    out = list(dims)
+    for i, v in zip(free_idx, sorted(best[1], reverse=True)):
+        out[i] = v
+    return out
+
+
+def coords_of(rank: int, dims: Sequence[int]) -> Tuple[int, int, int]:
+    """Row-major rank -> Cartesian coordinates (MPI_Cart_coords, last dim fastest)."""
+    c2 = rank % dims[2]
+    r = rank // dims[2]
+    c1 = r % dims[1]
+    c0 = r // dims[1]
+    return (c0, c1, c2)
+
+
+def rank_of(coords: Sequence[int], dims: Sequence[int], periodic: bool = False) -> int:
+    c = list(coords)
+    for a in range(3):
+        if periodic:
+            c[a] %= dims[a]
+        elif not 0 <= c[a] < dims[a]:
+            return -1
+    return (c[0] * dims[1] + c[1]) * dims[2] + c[2]
+
+
+def split_extent(L: int, nparts: int, coord: int) -> Tuple[int, int]:
+    """(size, offset) of part ``coord`` of ``L`` cells split ``nparts`` ways (communication.jl:73-87)."""
+    base, rem = divmod(L, nparts)
+    size = base + (1 if coord < rem else 0)
+    offset = base * coord + min(rem, coord)
+    return size, offset
+
+
+@dataclass
+class CartDomain:
+    """Reference ``MPICartDomain`` (Structs.jl:57-73) without the MPI communicator."""
+
+    nprocs: int
+    rank: int
+    L: Tuple[int, int, int]
+    dims: List[int]
+    coords: Tuple[int, int, int]
+    proc_sizes: List[int]
+    proc_offsets: List[int]
+    periodic: bool = False
+    proc_neighbors: Dict[str, int] = field(default_factory=dict)
+    nbr27: List[int] = field(default_factory=list)
+
+    def neighbor(self, dx: int, dy: int, dz: int) -> int:
+        return self.nbr27[(dx + 1) * 9 + (dy + 1) * 3 + (dz + 1)]
+
+    @property
+    def has_neighbors(self) -> bool:
+        return any(r >= 0 for i, r in enumerate(self.nbr27) if i != 13)
+
+
+def init_domain(L, nprocs: int, rank: int, periodic: bool = False,
+                dims: Optional[Sequence[int]] = None) -> CartDomain:
+    """Build this rank's sub-domain (communication.jl:59-96).  ``L`` is an int or a 3-tuple."""
+    if isinstance(L, int):
+        Ls = (L, L, L)
+    else:
+        Ls = tuple(int(v) for v in L)
+    if not 0 <= rank < nprocs:
+        raise ValueError(f"rank {rank} out of range for {nprocs} ranks")
+    d = dims_create(nprocs, dims)
+    coords = coords_of(rank, d)
+    sizes, offsets = [], []
+    for a in range(3):
+        s, o = split_extent(Ls[a], d[a], coords[a])
+        if s < 1:
+            raise ValueError(f"L={Ls[a]} too small for {d[a]} ranks along axis {a}")
+        sizes.append(s)
+        offsets.append(o)
+    nbr27 = []
+    for dx, dy, dz in itertools.product((-1, 0, 1), repeat=3):
+        if (dx, dy, dz) == (0, 0, 0):
+            nbr27.append(-1)
+            continue
+        nbr27.append(rank_of((coords[0] + dx, coords[1] + dy, coords[2] + dz), d, periodic))
+    names = {name: nbr27[(v[0] + 1) * 9 + (v[1] + 1) * 3 + (v[2] + 1)]
+             for name, v in NEIGHBOR_NAMES.items()}
+    return CartDomain(nprocs=nprocs, rank=rank, L=Ls, dims=d, coords=coords, proc_sizes=sizes,
+                      proc_offsets=offsets, periodic=periodic, proc_neighbors=names, nbr27=nbr27)
+
+
+def all_domains(L, nprocs: int, periodic: bool = False) -> List[CartDomain]:
+    return [init_domain(L, nprocs, r, periodic) for r in range(nprocs)]

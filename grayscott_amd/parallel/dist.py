@@ -1,0 +1,107 @@
+"""Process-group bootstrap: one process per MI355X, torch.distributed control plane.
+
+The reference bootstraps with ``MPI.Init`` (communication.jl:20) and uses MPI for everything.
+Here the *control plane* (rendezvous, barriers, timing reductions, RCCL unique-id broadcast,
+BP metadata gathers) is a torch.distributed **gloo** group created from the torchrun
+environment (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR / MASTER_PORT); the *data plane*
+(halo exchange) is RCCL over xGMI, driven natively by ``libgs_hip.so``.
+"""
+from __future__ import annotations
+
+import os
+import pickle
+from dataclasses import dataclass
+from typing import Any, List, Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistContext:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    initialized_here: bool = False
+    _nccl_group: Any = None
+
+    @property
+    def is_distributed(self) -> bool:
+        return self.world_size > 1 and dist.is_available() and dist.is_initialized()
+
+    # -- control-plane collectives (cheap, CPU tensors over gloo) -------------------------
+    def barrier(self) -> None:
+        if self.is_distributed:
+            dist.barrier()
+
+    def allreduce(self, value: float, op: str = "max") -> float:
+        if not self.is_distributed:
+            return float(value)
+        t = torch.tensor([float(value)], dtype=torch.float64)
+        dist.all_reduce(t, op={"max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN,
+                               "sum": dist.ReduceOp.SUM}[op])
+        return float(t.item())
+
+    def allreduce_array(self, values, op: str = "sum"):
+        if not self.is_distributed:
+            return [float(v) for v in values]
+        t = torch.tensor([float(v) for v in values], dtype=torch.float64)
+        dist.all_reduce(t, op={"max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN,
+                               "sum": dist.ReduceOp.SUM}[op])
+        return t.tolist()
+
+    def gather_object(self, obj: Any, dst: int = 0) -> Optional[List[Any]]:
+        if not self.is_distributed:
+            return [obj]
+        out = [None] * self.world_size if self.rank == dst else None
+        dist.gather_object(obj, out, dst=dst)
+        return out
+
+    def broadcast_object(self, obj: Any, src: int = 0) -> Any:
+        if not self.is_distributed:
+            return obj
+        lst = [obj]
+        dist.broadcast_object_list(lst, src=src)
+        return lst[0]
+
+    def nccl_group(self):
+        """Lazily created NCCL(RCCL) process group, for the torch halo transport on GPU."""
+        if self._nccl_group is None:
+            self._nccl_group = dist.new_group(backend="nccl")
+        return self._nccl_group
+
+    def finalize(self) -> None:
+        if self.initialized_here and dist.is_initialized():
+            dist.destroy_process_group()
+            self.initialized_here = False
+
+
+_CTX: Optional[DistContext] = None
+
+
+def init_from_env(device: str = "cpu") -> DistContext:
+    """Initialise (once) from torchrun-style environment variables."""
+    global _CTX
+    if _CTX is not None:
+        return _CTX
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    ctx = DistContext(rank=rank, world_size=world, local_rank=local)
+    if device == "hip":
+        torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29531")
+        dist.init_process_group(backend="gloo", rank=rank, world_size=world)
+        ctx.initialized_here = True
+    _CTX = ctx
+    return ctx
+
+
+def reset() -> None:
+    """Forget the cached context (tests)."""
+    global _CTX
+    if _CTX is not None:
+        _CTX.finalize()
+    _CTX = None

@@ -1,0 +1,23 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP backend, libgs_hip.so)")
+    config.addinivalue_line("markers", "slow: long-running CPU test")
+
+
+@pytest.fixture(scope="session", autouse=True)
+def _native_built():
+    """Build the native libraries once per session if they are missing."""
+    from grayscott_amd.ops import native
+    if not os.path.exists(native.lib_path("core")) or not os.path.exists(native.lib_path("hip")):
+        import subprocess
+        subprocess.run(["make", "-C", ROOT, "-j8", "all"], check=True)
+    yield
