@@ -75,28 +75,28 @@ class CpuBackend final : public gs::Backend {
     {
       gs::U4* cache = new gs::U4[R.nx > 0 ? R.nx : 1];
 #pragma omp for schedule(static)
-      for (int y = R.y0; y < R.y0 + R.ny; ++y) {
-        int64_t gy = g.oy + y;
-        if (gy < 0) gy += g.Ly; else if (gy >= g.Ly) gy -= g.Ly;
-        for (int z = R.z0; z < R.z0 + R.nz; ++z) {
-          int64_t gz = g.oz + z;
-          if (gz < 0) gz += g.Lz; else if (gz >= g.Lz) gz -= g.Lz;
-          if (noise && (z == R.z0 || (gz & 3) == 0)) {
+      for (int z = R.z0; z < R.z0 + R.nz; ++z) {
+        int64_t gz = g.oz + z;
+        if (gz < 0) gz += g.Lz; else if (gz >= g.Lz) gz -= g.Lz;
+        for (int y = R.y0; y < R.y0 + R.ny; ++y) {
+          int64_t gy = g.oy + y;
+          if (gy < 0) gy += g.Ly; else if (gy >= g.Ly) gy -= g.Ly;
+          if (noise && (y == R.y0 || (gy & 3) == 0)) {
             for (int x = R.x0; x < R.x0 + R.nx; ++x) {
               int64_t gx = g.ox + x;
               if (gx < 0) gx += g.Lx; else if (gx >= g.Lx) gx -= g.Lx;
-              cache[x - R.x0] = gs::noise_block(gx, gy, gz >> 2, g.Lx, g.Ly, (uint64_t)t, seed);
+              cache[x - R.x0] = gs::noise_block(gx, gy >> 2, gz, g.Lx, g.Ly, (uint64_t)t, seed);
             }
           }
           const int64_t base = 2 * gs::lin(g, 0, y, z);
           for (int x = R.x0; x < R.x0 + R.nx; ++x) {
             const int64_t i = base + 2 * (int64_t)x;
             const T u = s[i], v = s[i + 1];
-            const T su = s[i - sx] + s[i + sx] + s[i - sy] + s[i + sy] + s[i - sz] + s[i + sz];
-            const T sv = s[i - sx + 1] + s[i + sx + 1] + s[i - sy + 1] + s[i + sy + 1] +
-                         s[i - sz + 1] + s[i + sz + 1];
+            const T su = (s[i - sx] + s[i + sx]) + (s[i - sy] + s[i + sy]) + (s[i - sz] + s[i + sz]);
+            const T sv = (s[i - sx + 1] + s[i + sx + 1]) + (s[i - sy + 1] + s[i + sy + 1]) +
+                         (s[i - sz + 1] + s[i + sz + 1]);
             T r = (T)0;
-            if (noise) r = gs::uniform_pm1<T>(gs::u4_get(cache[x - R.x0], (int)(gz & 3)));
+            if (noise) r = gs::uniform_pm1<T>(gs::u4_get(cache[x - R.x0], (int)(gy & 3)));
             T uo, vo;
             gs::gs_update<T>(c, u, v, su, sv, r, uo, vo);
             d[i] = uo;

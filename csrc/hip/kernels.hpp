@@ -4,6 +4,9 @@
 
 #include <hip/hip_runtime.h>
 
+#include <stdlib.h>
+#include <string.h>
+
 #include <algorithm>
 
 #include "gs/common.h"
@@ -67,85 +70,7 @@ void launch_seed(typename Vec2<T>::type* f, const Geom& g, hipStream_t s) {
   launch_fill<T>(f, g, b, (T)0.25, (T)0.33, s);
 }
 
-// ------------------------------------------------------------------------------------------
-// Single fused step (7-point Laplacian + reaction + Philox noise + Euler) over a region.
-// Lanes run along x (coalesced 8/16-B loads of interleaved (u,v)); each thread marches in z
-// keeping planes z-1, z, z+1 in registers, so every cell is fetched from HBM once and the
-// x/y neighbours are L1/L2 hits.  One Philox block per thread feeds four z-planes.
-// ------------------------------------------------------------------------------------------
-struct StepArgs {
-  Geom g;
-  Box r;
-  int32_t zchunk;
-  int32_t _pad;
-  int64_t t;
-};
-
-template <typename T, bool NOISE>
-__global__ __launch_bounds__(256) void k_step1(const typename Vec2<T>::type* __restrict__ s,
-                                               typename Vec2<T>::type* __restrict__ d,
-                                               StepArgs a, gs::Coef<T> c, uint64_t seed) {
-  using V2 = typename Vec2<T>::type;
-  const Geom& g = a.g;
-  const int x = a.r.x0 + blockIdx.x * 64 + threadIdx.x;
-  const int y = a.r.y0 + blockIdx.y * 4 + threadIdx.y;
-  const int z0 = a.r.z0 + blockIdx.z * a.zchunk;
-  const int z1 = min(z0 + a.zchunk, a.r.z0 + a.r.nz);
-  if (x >= a.r.x0 + a.r.nx || y >= a.r.y0 + a.r.ny || z0 >= z1) return;
-  const int64_t PX = g.px;
-  const int64_t PZ = gs::plane_elems(g);
-  int64_t i = gs::lin(g, x, y, z0);
-  const int64_t gx = wrap(g.ox + x, g.Lx);
-  const int64_t gy = wrap(g.oy + y, g.Ly);
-  V2 cm = s[i - PZ];
-  V2 c0 = s[i];
-  gs::U4 blk{0, 0, 0, 0};
-  for (int z = z0; z < z1; ++z) {
-    const V2 cp = s[i + PZ];
-    const V2 xm = s[i - 1], xp = s[i + 1], ym = s[i - PX], yp = s[i + PX];
-    const T su = (xm.x + xp.x) + (ym.x + yp.x) + (cm.x + cp.x);
-    const T sv = (xm.y + xp.y) + (ym.y + yp.y) + (cm.y + cp.y);
-    T r = (T)0;
-    if (NOISE) {
-      const int64_t gz = wrap(g.oz + z, g.Lz);
-      if (z == z0 || (gz & 3) == 0) blk = gs::noise_block(gx, gy, gz >> 2, g.Lx, g.Ly, (uint64_t)a.t, seed);
-      r = gs::uniform_pm1<T>(gs::u4_get(blk, (int)(gz & 3)));
-    }
-    V2 o;
-    gs::gs_update<T>(c, c0.x, c0.y, su, sv, r, o.x, o.y);
-    d[i] = o;
-    cm = c0;
-    c0 = cp;
-    i += PZ;
-  }
-}
-
-template <typename T>
-void launch_step1(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, const Geom& g,
-                  const gs::Params& p, const Box& r, int64_t t, hipStream_t st) {
-  StepArgs a;
-  a.g = g;
-  a.r = r;
-  a.t = t;
-  const int bx = (r.nx + 63) / 64, by = (r.ny + 3) / 4;
-  const int64_t xy = (int64_t)bx * by;
-  int nzc = (int)std::max<int64_t>(1, (2048 + xy - 1) / xy);
-  int zc = (r.nz + nzc - 1) / nzc;
-  zc = std::max(zc, std::min(r.nz, 8));
-  nzc = (r.nz + zc - 1) / zc;
-  a.zchunk = zc;
-  dim3 grid(bx, by, nzc), block(64, 4, 1);
-  const gs::Coef<T> c = gs::make_coef<T>(p);
-  if (p.noise != 0.0) k_step1<T, true><<<grid, block, 0, st>>>(s, d, a, c, p.seed);
-  else k_step1<T, false><<<grid, block, 0, st>>>(s, d, a, c, p.seed);
-}
-
-template <typename T>
-bool launch_fused(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, const Geom& g,
-                  const gs::Params& p, int n, int64_t t, hipStream_t st) {
-  (void)s; (void)d; (void)g; (void)p; (void)n; (void)t; (void)st;
-  return false;
-}
+#include "stencil.hpp"
 
 // ------------------------------------------------------------------------------------------
 // halo pack / unpack: all messages in one launch (blockIdx.y = message)

@@ -38,7 +38,7 @@ int gs_plan_msg(gs_engine* e, int32_t which, int32_t i, int64_t* out4);
 int64_t gs_geom_total_elems(const gs::Geom* g);
 void gs_make_geom(gs::Geom* out, int nx, int ny, int nz, int H, int64_t ox, int64_t oy, int64_t oz,
                   int64_t Lx, int64_t Ly, int64_t Lz, int periodic);
-void gs_noise_block(int64_t gx, int64_t gy, int64_t gz4, int64_t Lx, int64_t Ly, uint64_t step,
+void gs_noise_block(int64_t gx, int64_t gy4, int64_t gz, int64_t Lx, int64_t Ly, uint64_t step,
                     uint64_t seed, uint32_t* out4);
 int gs_plan_sizes(const gs::Geom* g, const int32_t* nbr27, int32_t diagonals, int64_t* send_cells,
                   int64_t* recv_cells);

@@ -101,9 +101,9 @@ void gs_make_geom(gs::Geom* out, int nx, int ny, int nz, int H, int64_t ox, int6
   *out = gs::make_geom(nx, ny, nz, H, ox, oy, oz, Lx, Ly, Lz, periodic);
 }
 
-void gs_noise_block(int64_t gx, int64_t gy, int64_t gz4, int64_t Lx, int64_t Ly, uint64_t step,
+void gs_noise_block(int64_t gx, int64_t gy4, int64_t gz, int64_t Lx, int64_t Ly, uint64_t step,
                     uint64_t seed, uint32_t* out4) {
-  gs::U4 r = gs::noise_block(gx, gy, gz4, Lx, Ly, step, seed);
+  gs::U4 r = gs::noise_block(gx, gy4, gz, Lx, Ly, step, seed);
   out4[0] = r.x; out4[1] = r.y; out4[2] = r.z; out4[3] = r.w;
 }
 

@@ -80,11 +80,12 @@ GS_HD int64_t box_cells(const Box& b) { return (int64_t)b.nx * b.ny * b.nz; }
 
 // ------------------------------------------------------------------------------------------
 // Noise: rocRAND Philox4x32-10 stream (rocrand_philox4x32_10.h), evaluated counter-mode.
-//   cell (gx,gy,gz), step n  ->  engine(seed, subsequence = n, offset = 4*q + (gz & 3))
-//   with q = gx + Lx*(gy + Ly*(gz >> 2)).
-// One Philox block therefore feeds four consecutive z-planes of one (x,y) column, which is
-// exactly what a thread marching in z consumes.  The stream depends only on global
-// coordinates and the step, so results are decomposition- and restart-invariant.
+//   cell (gx,gy,gz), step n  ->  engine(seed, subsequence = n, offset = 4*q + (gy & 3))
+//   with q = gx + Lx*((gy >> 2) + Ly4*gz),  Ly4 = ceil(Ly / 4).
+// One Philox block therefore feeds four consecutive y-rows of one (x,z) column: the gfx950
+// kernels give each thread a strip of rows, so a block is consumed by the thread that made
+// it.  The stream depends only on global coordinates and the step, so results are
+// decomposition- and restart-invariant.
 // ------------------------------------------------------------------------------------------
 struct U4 { uint32_t x, y, z, w; };
 
@@ -112,9 +113,10 @@ GS_HD U4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint6
   return U4{c0, c1, c2, c3};
 }
 
-GS_HD U4 noise_block(int64_t gx, int64_t gy, int64_t gz4, int64_t Lx, int64_t Ly,
+GS_HD U4 noise_block(int64_t gx, int64_t gy4, int64_t gz, int64_t Lx, int64_t Ly,
                      uint64_t step, uint64_t seed) {
-  const uint64_t q = (uint64_t)gx + (uint64_t)Lx * ((uint64_t)gy + (uint64_t)Ly * (uint64_t)gz4);
+  const uint64_t Ly4 = ((uint64_t)Ly + 3) >> 2;
+  const uint64_t q = (uint64_t)gx + (uint64_t)Lx * ((uint64_t)gy4 + Ly4 * (uint64_t)gz);
   return philox4x32_10((uint32_t)q, (uint32_t)(q >> 32), (uint32_t)step,
                        (uint32_t)(step >> 32), seed);
 }

@@ -2,7 +2,8 @@
 
 Used only as a test oracle: the native CPU backend and the gfx950 kernels are checked against
 it.  It re-implements, without sharing code with ``csrc/``:
-  * the Philox4x32-10 noise stream (rocrand_philox4x32_10.h semantics, counter mode)
+  * the Philox4x32-10 noise stream (rocrand_philox4x32_10.h semantics, counter mode,
+    one block per 4 consecutive y-rows: q = gx + Lx*((gy>>2) + ceil(Ly/4)*gz), word gy&3)
   * the reference initial condition (Simulation_CPU.jl:14-65)
   * one explicit Euler step of the Gray-Scott system (Simulation_CPU.jl:77-113, Common.jl:13-18)
   * the reference boundary behaviour: outer u ghost = 1 at even t, 0 at odd t.
@@ -46,15 +47,16 @@ def noise(L: Sequence[int], offsets: Sequence[int], sizes: Sequence[int], step: 
           seed: int, dtype=np.float64) -> np.ndarray:
     """Uniform[-1,1) draws for the cells of a sub-domain at ``step`` -> (nz, ny, nx)."""
     Lx, Ly, _ = (int(v) for v in L)
+    Ly4 = (Ly + 3) // 4
     nx, ny, nz = (int(v) for v in sizes)
     gx = np.arange(offsets[0], offsets[0] + nx, dtype=np.uint64)
     gy = np.arange(offsets[1], offsets[1] + ny, dtype=np.uint64)
     gz = np.arange(offsets[2], offsets[2] + nz, dtype=np.uint64)
     Z, Y, X = np.meshgrid(gz, gy, gx, indexing="ij")
-    q = X + np.uint64(Lx) * (Y + np.uint64(Ly) * (Z >> np.uint64(2)))
+    q = X + np.uint64(Lx) * ((Y >> np.uint64(2)) + np.uint64(Ly4) * Z)
     st = np.uint64(step)
     r = philox4x32_10(q & MASK32, q >> np.uint64(32), st & MASK32, st >> np.uint64(32), seed)
-    sel = (Z & np.uint64(3)).astype(np.int64)
+    sel = (Y & np.uint64(3)).astype(np.int64)
     words = np.choose(sel, r)
     dt = np.dtype(dtype).type
     return words.view(np.int32).astype(dt) * dt(2.0 ** -31)
