@@ -1,0 +1,400 @@
+// SPDX-License-Identifier: MIT
+// k_fused: T time levels per HBM pass over the interior (temporal blocking) for gfx950.
+// Included inside namespace gsk by kernels.hpp, after stencil.hpp.
+//
+// Work unit = one (tile, z-plane) pair; the units are split evenly over a persistent grid
+// of `occupancy x CUs` workgroups, each walking one or two contiguous z-segments.
+// Tile = 64 columns (one lane each) x WAVES*ROWS rows of level-0 data (ghosts included);
+// it yields (64-2T) x ystep interior outputs.  A segment [z0,z1) streams level-0 planes
+// z0-T .. z1+T-1; at iteration p level l produces plane p-l; level T is stored.
+//
+// Register plan (no rotation copies): level-0 planes live in a 3-deep ring LD[3] (plane p,
+// p-1 and the prefetch of p+1); level-l outputs in a 2-deep ring OUT[l][2]; per consumer
+// level a running partial sum A (xy-neighbours of plane q-1 plus plane q-2).  The loop is
+// unrolled by the ring period (6) so every ring index is a compile-time constant.
+// Memory goes through buffer descriptors built per plane: 32-bit lane offsets, no address
+// VGPRs, out-of-range loads return 0 and masked stores use an out-of-range offset.
+// Intermediate levels outside the global domain (non-periodic) are reset to the boundary
+// value of their time level -- what the single-step path reads from its ghost shell.
+#pragma once
+
+struct FusedArgs {
+  Geom g;
+  int32_t ntx, nty;
+  int32_t xstep, ystep;
+  int32_t ybase;
+  int32_t bcfix;
+  int64_t units;
+  int64_t t;
+  int64_t buf_bytes;  // bytes of one state buffer (descriptor range)
+};
+
+// Folded update coefficients: u' = au*u + asu*su + ac - dt*uvv + ar*r ; v' = bv*v + bsv*sv + dt*uvv
+template <typename T>
+struct FoldCoef {
+  T au, asu, ac, ar, dt, bv, bsv;
+};
+
+template <typename T>
+inline FoldCoef<T> make_fold(const gs::Params& p) {
+  FoldCoef<T> f;
+  f.au = (T)(1.0 - p.dt * (p.Du + p.F));
+  f.asu = (T)(p.dt * p.Du / 6.0);
+  f.ac = (T)(p.dt * p.F);
+  f.ar = (T)(p.dt * p.noise);
+  f.dt = (T)p.dt;
+  f.bv = (T)(1.0 - p.dt * (p.Dv + p.F + p.k));
+  f.bsv = (T)(p.dt * p.Dv / 6.0);
+  return f;
+}
+
+typedef unsigned int gs_u2 __attribute__((ext_vector_type(2)));
+typedef unsigned int gs_u4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const void* base, int64_t off_bytes,
+                                                             int64_t total_bytes) {
+  const int64_t rem = total_bytes - off_bytes;
+  const int nrec = (int)(rem > 0x7ffffff0LL ? 0x7ffffff0LL : (rem < 0 ? 0 : rem));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)base + off_bytes), 0, nrec,
+                                           0x00020000);
+}
+
+__device__ __forceinline__ float2 bload(__amdgpu_buffer_rsrc_t r, int voff, int soff, float2*) {
+  const gs_u2 v = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
+  return make_float2(__uint_as_float(v.x), __uint_as_float(v.y));
+}
+__device__ __forceinline__ double2 bload(__amdgpu_buffer_rsrc_t r, int voff, int soff, double2*) {
+  const gs_u4 v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
+  return make_double2(__longlong_as_double(((long long)v.y << 32) | v.x),
+                      __longlong_as_double(((long long)v.w << 32) | v.z));
+}
+__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, int voff, int soff, float2 c) {
+  gs_u2 v;
+  v.x = __float_as_uint(c.x);
+  v.y = __float_as_uint(c.y);
+  __builtin_amdgcn_raw_buffer_store_b64(v, r, voff, soff, 0);
+}
+__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, int voff, int soff, double2 c) {
+  const unsigned long long a = (unsigned long long)__double_as_longlong(c.x);
+  const unsigned long long b = (unsigned long long)__double_as_longlong(c.y);
+  gs_u4 v;
+  v.x = (unsigned)a; v.y = (unsigned)(a >> 32); v.z = (unsigned)b; v.w = (unsigned)(b >> 32);
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, soff, 0);
+}
+
+// Compile-time configuration of one fused-kernel instantiation.
+//   ROWS x WAVES : rows per wave x waves per workgroup (tile height = ROWS*WAVES)
+//   PF           : level-0 prefetch distance in planes (register ring of PF+2 planes)
+template <typename T, int TL_, int ROWS_, int WAVES_, int PF_, bool PERIODIC_, bool NOISE_,
+          int MINW_ = 1>
+struct FCfg {
+  static constexpr int MINW = MINW_;  // __launch_bounds__ min waves per SIMD
+  using V2 = typename Vec2<T>::type;
+  static constexpr int TL = TL_, ROWS = ROWS_, WAVES = WAVES_, PF = PF_;
+  static constexpr bool PERIODIC = PERIODIC_, NOISE = NOISE_;
+  static constexpr int R = PF + 2;                          // level-0 ring slots
+  static constexpr int PERIOD = (R % 2 == 0) ? R : 2 * R;  // lcm(R, 2)
+  static constexpr int NO = TL > 1 ? TL - 1 : 1;
+};
+
+template <class C>
+struct FusedState {
+  using V2 = typename C::V2;
+  V2 LD[C::R][C::ROWS];
+  V2 OUT[C::NO][2][C::ROWS];
+  V2 A[C::TL][C::ROWS];
+};
+
+// Per-segment constants (wave-uniform values and the lane's offsets).
+struct FusedSeg {
+  int p, pend, z0;
+  int lane, wave;
+  int voff, svoff, pitchb;
+  int srow0, srow1;
+  int64_t gx, gxu, gy0;
+  bool edge;
+};
+
+template <class C>
+__device__ __forceinline__ int64_t gwrap(int64_t v, int64_t L) {
+  if constexpr (C::PERIODIC) return wrap(v, L);
+  else return v;
+}
+
+// One pipeline iteration p (i = p - pstart).  IR = i % R, I2 = i % 2.
+template <class C, typename T, int IR, int I2>
+__device__ __forceinline__ void fused_iter(FusedState<C>& S,
+                                           typename C::V2 (*xch)[2][C::WAVES][2][64],
+                                           const FusedArgs& a, const FoldCoef<T>& f,
+                                           uint64_t seed, const typename C::V2* src,
+                                           typename C::V2* dst, const FusedSeg& sg) {
+  using V2 = typename C::V2;
+  constexpr int ROWS = C::ROWS, WAVES = C::WAVES, TL = C::TL;
+  const Geom& g = a.g;
+  const int p = sg.p;
+  const int64_t PZB = gs::plane_elems(g) * (int64_t)sizeof(V2);
+  // prefetch level-0 plane p+PF into the ring slot of plane p-2
+  if (p + C::PF < sg.pend) {
+    const __amdgpu_buffer_rsrc_t r = plane_rsrc(src, (int64_t)(p + C::PF + g.H) * PZB, a.buf_bytes);
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j)
+      S.LD[(IR + C::PF) % C::R][j] = bload(r, sg.voff + j * sg.pitchb, 0, (V2*)nullptr);
+  }
+#pragma unroll
+  for (int l = 0; l < TL; ++l) {
+    // input plane of level l (plane p-l) and the centre plane p-l-1
+    V2* in = l == 0 ? S.LD[IR] : S.OUT[l == 0 ? 0 : l - 1][I2];
+    V2* Cc = l == 0 ? S.LD[(IR + C::R - 1) % C::R] : S.OUT[l == 0 ? 0 : l - 1][1 - I2];
+    xch[l][I2][sg.wave][0][sg.lane] = in[0];
+    xch[l][I2][sg.wave][1][sg.lane] = in[ROWS - 1];
+    __syncthreads();
+    const V2 up = sg.wave > 0 ? xch[l][I2][sg.wave - 1][1][sg.lane] : in[0];
+    const V2 dn = sg.wave < WAVES - 1 ? xch[l][I2][sg.wave + 1][0][sg.lane] : in[ROWS - 1];
+    const int q = p - l - 1;  // plane produced by level l+1
+    const int64_t gz = gwrap<C>(g.oz + q, g.Lz);
+    const uint64_t tstep = (uint64_t)(a.t + l);
+    V2 res[ROWS];
+#pragma unroll
+    for (int m = 0; m < ROWS / 4; ++m) {
+      gs::U4 blk{0, 0, 0, 0};
+      if constexpr (C::NOISE) {
+        const int64_t gyq = gwrap<C>(sg.gy0 + 4 * m, g.Ly);
+        blk = gs::noise_block(sg.gx, gyq >> 2, gz, g.Lx, g.Ly, tstep, seed);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int j = 4 * m + k;
+        const V2 ym = j == 0 ? up : in[j - 1];
+        const V2 yp = j == ROWS - 1 ? dn : in[j + 1];
+        const T xyu = (lane_from_left(in[j].x) + lane_from_right(in[j].x)) + (ym.x + yp.x);
+        const T xyv = (lane_from_left(in[j].y) + lane_from_right(in[j].y)) + (ym.y + yp.y);
+        const T su = S.A[l][j].x + in[j].x;
+        const T sv = S.A[l][j].y + in[j].y;
+        const T cu = Cc[j].x, cv = Cc[j].y;
+        const T uvv = cu * cv * cv;
+        T ru = f.ac;
+        if constexpr (C::NOISE) {
+          const uint32_t w = k == 0 ? blk.x : (k == 1 ? blk.y : (k == 2 ? blk.z : blk.w));
+          ru = fma(f.ar, gs::uniform_pm1<T>(w), ru);
+        }
+        res[j].x = fma(f.au, cu, fma(f.asu, su, fma(-f.dt, uvv, ru)));
+        res[j].y = fma(f.bv, cv, fma(f.bsv, sv, f.dt * uvv));
+        S.A[l][j].x = xyu + cu;
+        S.A[l][j].y = xyv + cv;
+      }
+    }
+    if (l + 1 < TL) {
+      if (sg.edge) {
+        const T bu = (T)gs::bc_u(a.t + l + 1);
+        const bool zout = (g.oz + q < 0) || (g.oz + q >= g.Lz);
+        const bool xout = sg.gxu < 0 || sg.gxu >= g.Lx;
+#pragma unroll
+        for (int j = 0; j < ROWS; ++j) {
+          const int64_t gyj = sg.gy0 + j;
+          if (zout || xout || gyj < 0 || gyj >= g.Ly) {
+            res[j].x = bu;
+            res[j].y = (T)0;
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < ROWS; ++j) S.OUT[l][I2][j] = res[j];
+    } else {
+      const int zs = p - TL;
+      if (zs >= sg.z0) {
+        const __amdgpu_buffer_rsrc_t w = plane_rsrc(dst, (int64_t)(zs + g.H) * PZB, a.buf_bytes);
+#pragma unroll
+        for (int j = 0; j < ROWS; ++j) {
+          const int off = (j >= sg.srow0 && j < sg.srow1) ? sg.svoff + j * sg.pitchb : (int)0x80000000;
+          bstore(w, off, 0, res[j]);
+        }
+      }
+    }
+  }
+}
+
+// Unrolled walk over one ring period; returns false when the segment is done.
+template <class C, typename T, int I>
+__device__ __forceinline__ bool fused_period(FusedState<C>& S,
+                                             typename C::V2 (*xch)[2][C::WAVES][2][64],
+                                             const FusedArgs& a, const FoldCoef<T>& f,
+                                             uint64_t seed, const typename C::V2* src,
+                                             typename C::V2* dst, FusedSeg& sg) {
+  if constexpr (I == C::PERIOD) {
+    return true;
+  } else {
+    fused_iter<C, T, I % C::R, I % 2>(S, xch, a, f, seed, src, dst, sg);
+    if (++sg.p >= sg.pend) return false;
+    return fused_period<C, T, I + 1>(S, xch, a, f, seed, src, dst, sg);
+  }
+}
+
+template <class C, typename T>
+__global__ __launch_bounds__(64 * C::WAVES, C::MINW) void k_fused(const typename C::V2* __restrict__ s,
+                                                         typename C::V2* __restrict__ d,
+                                                         FusedArgs a, FoldCoef<T> f,
+                                                         uint64_t seed) {
+  using V2 = typename C::V2;
+  constexpr int ROWS = C::ROWS, WAVES = C::WAVES, TL = C::TL;
+  static_assert(ROWS % 4 == 0, "rows per wave must hold whole noise quads");
+  __shared__ V2 xch[TL][2][WAVES][2][64];  // [level][parity][wave][first/last row][lane]
+  const Geom& g = a.g;
+  FusedSeg sg;
+  sg.lane = threadIdx.x & 63;
+  sg.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  sg.pitchb = g.px * (int)sizeof(V2);
+  const int nz = g.nz;
+  const int64_t U = a.units;
+  int64_t u = (int64_t)blockIdx.x * U / gridDim.x;
+  const int64_t uend = (int64_t)(blockIdx.x + 1) * U / gridDim.x;
+  FusedState<C> S;
+
+  while (u < uend) {
+    const int tile = (int)(u / nz);
+    const int z0 = (int)(u % nz);
+    const int z1 = (int)std::min<int64_t>(nz, z0 + (uend - u));
+    u += z1 - z0;
+    const int tx = tile % a.ntx, ty = tile / a.ntx;
+    const int X0 = tx * a.xstep - TL;
+    const int Y0 = a.ybase + ty * a.ystep - TL;
+    const int x = X0 + sg.lane;
+    const int ylo = Y0 + sg.wave * ROWS;
+    // lane byte offset inside a plane (row ylo); negative values are out of range
+    sg.voff = ((ylo + g.H) * g.px + x + g.xo) * (int)sizeof(V2);
+    sg.gxu = g.ox + x;
+    sg.gx = gwrap<C>(sg.gxu, g.Lx);
+    sg.gy0 = g.oy + ylo;
+    const int ox1 = min(X0 + TL + a.xstep, g.nx);
+    const int oy0 = max(Y0 + TL, 0), oy1 = min(Y0 + TL + a.ystep, g.ny);
+    const bool xin = x >= max(X0 + TL, 0) && x < ox1;
+    sg.svoff = xin ? sg.voff : (int)0x80000000;  // masked lanes store out of range
+    sg.srow0 = max(oy0 - ylo, 0);
+    sg.srow1 = min(oy1 - ylo, ROWS);
+    sg.edge = a.bcfix &&
+        (g.ox + X0 < 0 || g.ox + X0 + 64 > g.Lx || g.oy + Y0 < 0 ||
+         g.oy + Y0 + WAVES * ROWS > g.Ly || g.oz + z0 - TL < 0 || g.oz + z1 + TL > g.Lz);
+    sg.z0 = z0;
+#pragma unroll
+    for (int l = 0; l < TL; ++l)
+#pragma unroll
+      for (int j = 0; j < ROWS; ++j) S.A[l][j].x = S.A[l][j].y = (T)0;
+    sg.p = z0 - TL;
+    sg.pend = z1 + TL;
+    const int64_t PZB = gs::plane_elems(g) * (int64_t)sizeof(V2);
+#pragma unroll
+    for (int k = 0; k < C::PF; ++k) {
+      if (sg.p + k < sg.pend) {
+        const __amdgpu_buffer_rsrc_t r = plane_rsrc(s, (int64_t)(sg.p + k + g.H) * PZB, a.buf_bytes);
+#pragma unroll
+        for (int j = 0; j < ROWS; ++j) S.LD[k][j] = bload(r, sg.voff + j * sg.pitchb, 0, (V2*)nullptr);
+      }
+    }
+    while (fused_period<C, T, 0>(S, xch, a, f, seed, s, d, sg)) {
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+template <class C, typename T>
+struct FusedLaunch {
+  static int occupancy() {
+    static int occ = -1;
+    if (occ < 0) {
+      int o = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k_fused<C, T>, 64 * C::WAVES, 0) !=
+              hipSuccess || o < 1)
+        o = 1;
+      occ = o;
+    }
+    return occ;
+  }
+  static void run(const typename C::V2* s, typename C::V2* d, const FusedArgs& a0,
+                  const gs::Params& p, hipStream_t st) {
+    FusedArgs a = a0;
+    a.xstep = 64 - 2 * C::TL;
+    a.ystep = (C::WAVES * C::ROWS - 2 * C::TL) & ~3;
+    a.ybase = -mod4(a.g.oy - C::TL);  // (oy + ybase - TL) % 4 == 0
+    a.ntx = (a.g.nx + a.xstep - 1) / a.xstep;
+    a.nty = (a.g.ny - a.ybase + a.ystep - 1) / a.ystep;
+    a.units = (int64_t)a.ntx * a.nty * a.g.nz;
+    static int cus = 0;
+    if (!cus) {
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+    }
+    int64_t nwg = (int64_t)occupancy() * cus;
+    nwg = std::max<int64_t>(1, std::min<int64_t>(nwg, a.units / (4 * C::TL + 8)));
+    const FoldCoef<T> f = make_fold<T>(p);
+    k_fused<C, T><<<(unsigned)nwg, 64 * C::WAVES, 0, st>>>(s, d, a, f, p.seed);
+  }
+};
+
+// Tuning hook: GS_FUSED_CFG=<rows>x<waves>:<pf> picks a non-default fp32 configuration.
+inline int fused_cfg_env() {
+  static int v = -1;
+  if (v < 0) {
+    v = 0;
+    const char* e = getenv("GS_FUSED_CFG");
+    if (e) {
+      static const char* names[] = {"",      "4x8:1",   "4x8:2",   "4x8:4",  "8x4:1",
+                                    "8x4:2", "4x16:2",  "8x8:2",   "4x8:3",  "8x4:2w3",
+                                    "8x4:1w3", "4x8:2w4", "8x4:3"};
+      for (int i = 1; i < (int)(sizeof(names) / sizeof(names[0])); ++i)
+        if (!strcmp(e, names[i])) v = i;
+    }
+  }
+  return v;
+}
+
+template <typename T, int TL, bool PER, bool NZ>
+void run_fused_cfg(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, const FusedArgs& a,
+                   const gs::Params& p, hipStream_t st) {
+  if constexpr (sizeof(T) == 4 && !PER && NZ) {
+    switch (fused_cfg_env()) {
+      case 1: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ>, T>::run(s, d, a, p, st); return;
+      case 3: FusedLaunch<FCfg<T, TL, 4, 8, 4, PER, NZ>, T>::run(s, d, a, p, st); return;
+      case 4: FusedLaunch<FCfg<T, TL, 8, 4, 1, PER, NZ>, T>::run(s, d, a, p, st); return;
+      case 5: FusedLaunch<FCfg<T, TL, 8, 4, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
+      case 6: FusedLaunch<FCfg<T, TL, 4, 16, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
+      case 7: FusedLaunch<FCfg<T, TL, 8, 8, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
+      case 8: FusedLaunch<FCfg<T, TL, 4, 8, 3, PER, NZ>, T>::run(s, d, a, p, st); return;
+      case 9: FusedLaunch<FCfg<T, TL, 8, 4, 2, PER, NZ, 3>, T>::run(s, d, a, p, st); return;
+      case 10: FusedLaunch<FCfg<T, TL, 8, 4, 1, PER, NZ, 3>, T>::run(s, d, a, p, st); return;
+      case 11: FusedLaunch<FCfg<T, TL, 4, 8, 2, PER, NZ, 4>, T>::run(s, d, a, p, st); return;
+      case 12: FusedLaunch<FCfg<T, TL, 8, 4, 3, PER, NZ>, T>::run(s, d, a, p, st); return;
+      default: break;
+    }
+  }
+  // measured defaults (L=512, MI355X): fp32 8x4 tile with a 2-plane prefetch; fp64 4x8
+  if constexpr (sizeof(T) == 4) FusedLaunch<FCfg<T, TL, 8, 4, 2, PER, NZ>, T>::run(s, d, a, p, st);
+  else FusedLaunch<FCfg<T, TL, 4, 8, 2, PER, NZ>, T>::run(s, d, a, p, st);
+}
+
+template <typename T, int TL>
+void run_fused_tl(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, const FusedArgs& a,
+                  const gs::Params& p, hipStream_t st) {
+  const bool per = a.g.periodic != 0, nz = p.noise != 0.0;
+  if (per) {
+    if (nz) run_fused_cfg<T, TL, true, true>(s, d, a, p, st);
+    else run_fused_cfg<T, TL, true, false>(s, d, a, p, st);
+  } else {
+    if (nz) run_fused_cfg<T, TL, false, true>(s, d, a, p, st);
+    else run_fused_cfg<T, TL, false, false>(s, d, a, p, st);
+  }
+}
+
+template <typename T>
+bool launch_fused(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, const Geom& g,
+                  const gs::Params& p, int n, int64_t t, hipStream_t st) {
+  if (n < 2 || n > 3 || g.H < n) return false;
+  if (g.periodic && (g.Ly % 4 != 0)) return false;  // noise quads would straddle the wrap
+  FusedArgs a{};
+  a.g = g;
+  a.t = t;
+  a.bcfix = g.periodic ? 0 : 1;
+  a.buf_bytes = gs::total_elems(g) * (int64_t)sizeof(typename Vec2<T>::type);
+  if (n == 2) run_fused_tl<T, 2>(s, d, a, p, st);
+  else run_fused_tl<T, 3>(s, d, a, p, st);
+  return true;
+}

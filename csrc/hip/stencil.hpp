@@ -185,231 +185,4 @@ void launch_step1(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, co
 // Intermediate levels that fall outside the global domain (non-periodic) are reset to the
 // boundary value of their time level, exactly what the single-step path sees in its ghosts.
 // ------------------------------------------------------------------------------------------
-struct FusedArgs {
-  Geom g;
-  int32_t ntx, nty;
-  int32_t xstep, ystep;
-  int32_t ybase;
-  int32_t bcfix;
-  int64_t units;
-  int64_t t;
-};
-
-template <typename T, int TL, int ROWS, int WAVES, bool NOISE>
-__global__ __launch_bounds__(64 * WAVES) void k_fused(const typename Vec2<T>::type* __restrict__ s,
-                                                      typename Vec2<T>::type* __restrict__ d,
-                                                      FusedArgs a, gs::Coef<T> c, uint64_t seed) {
-  using V2 = typename Vec2<T>::type;
-  static_assert(ROWS % 4 == 0, "rows per wave must hold whole noise quads");
-  __shared__ V2 xch[TL][2][WAVES][2][64];  // [level][parity][wave][first/last row][lane]
-  const Geom& g = a.g;
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform -> SGPR
-  const int H = g.H;
-  const int nz = g.nz;
-  const int64_t PZ = gs::plane_elems(g);
-  const int64_t U = a.units;
-  int64_t u = (int64_t)blockIdx.x * U / gridDim.x;
-  const int64_t uend = (int64_t)(blockIdx.x + 1) * U / gridDim.x;
-
-  while (u < uend) {
-    const int tile = (int)(u / nz);
-    const int z0 = (int)(u % nz);
-    const int z1 = (int)std::min<int64_t>(nz, z0 + (uend - u));
-    u += z1 - z0;
-    const int tx = tile % a.ntx, ty = tile / a.ntx;
-    const int X0 = tx * a.xstep - TL;                 // level-0 region origin
-    const int Y0 = a.ybase + ty * a.ystep - TL;
-    const int x = X0 + lane;
-    const int ylo = Y0 + wave * ROWS;
-    const int xc = clampi(x, -H, g.nx + H - 1);
-    const V2* __restrict__ sc = s + xc + g.xo;
-    // global coordinates used by the noise stream and the boundary fix
-    const int64_t gxu = g.ox + x;
-    const int64_t gx = g.periodic ? wrap(gxu, g.Lx) : gxu;
-    const int64_t gy0 = g.oy + ylo;  // multiple of 4 by construction of ybase
-    // output window
-    const int ox0 = X0 + TL, ox1 = min(X0 + TL + a.xstep, g.nx);
-    const int oy0 = max(Y0 + TL, 0), oy1 = min(Y0 + TL + a.ystep, g.ny);
-    const bool xout = x >= max(ox0, 0) && x < ox1;
-    const bool edge = a.bcfix &&
-        (g.ox + X0 < 0 || g.ox + X0 + 64 > g.Lx || g.oy + Y0 < 0 ||
-         g.oy + Y0 + WAVES * ROWS > g.Ly || g.oz + z0 - TL < 0 || g.oz + z1 + TL > g.Lz);
-
-    V2 C[TL][ROWS], A[TL][ROWS], ld[ROWS];
-#pragma unroll
-    for (int l = 0; l < TL; ++l)
-#pragma unroll
-      for (int j = 0; j < ROWS; ++j) {
-        C[l][j].x = C[l][j].y = (T)0;
-        A[l][j].x = A[l][j].y = (T)0;
-      }
-    int ro[ROWS];
-#pragma unroll
-    for (int j = 0; j < ROWS; ++j) ro[j] = (clampi(ylo + j, -H, g.ny + H - 1) + H) * g.px;
-    {
-      const int64_t zo = (int64_t)(z0 - TL + H) * PZ;
-#pragma unroll
-      for (int j = 0; j < ROWS; ++j) ld[j] = sc[zo + ro[j]];
-    }
-    for (int p = z0 - TL; p < z1 + TL; ++p) {
-      V2 in[ROWS];
-#pragma unroll
-      for (int j = 0; j < ROWS; ++j) in[j] = ld[j];
-      if (p + 1 < z1 + TL) {
-        const int64_t zo = (int64_t)(p + 1 + H) * PZ;
-#pragma unroll
-        for (int j = 0; j < ROWS; ++j) ld[j] = sc[zo + ro[j]];
-      }
-      const int par = p & 1;
-#pragma unroll
-      for (int l = 0; l < TL; ++l) {
-        // ---- y-neighbours across waves: publish first/last row, read the neighbours' ----
-        xch[l][par][wave][0][lane] = in[0];
-        xch[l][par][wave][1][lane] = in[ROWS - 1];
-        __syncthreads();
-        const V2 up = wave > 0 ? xch[l][par][wave - 1][1][lane] : in[0];
-        const V2 dn = wave < WAVES - 1 ? xch[l][par][wave + 1][0][lane] : in[ROWS - 1];
-        // ---- level l+1 at plane q = p-l-1, from level-l planes q-1 (in A), q (C), q+1 (in) ----
-        const int q = p - l - 1;
-        const int64_t tstep = a.t + l;
-        const int64_t gz = g.periodic ? wrap(g.oz + q, g.Lz) : g.oz + q;
-        V2 out[ROWS];
-#pragma unroll
-        for (int m = 0; m < ROWS / 4; ++m) {
-          gs::U4 blk{0, 0, 0, 0};
-          if (NOISE) {
-            const int64_t gyq = g.periodic ? wrap(gy0 + 4 * m, g.Ly) : gy0 + 4 * m;
-            blk = gs::noise_block(gx, gyq >> 2, gz, g.Lx, g.Ly, (uint64_t)tstep, seed);
-          }
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int j = 4 * m + k;
-            const V2 ym = j == 0 ? up : in[j - 1];
-            const V2 yp = j == ROWS - 1 ? dn : in[j + 1];
-            const T xyu = (lane_from_left(in[j].x) + lane_from_right(in[j].x)) + (ym.x + yp.x);
-            const T xyv = (lane_from_left(in[j].y) + lane_from_right(in[j].y)) + (ym.y + yp.y);
-            const T su = A[l][j].x + in[j].x;
-            const T sv = A[l][j].y + in[j].y;
-            T r = (T)0;
-            if (NOISE) r = gs::uniform_pm1<T>(k == 0 ? blk.x : (k == 1 ? blk.y : (k == 2 ? blk.z : blk.w)));
-            gs::gs_update<T>(c, C[l][j].x, C[l][j].y, su, sv, r, out[j].x, out[j].y);
-            A[l][j].x = xyu + C[l][j].x;
-            A[l][j].y = xyv + C[l][j].y;
-            C[l][j] = in[j];
-          }
-        }
-        if (l + 1 < TL && edge) {
-          // cells outside the global domain hold the boundary value of time t+l+1
-          const T bu = (T)gs::bc_u(a.t + l + 1);
-          const bool zo_ = (g.oz + q < 0) || (g.oz + q >= g.Lz);
-          const bool xo_ = gxu < 0 || gxu >= g.Lx;
-#pragma unroll
-          for (int j = 0; j < ROWS; ++j) {
-            const int64_t gyj = gy0 + j;
-            if (zo_ || xo_ || gyj < 0 || gyj >= g.Ly) {
-              out[j].x = bu;
-              out[j].y = (T)0;
-            }
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < ROWS; ++j) in[j] = out[j];
-      }
-      // level TL holds plane p - TL
-      const int zs = p - TL;
-      if (zs >= z0 && xout) {
-        const int64_t zo = (int64_t)(zs + H) * PZ;
-        V2* __restrict__ dc = d + zo + x + g.xo;
-#pragma unroll
-        for (int j = 0; j < ROWS; ++j) {
-          const int y = ylo + j;
-          if (y >= oy0 && y < oy1) dc[ro[j]] = in[j];
-        }
-      }
-    }
-  }
-}
-
-template <typename T, int TL, int ROWS, int WAVES>
-struct FusedLaunch {
-  static int occupancy() {
-    static int occ = -1;
-    if (occ < 0) {
-      int o = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k_fused<T, TL, ROWS, WAVES, true>,
-                                                       64 * WAVES, 0) != hipSuccess || o < 1)
-        o = 1;
-      occ = o;
-    }
-    return occ;
-  }
-  static void run(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, const Geom& g,
-                  const gs::Params& p, int64_t t, hipStream_t st) {
-    FusedArgs a;
-    a.g = g;
-    a.t = t;
-    a.xstep = 64 - 2 * TL;
-    a.ystep = (WAVES * ROWS - 2 * TL) & ~3;
-    a.ybase = -mod4(g.oy - TL);  // (oy + ybase - TL) % 4 == 0
-    a.ntx = (g.nx + a.xstep - 1) / a.xstep;
-    a.nty = (g.ny - a.ybase + a.ystep - 1) / a.ystep;
-    a.bcfix = g.periodic ? 0 : 1;
-    a.units = (int64_t)a.ntx * a.nty * g.nz;
-    static int cus = 0;
-    if (!cus) {
-      int dev = 0;
-      (void)hipGetDevice(&dev);
-      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
-    }
-    int64_t nwg = (int64_t)occupancy() * cus;
-    // at least ~2*TL+8 planes per workgroup so the pipeline fill stays cheap
-    nwg = std::max<int64_t>(1, std::min<int64_t>(nwg, a.units / (4 * TL + 8)));
-    const gs::Coef<T> c = gs::make_coef<T>(p);
-    if (p.noise != 0.0)
-      k_fused<T, TL, ROWS, WAVES, true><<<(unsigned)nwg, 64 * WAVES, 0, st>>>(s, d, a, c, p.seed);
-    else
-      k_fused<T, TL, ROWS, WAVES, false><<<(unsigned)nwg, 64 * WAVES, 0, st>>>(s, d, a, c, p.seed);
-  }
-};
-
-// Tile shapes (rows per wave x waves): selectable with GS_FUSED_SHAPE=<rows>x<waves> for
-// tuning; the defaults are the measured best on MI355X.
-inline int fused_shape_env() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("GS_FUSED_SHAPE");
-    v = 0;
-    if (e) {
-      if (!strcmp(e, "8x8")) v = 1;
-      else if (!strcmp(e, "8x4")) v = 2;
-      else if (!strcmp(e, "4x16")) v = 3;
-      else if (!strcmp(e, "4x8")) v = 4;
-    }
-  }
-  return v;
-}
-
-template <typename T, int TL>
-void run_fused_shape(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, const Geom& g,
-                     const gs::Params& p, int64_t t, hipStream_t st) {
-  const int shape = fused_shape_env();
-  if constexpr (sizeof(T) == 4) {
-    if (shape == 3) { FusedLaunch<T, TL, 4, 16>::run(s, d, g, p, t, st); return; }
-  }
-  switch (shape) {
-    case 2: FusedLaunch<T, TL, 8, 4>::run(s, d, g, p, t, st); break;
-    case 4: FusedLaunch<T, TL, 4, 8>::run(s, d, g, p, t, st); break;
-    default: FusedLaunch<T, TL, 8, 8>::run(s, d, g, p, t, st); break;
-  }
-}
-
-template <typename T>
-bool launch_fused(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, const Geom& g,
-                  const gs::Params& p, int n, int64_t t, hipStream_t st) {
-  if (n < 2 || n > 3 || g.H < n) return false;
-  if (g.periodic && (g.Ly % 4 != 0)) return false;  // noise quads would straddle the wrap
-  if (n == 2) run_fused_shape<T, 2>(s, d, g, p, t, st);
-  else run_fused_shape<T, 3>(s, d, g, p, t, st);
-  return true;
-}
+#include "fused.hpp"

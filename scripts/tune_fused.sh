@@ -1,13 +1,13 @@
 #!/bin/bash
-# Sweep fused-kernel tile shapes and temporal depth on one GPU (L=512 fp32 bench config).
-# usage: scripts/tune_fused.sh [outdir]
+# Sweep fused-kernel configurations (GS_FUSED_CFG=<rows>x<waves>:<prefetch>) and temporal
+# depth on one GPU with the L=512 fp32 bench config.   usage: scripts/tune_fused.sh [outdir]
 out=${1:-gpurun_out/tune}
 mkdir -p "$out"
-for fuse in 1 2 3; do
-  for shape in 8x8 8x4 4x16 4x8; do
-    if [ "$fuse" = 1 ] && [ "$shape" != 8x8 ]; then continue; fi
-    GS_FUSED_SHAPE=$shape timeout -k 10 120 python bench.py --steps 120 --warmup 12 --fuse $fuse \
-      > "$out/f${fuse}_${shape}.json" 2> "$out/f${fuse}_${shape}.err" || { echo "FAIL fuse=$fuse shape=$shape rc=$?"; exit 1; }
-    python -c "import json,sys; d=json.load(open('$out/f${fuse}_${shape}.json')); print('fuse=$fuse shape=$shape', d['value'], 'MLUPS', d['ms_per_step'], 'ms/step', d['check'])"
+for fuse in ${FUSES:-2 3}; do
+  for cfg in ${CFGS:-4x8:1 4x8:2 4x8:3 4x8:4 8x4:1 8x4:2 4x16:2 8x8:2}; do
+    tag="f${fuse}_${cfg/:/_}"
+    GS_FUSED_CFG=$cfg timeout -k 10 120 python bench.py --steps ${STEPS:-120} --warmup 12 --fuse $fuse \
+      > "$out/$tag.json" 2> "$out/$tag.err" || { echo "FAIL fuse=$fuse cfg=$cfg rc=$?"; exit 1; }
+    python -c "import json; d=json.load(open('$out/$tag.json')); print('fuse=$fuse cfg=$cfg', d['value'], 'MLUPS', d['ms_per_step'], 'ms/step')"
   done
 done
