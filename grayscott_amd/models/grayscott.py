@@ -97,10 +97,11 @@ class GrayScott:
             uid = native.rccl_unique_id() if self.ctx.rank == 0 else None
             uid = self.ctx.broadcast_object(uid, src=0)
             self.engine.rccl_init(uid, self.ctx.world_size, self.ctx.rank)
-        elif kind == "torch":
-            group = self.ctx.nccl_group() if self.backend == "hip" else None
+        elif kind in ("torch", "host"):
+            stage = kind == "host" and self.backend == "hip"
+            group = self.ctx.nccl_group() if (self.backend == "hip" and not stage) else None
             self._torch_transport = TorchTransport(self.engine.plan(), self.sendbuf, self.recvbuf,
-                                                   self.domain.rank, group)
+                                                   self.domain.rank, group, stage_host=stage)
             self.engine.set_transport(self._torch_transport)
         else:
             raise ValueError(f"unknown transport {kind!r}")

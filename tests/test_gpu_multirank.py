@@ -1,0 +1,43 @@
+"""Multi-rank GPU runs on ONE MI355X (several processes share the device).
+
+RCCL refuses two ranks on one GPU, so these use the host-staged gloo transport: they verify
+the gfx950 pack/unpack kernels, the 26-direction halo plan and the fused kernel's ghost
+handling across real process boundaries.  The RCCL transport itself runs in bench.py on the
+8-GPU node.
+"""
+import numpy as np
+import pytest
+import torch
+
+from .mp_utils import run_ranks
+
+pytestmark = pytest.mark.gpu
+
+
+def _cfg(L, steps, fuse, periodic=False, prec="Float32", transport="host"):
+    return {"settings": dict(L=L, precision=prec, F=0.02, k=0.048, dt=1.0, Du=0.2, Dv=0.1,
+                             noise=0.1, backend="AMDGPU", periodic=periodic, seed=1234),
+            "steps": steps, "fuse": fuse, "transport": transport}
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+@pytest.mark.parametrize("world,L,fuse,periodic,prec", [
+    (2, 48, 2, False, "Float32"),
+    (4, 40, 2, False, "Float64"),
+    (8, 36, 2, False, "Float32"),
+    (4, 32, 3, True, "Float32"),
+    (2, 30, 1, False, "Float64"),
+])
+def test_gpu_decomposed_matches_single_rank(world, L, fuse, periodic, prec):
+    steps = 9
+    u1, v1, _ = run_ranks(1, _cfg(L, steps, fuse, periodic, prec))
+    un, vn, meta = run_ranks(world, _cfg(L, steps, fuse, periodic, prec))
+    assert all(m["transport"] == "host" for m in meta)
+    tol = 0 if prec == "Float64" else 0
+    np.testing.assert_allclose(un, u1, rtol=0, atol=tol)
+    np.testing.assert_allclose(vn, v1, rtol=0, atol=tol)
