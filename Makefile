@@ -12,7 +12,7 @@ CXXFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-parameter \
             -Wno-unused-result
 
-CORE_SRC := csrc/cpu/backend_cpu.cpp
+CORE_SRC := csrc/cpu/backend_cpu.cpp csrc/io/bp4.cpp
 HIP_SRC  := csrc/hip/backend_hip.hip
 HDRS     := $(wildcard csrc/include/gs/*.h) $(wildcard csrc/hip/*.hpp)
 

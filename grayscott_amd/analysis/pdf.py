@@ -1,0 +1,167 @@
+"""PDF (histogram) analysis of a Gray-Scott output stream -- a working version of the
+reference's non-functional stub src/analysis/pdfcalc.jl (defect D10), following the intended
+design of that file and of the ADIOS2-Examples ``pdf_calc``:
+
+* positional arguments ``input`` ``output`` [``N`` = 1000] [``output_inputdata`` = false]
+  (pdfcalc.jl:51-84)
+* for every step of ``input`` (IO "SimulationOutput"): read U and V, split along the slowest
+  dimension (z) across the ranks -- the last rank takes the remainder (pdfcalc.jl:133-139)
+* per z-slice histogram with N bins between the global min and max of the variable at that
+  step (the min/max come from the BP4 block statistics); a value equal to max lands in the
+  last bin; degenerate ranges put the whole slice into every bin (pdfcalc.jl:13-49)
+* write ``output`` (IO "PDFAnalysisOutput"): ``U/pdf``, ``V/pdf`` (global [Lz, N] arrays, one
+  block per rank), ``U/bins``, ``V/bins`` ([N], rank 0), ``step``; with output_inputdata also
+  the slices of ``U`` and ``V`` that were read.
+* ``--follow`` keeps polling an active (still being written) stream until its writer closes,
+  like the reference's ``begin_step(..., timeout)`` loop (pdfcalc.jl:112-123).
+
+Run:  python -m grayscott_amd.analysis.pdf gs.bp pdf.bp 1000   (torchrun for several ranks)
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from ..io.bp4 import BP4Reader, BP4Writer
+from ..parallel.dist import DistContext, init_from_env
+
+
+def _epsilon(d: float) -> bool:
+    return d < 1.0e-20
+
+
+def _str2bool(s: str) -> bool:
+    v = str(s).strip().lower()
+    if v in ("true", "1", "yes", "y"):
+        return True
+    if v in ("false", "0", "no", "n"):
+        return False
+    raise argparse.ArgumentTypeError(f"expected a Bool, got {s!r}")
+
+
+def parse_arguments(args: Sequence[str]) -> Dict[str, object]:
+    """pdfcalc.jl:51-84 (same positional names and defaults)."""
+    p = argparse.ArgumentParser(prog="gs-pdf",
+                                description="gray-scott workflow pdf generator (grayscott_amd)")
+    p.add_argument("input", help="Name of the input file handle for reading data")
+    p.add_argument("output", help="Name of the output file to which data must be written")
+    p.add_argument("N", nargs="?", type=int, default=1000,
+                   help="Number of bins for the PDF calculation, default = 1000")
+    p.add_argument("output_inputdata", nargs="?", type=_str2bool, default=False,
+                   help="YES will write the original variables besides the analysis results")
+    p.add_argument("--follow", action="store_true", help="poll a stream that is still being written")
+    p.add_argument("--timeout", type=float, default=10.0, help="seconds to wait for new steps")
+    ns = p.parse_args(list(args))
+    return {"input": ns.input, "output": ns.output, "N": ns.N,
+            "output_inputdata": ns.output_inputdata, "follow": ns.follow, "timeout": ns.timeout}
+
+
+def compute_pdf(data: np.ndarray, nbins: int, vmin: float, vmax: float) -> Tuple[np.ndarray, np.ndarray]:
+    """Per-slice histograms of ``data`` (count, ny, nx) -> (pdf[count, nbins], bins[nbins])."""
+    count = data.shape[0]
+    slice_size = int(np.prod(data.shape[1:]))
+    bin_width = (vmax - vmin) / nbins
+    bins = vmin + bin_width * np.arange(nbins, dtype=np.float64)
+    if nbins == 1 or _epsilon(vmax - vmin) or _epsilon(abs(bin_width)):
+        return np.full((count, nbins), float(slice_size)), bins
+    flat = data.reshape(count, slice_size).astype(np.float64)
+    idx = np.floor((flat - vmin) / bin_width).astype(np.int64)
+    np.clip(idx, 0, nbins - 1, out=idx)  # value == max -> last bin; outliers clamp
+    pdf = np.zeros((count, nbins), dtype=np.float64)
+    rows = np.repeat(np.arange(count), slice_size)
+    np.add.at(pdf, (rows, idx.ravel()), 1.0)
+    return pdf, bins
+
+
+def _split_z(nz: int, rank: int, size: int) -> Tuple[int, int]:
+    count = nz // size
+    start = count * rank
+    if rank == size - 1:
+        count = nz - count * (size - 1)
+    return start, count
+
+
+def _global_minmax(vi) -> Tuple[float, float]:
+    mins = [b.vmin for b in vi.blocks if b.vmin is not None]
+    maxs = [b.vmax for b in vi.blocks if b.vmax is not None]
+    return float(min(mins)), float(max(maxs))
+
+
+def run(inputs: Dict[str, object], ctx: Optional[DistContext] = None, out=sys.stdout) -> int:
+    ctx = ctx or init_from_env("cpu")
+    nbins = int(inputs["N"])
+    if nbins < 1:
+        raise ValueError("N must be >= 1")
+    writer: Optional[BP4Writer] = None
+    done = 0
+    last_progress = time.time()
+    while True:
+        reader = BP4Reader(str(inputs["input"]))
+        new = reader.steps - done
+        if writer is None and reader.steps > 0:
+            vi = reader.variables(0)["U"]
+            Lz, Ly, Lx = vi.shape
+            zs, zc = _split_z(Lz, ctx.rank, ctx.world_size)
+            if ctx.rank == 0 and os.path.isdir(str(inputs["output"])):
+                import shutil
+                shutil.rmtree(str(inputs["output"]))
+            ctx.barrier()
+            writer = BP4Writer(str(inputs["output"]), "PDFAnalysisOutput", ctx.rank, ctx.world_size)
+            writer.define_variable("step", np.int32)
+            for v in ("U", "V"):
+                writer.define_variable(f"{v}/pdf", np.float64, (Lz, nbins), (zs, 0), (zc, nbins))
+                writer.define_variable(f"{v}/bins", np.float64, (nbins,), (0,), (nbins,))
+                if inputs["output_inputdata"]:
+                    writer.define_variable(v, vi.dtype, (Lz, Ly, Lx), (zs, 0, 0), (zc, Ly, Lx))
+            if ctx.rank == 0:
+                print(f"PDF analysis reads from Simulation using engine type:  BP4", file=out)
+                print(f"PDF analysis writes using engine type:  BP4", file=out)
+        for s in range(done, reader.steps):
+            step = int(reader.read("step", s))
+            writer.begin_step()
+            writer.put("step", np.int32(step))
+            for v in ("U", "V"):
+                vi = reader.variables(s)[v]
+                vmin, vmax = _global_minmax(vi)
+                data = reader.read(v, s, (zs, 0, 0), (zc, Ly, Lx))
+                pdf, bins = compute_pdf(data, nbins, vmin, vmax)
+                writer.put(f"{v}/pdf", pdf)
+                if ctx.rank == 0:
+                    writer.put(f"{v}/bins", bins)
+                if inputs["output_inputdata"]:
+                    writer.put(v, data)
+            blobs = ctx.gather_object(writer.end_step(), dst=0)
+            if ctx.rank == 0:
+                writer.write_metadata(blobs)
+            done += 1
+            last_progress = time.time()
+        active = reader.active
+        reader.close()
+        if not inputs.get("follow") or not active:
+            break
+        if new == 0 and time.time() - last_progress > float(inputs.get("timeout", 10.0)):
+            break
+        time.sleep(1.0)
+    if writer is not None:
+        writer.close()
+    ctx.barrier()
+    return done
+
+
+def main(args: Optional[Sequence[str]] = None) -> int:
+    inputs = parse_arguments(sys.argv[1:] if args is None else args)
+    ctx = init_from_env("cpu")
+    n = run(inputs, ctx)
+    if ctx.rank == 0:
+        print(f"PDF analysis processed {n} steps", flush=True)
+    ctx.finalize()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,140 @@
+"""Application driver: the Gray-Scott time loop (reference src/GrayScott.jl).
+
+Parity:
+  * ``main(args)``      -- GrayScott.jl:68-103: settings -> init -> output stream -> loop
+                           {iterate!, step += 1, write every plotgap} -> close -> finalize
+  * ``julia_main()``    -- GrayScott.jl:40-48: catches errors, prints them, returns 1
+  * verbose line        -- GrayScott.jl:88-91 ("Simulation at step s writing output step s/plotgap",
+                           float division)
+  * no output at step 0; `steps` steps; output steps plotgap, 2*plotgap, ...
+
+Additions: checkpoint every ``checkpoint_freq`` steps and restart from ``restart_input`` (the
+reference parses these keys but ignores them, D6), a JSON-lines perf log, optional global
+diagnostics, and fault injection for restart testing (``GS_FAIL_AT_STEP=<n>`` makes every
+rank exit with status 3 right after step n has been computed and checkpointed).
+
+The loop advances in chunks up to the next output/checkpoint event, so steps between events
+run back to back in the native engine (temporal blocking, no per-step Python).
+"""
+from __future__ import annotations
+
+import os
+import sys
+import time
+import traceback
+from typing import List, Optional, Sequence
+
+from .io.checkpoint import restart as do_restart
+from .io.checkpoint import write_checkpoint
+from .io.output import SimulationOutput
+from .models.grayscott import GrayScott
+from .parallel.decomp import init_domain
+from .parallel.dist import init_from_env
+from .utils.config import Settings, get_settings, load_backend_and_lang
+from .utils.timers import PerfLog, PhaseTimer
+
+
+def initialization(args: Sequence[str]):
+    """communication.jl:15-33: settings, process group, decomposition, fields."""
+    settings = get_settings(args)
+    return initialize_from_settings(settings)
+
+
+def initialize_from_settings(settings: Settings):
+    backend, _ = load_backend_and_lang(settings)
+    ctx = init_from_env(backend)
+    domain = init_domain(settings.L, ctx.world_size, ctx.rank, periodic=settings.periodic)
+    sim = GrayScott(settings, domain, ctx)
+    sim.init_fields()
+    return ctx, settings, domain, sim
+
+
+def _next_event(step: int, settings: Settings) -> int:
+    nxt = settings.steps
+    if settings.plotgap > 0:
+        nxt = min(nxt, (step // settings.plotgap + 1) * settings.plotgap)
+    if settings.checkpoint and settings.checkpoint_freq > 0:
+        nxt = min(nxt, (step // settings.checkpoint_freq + 1) * settings.checkpoint_freq)
+    return nxt
+
+
+def run(settings: Settings, out=sys.stdout) -> dict:
+    ctx, settings, domain, sim = initialize_from_settings(settings)
+    rank = ctx.rank
+    timer = PhaseTimer(sync=sim.synchronize)
+    perf = PerfLog(settings.perf_log, enabled=(rank == 0))
+    fail_at = int(os.environ.get("GS_FAIL_AT_STEP", "-1"))
+    with timer.phase("io_init"):
+        stream = SimulationOutput(settings, domain, ctx)
+    step = 0
+    if settings.restart:
+        with timer.phase("restart"):
+            step = do_restart(sim, settings, ctx)
+        if rank == 0 and settings.verbose:
+            print(f"Restarting from step {step} ({settings.restart_input})", file=out, flush=True)
+    t_loop = time.perf_counter()
+    compute_s = 0.0
+    cells = float(domain.L[0]) * domain.L[1] * domain.L[2]
+    while step < settings.steps:
+        nxt = _next_event(step, settings)
+        t0 = time.perf_counter()
+        with timer.phase("compute"):
+            sim.iterate(nxt - step)
+        dt_c = time.perf_counter() - t0
+        compute_s += dt_c
+        nsteps = nxt - step
+        step = nxt
+        io_s = 0.0
+        if settings.plotgap > 0 and step % settings.plotgap == 0:
+            if rank == 0 and settings.verbose:
+                print(f"Simulation at step {step} writing output step "
+                      f"{step / settings.plotgap}", file=out, flush=True)
+            t1 = time.perf_counter()
+            with timer.phase("output"):
+                stream.write_step(step, sim)
+            io_s += time.perf_counter() - t1
+            if settings.diagnostics:
+                d = sim.global_stats()
+                if rank == 0:
+                    print(f"  step {step}: " + " ".join(f"{k}={v:.6g}" for k, v in d.items()),
+                          file=out, flush=True)
+        if settings.checkpoint and settings.checkpoint_freq > 0 and step % settings.checkpoint_freq == 0:
+            t1 = time.perf_counter()
+            with timer.phase("checkpoint"):
+                write_checkpoint(settings.checkpoint_output, step, sim, settings, ctx)
+            io_s += time.perf_counter() - t1
+        perf.write(step=step, steps=nsteps, compute_s=dt_c, io_s=io_s,
+                   mlups=cells * nsteps / max(dt_c, 1e-12) / 1e6, ranks=ctx.world_size)
+        if fail_at >= 0 and step >= fail_at:
+            sys.stdout.flush()
+            os._exit(3)  # simulated node failure (no clean shutdown)
+    loop_s = time.perf_counter() - t_loop
+    with timer.phase("io_close"):
+        stream.close()
+    result = {"steps": step, "loop_s": loop_s, "compute_s": compute_s,
+              "mlups_compute": cells * settings.steps / max(compute_s, 1e-12) / 1e6,
+              "timers": timer.summary(), "ranks": ctx.world_size, "fuse": sim.fuse,
+              "transport": sim.transport}
+    perf.write(summary=result)
+    perf.close()
+    sim.close()
+    ctx.finalize()
+    return result
+
+
+def main(args: Optional[Sequence[str]] = None) -> dict:
+    """GrayScott.main (GrayScott.jl:68-103)."""
+    settings = get_settings(list(sys.argv[1:] if args is None else args))
+    return run(settings)
+
+
+def julia_main(args: Optional[Sequence[str]] = None) -> int:
+    """GrayScott.julia_main (GrayScott.jl:40-48): 0 on success, 1 on error."""
+    try:
+        main(args)
+    except SystemExit as e:
+        return int(e.code or 0)
+    except BaseException:
+        traceback.print_exc()
+        return 1
+    return 0
