@@ -67,7 +67,8 @@ class GrayScott:
         self.geom = native.make_geom(nx, ny, nz, self.H, ox, oy, oz, Lx, Ly, Lz, domain.periodic)
         n = native.total_elems(self.geom)
         tdt = _TORCH_DTYPES[self.dtype]
-        self.buffers = [torch.empty(2 * n, dtype=tdt, device=self.device) for _ in range(2)]
+        # zeroed once so the row padding never holds garbage (it is never read for valid cells)
+        self.buffers = [torch.zeros(2 * n, dtype=tdt, device=self.device) for _ in range(2)]
         scells, rcells = native.plan_sizes(self.geom, domain.nbr27, self.H > 1)
         self.sendbuf = torch.empty(max(2 * scells, 2), dtype=tdt, device=self.device)
         self.recvbuf = torch.empty(max(2 * rcells, 2), dtype=tdt, device=self.device)

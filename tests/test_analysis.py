@@ -1,0 +1,93 @@
+"""PDF analysis (working version of the reference stub src/analysis/pdfcalc.jl), plot and
+bpls tools.  Argument parsing mirrors test/unit/analysis/unit-pdfcalc.jl."""
+import os
+
+import numpy as np
+import pytest
+
+from grayscott_amd.analysis.pdf import compute_pdf, parse_arguments, run
+from grayscott_amd.io.bp4 import BP4Reader
+from grayscott_amd.io.bpls import listing
+from grayscott_amd.io.output import SimulationOutput
+from grayscott_amd.parallel.decomp import init_domain
+from grayscott_amd.plot import decomp as pdecomp
+from grayscott_amd.plot import gsplot
+from grayscott_amd.utils.config import Settings
+
+from .mp_utils import ROOT
+
+
+def test_parse_arguments_like_reference():
+    a = parse_arguments(["foo.bp", "bar.bp", "1500"])
+    assert (a["input"], a["output"], a["N"], a["output_inputdata"]) == ("foo.bp", "bar.bp", 1500, False)
+    a = parse_arguments(["input.bp", "output.bp", "1000", "true"])
+    assert (a["input"], a["output"], a["N"], a["output_inputdata"]) == ("input.bp", "output.bp", 1000, True)
+    a = parse_arguments(["i.bp", "o.bp"])
+    assert a["N"] == 1000 and a["output_inputdata"] is False
+
+
+def test_compute_pdf_matches_numpy_histogram():
+    rng = np.random.default_rng(0)
+    data = rng.random((5, 8, 9))
+    vmin, vmax = float(data.min()), float(data.max())
+    pdf, bins = compute_pdf(data, 17, vmin, vmax)
+    assert pdf.shape == (5, 17) and bins.shape == (17,)
+    for c in range(5):
+        h, edges = np.histogram(data[c], bins=17, range=(vmin, vmax))
+        np.testing.assert_array_equal(pdf[c], h)
+    np.testing.assert_allclose(bins, edges[:-1])
+    assert pdf.sum() == data.size
+
+
+def test_compute_pdf_degenerate():
+    pdf, bins = compute_pdf(np.ones((2, 3, 3)), 4, 1.0, 1.0)
+    assert (pdf == 9).all()
+    pdf, _ = compute_pdf(np.ones((2, 3, 3)), 1, 0.0, 2.0)
+    assert (pdf == 9).all()
+
+
+@pytest.fixture()
+def sim_file(tmp_path):
+    s = Settings(L=16, precision="Float64", output=str(tmp_path / "gs.bp"))
+    dom = init_domain(16, 1, 0)
+    out = SimulationOutput(s, dom)
+    rng = np.random.default_rng(5)
+    for step in (10, 20):
+        u = rng.random((16, 16, 16))
+        out.write_fields(step, u, 1 - u)
+    out.close()
+    return s.output
+
+
+def test_pdf_tool_end_to_end(sim_file, tmp_path):
+    outp = str(tmp_path / "pdf.bp")
+    n = run({"input": sim_file, "output": outp, "N": 32, "output_inputdata": True,
+             "follow": False, "timeout": 1.0})
+    assert n == 2
+    with BP4Reader(sim_file) as src, BP4Reader(outp) as r:
+        assert r.steps == 2 and r.read("step", 1) == 20
+        u = src.read("U", 1)
+        pdf = r.read("U/pdf", 1)
+        ref, _ = compute_pdf(u, 32, float(u.min()), float(u.max()))
+        np.testing.assert_array_equal(pdf, ref)
+        np.testing.assert_array_equal(r.read("U", 1), u)
+        assert r.read("V/bins", 0).shape == (32,)
+        assert r.process_groups(0)[0]["io"] == "PDFAnalysisOutput"
+
+
+def test_plot_and_listing_tools(sim_file, tmp_path):
+    png = str(tmp_path / "v.png")
+    assert gsplot.main([sim_file, "--var", "U", "-o", png]) == 0
+    assert os.path.getsize(png) > 100
+    assert gsplot.main([sim_file, "--all", "--axis", "y", "-o", png]) == 0
+    sl = gsplot.read_slice(sim_file, "U", 0, "x", 3)
+    with BP4Reader(sim_file) as r:
+        np.testing.assert_array_equal(sl, r.read("U", 0)[:, :, 3])
+    txt = listing(sim_file, attrs=True, decomp=True)
+    assert "U" in txt and "Fides_Data_Model" in txt and "block" in txt
+    blocks = pdecomp.blocks_from_domains(30, 6)
+    own = pdecomp.owner_slice(blocks, (30, 30, 30), 15)
+    assert (own >= 0).all() and len(np.unique(own)) == 6
+    fb, shape = pdecomp.blocks_from_file(sim_file)
+    assert shape == (16, 16, 16) and fb[0]["count_xyz"] == (16, 16, 16)
+    assert pdecomp.main(["12", "4", "--png", str(tmp_path / "d.png")]) == 0

@@ -1,0 +1,108 @@
+"""Functional CLI runs (reference test/functional/functional-GrayScott.jl: `mpirun -n 4` of the
+CPU configs, exit code 0) plus checkpoint/restart and fault-injection scenarios.  Ranks are
+launched with torchrun on 127.0.0.1 (gloo control plane)."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from grayscott_amd.io.bp4 import BP4Reader
+from grayscott_amd.utils.config import get_settings, write_settings_toml
+
+from .mp_utils import ROOT, free_port
+
+FUNC = os.path.join(ROOT, "tests", "functional")
+
+
+def launch(cfg_path, nprocs, cwd, env=None, timeout=600):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node",
+           str(nprocs), "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(ROOT, "gray-scott.py"), cfg_path]
+    e = dict(os.environ)
+    e["OMP_NUM_THREADS"] = "1"
+    e.update(env or {})
+    return subprocess.run(cmd, cwd=cwd, env=e, capture_output=True, text=True, timeout=timeout)
+
+
+def _cfg(tmp_path, name, **kw):
+    s = get_settings([os.path.join(FUNC, "config_cpu_plain.toml")])
+    for k, v in kw.items():
+        setattr(s, k, v)
+    p = str(tmp_path / name)
+    write_settings_toml(s, p)
+    return p
+
+
+@pytest.mark.parametrize("cfg", ["config_cpu_plain.toml", "config_cpu_ka.toml"])
+def test_functional_4_ranks(cfg, tmp_path):
+    r = launch(os.path.join(FUNC, cfg), 4, str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    with BP4Reader(str(tmp_path / "gs-4ranks-64L-F32.bp")) as rd:
+        assert rd.steps == 100
+        assert [rd.read("step", i) for i in (0, 1, 99)] == [10, 20, 1000]
+        assert len(rd.variables(0)["U"].blocks) == 4
+        u = rd.read("U", -1)
+        assert np.isfinite(u).all() and u.shape == (64, 64, 64)
+
+
+def test_decomposition_invariant_output(tmp_path):
+    out = {}
+    for n in (1, 3):
+        d = tmp_path / f"r{n}"
+        d.mkdir()
+        cfg = _cfg(d, "c.toml", steps=30, plotgap=15, L=24, output="o.bp")
+        r = launch(cfg, n, str(d))
+        assert r.returncode == 0, r.stderr[-3000:]
+        with BP4Reader(str(d / "o.bp")) as rd:
+            out[n] = (rd.read("U", -1), rd.read("V", -1))
+    np.testing.assert_array_equal(out[1][0], out[3][0])
+    np.testing.assert_array_equal(out[1][1], out[3][1])
+
+
+def test_checkpoint_restart_bitwise(tmp_path):
+    """Run 40 steps straight vs 20 steps + restart (with a different rank count) to 40."""
+    full = tmp_path / "full"
+    full.mkdir()
+    r = launch(_cfg(full, "c.toml", L=24, steps=40, plotgap=20, output="o.bp"), 2, str(full))
+    assert r.returncode == 0, r.stderr[-3000:]
+    part = tmp_path / "part"
+    part.mkdir()
+    r = launch(_cfg(part, "a.toml", L=24, steps=20, plotgap=20, output="a.bp", checkpoint=True,
+                    checkpoint_freq=20, checkpoint_output="ck.bp"), 2, str(part))
+    assert r.returncode == 0, r.stderr[-3000:]
+    with BP4Reader(str(part / "ck.bp")) as ck:
+        assert ck.read("step") == 20
+        assert ck.process_groups(0)[0]["io"] == "SimulationCheckpoint"
+    r = launch(_cfg(part, "b.toml", L=24, steps=40, plotgap=20, output="b.bp", restart=True,
+                    restart_input="ck.bp"), 3, str(part))
+    assert r.returncode == 0, r.stderr[-3000:]
+    with BP4Reader(str(full / "o.bp")) as a, BP4Reader(str(part / "b.bp")) as b:
+        assert b.steps == 1 and b.read("step", 0) == 40
+        np.testing.assert_array_equal(a.read("U", -1), b.read("U", -1))
+        np.testing.assert_array_equal(a.read("V", -1), b.read("V", -1))
+
+
+def test_fault_injection_and_recovery(tmp_path):
+    """A run killed after step 30 resumes from its last checkpoint (step 30) and ends with the
+    same state as an uninterrupted run."""
+    ref = tmp_path / "ref"
+    ref.mkdir()
+    r = launch(_cfg(ref, "c.toml", L=20, steps=50, plotgap=50, output="o.bp"), 2, str(ref))
+    assert r.returncode == 0, r.stderr[-3000:]
+    run = tmp_path / "run"
+    run.mkdir()
+    cfg = _cfg(run, "c.toml", L=20, steps=50, plotgap=50, output="o.bp", checkpoint=True,
+               checkpoint_freq=10, checkpoint_output="ck.bp")
+    r = launch(cfg, 2, str(run), env={"GS_FAIL_AT_STEP": "30"})
+    assert r.returncode != 0
+    with BP4Reader(str(run / "ck.bp")) as ck:
+        assert ck.read("step") == 30
+    cfg2 = _cfg(run, "c2.toml", L=20, steps=50, plotgap=50, output="o.bp", checkpoint=True,
+                checkpoint_freq=10, checkpoint_output="ck.bp", restart=True, restart_input="ck.bp")
+    r = launch(cfg2, 2, str(run))
+    assert r.returncode == 0, r.stderr[-3000:]
+    with BP4Reader(str(ref / "o.bp")) as a, BP4Reader(str(run / "o.bp")) as b:
+        np.testing.assert_array_equal(a.read("U", -1), b.read("U", -1))
+        np.testing.assert_array_equal(a.read("V", -1), b.read("V", -1))

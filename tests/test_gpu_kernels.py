@@ -119,3 +119,30 @@ def test_stats_and_determinism():
     assert abs(s[0] - u.astype(np.float64).sum()) < 1e-3 * u.size
     assert s[1] == pytest.approx(float(u.min()))
     assert s[5] == pytest.approx(float(v.max()))
+
+
+def test_gpu_cli_run(tmp_path):
+    """The reference CUDA job configuration (scripts/job_*: 1 rank, 1 GPU) on the HIP backend."""
+    import os
+    import subprocess
+    import sys
+
+    from grayscott_amd.io.bp4 import BP4Reader
+    from grayscott_amd.utils.config import get_settings, write_settings_toml
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    s = get_settings([os.path.join(root, "tests", "functional", "config_amdgpu.toml")])
+    s.steps, s.plotgap, s.checkpoint, s.checkpoint_freq = 200, 50, True, 100
+    s.output, s.checkpoint_output = str(tmp_path / "gs.bp"), str(tmp_path / "ck.bp")
+    cfg = str(tmp_path / "c.toml")
+    write_settings_toml(s, cfg)
+    r = subprocess.run([sys.executable, os.path.join(root, "gray-scott.py"), cfg],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    with BP4Reader(s.output) as rd:
+        assert rd.steps == 4 and rd.read("step", 3) == 200
+        u = rd.read("U", -1)
+    c = _sim("CPU", 64, "Float32", 0.1, fuse=1, steps=200, seed=s.seed)
+    assert np.abs(u - c.get_fields()[0]).max() < 1e-3
+    with BP4Reader(s.checkpoint_output) as ck:
+        assert ck.read("step") == 200

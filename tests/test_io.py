@@ -1,0 +1,171 @@
+"""BP4 writer/reader and the SimulationOutput schema (reference src/simulation/IO.jl; the
+reference's own unit-IO.jl is disabled/stale, D11).  There is no libadios2 in this environment:
+the C++ writer is checked against the independent Python reader, golden header bytes and a
+byte-level walk of the data subfiles."""
+import os
+import struct
+
+import numpy as np
+import pytest
+
+from grayscott_amd.io.bp4 import BP4Error, BP4Reader, BP4Writer
+from grayscott_amd.io.output import SimulationOutput, vtk_schema
+from grayscott_amd.parallel.decomp import init_domain
+from grayscott_amd.utils.config import Settings
+
+from .mp_utils import ROOT
+
+
+def _write(path, steps=3, shape=(4, 5, 6), dtype=np.float32):
+    w = BP4Writer(path, "TestIO", 0, 1)
+    w.define_attribute("F", 0.02)
+    w.define_attribute("arr", [1.0, 2.0, 3.0])
+    w.define_attribute("name", "uniform")
+    w.define_attribute("list", ["U", "V"])
+    w.define_variable("step", np.int32)
+    w.define_variable("A", dtype, shape, (0, 0, 0), shape)
+    data = []
+    for s in range(steps):
+        w.begin_step()
+        w.put("step", np.int32(s * 10))
+        a = (np.arange(np.prod(shape)).reshape(shape) + 100 * s).astype(dtype)
+        data.append(a)
+        w.put("A", a)
+        w.write_metadata([w.end_step()])
+    w.close()
+    return data
+
+
+def test_header_bytes(tmp_path):
+    p = str(tmp_path / "h.bp")
+    _write(p, 1)
+    for fname, kind in (("data.0", b"D"), ("md.0", b"M"), ("md.idx", b"I")):
+        with open(os.path.join(p, fname), "rb") as fh:
+            h = fh.read(64)
+        assert h[:16] == b"ADIOS-BP v2.10.2"
+        assert h[31:32] == kind
+        assert h[32:35] == b"212"
+        assert h[36] == 0 and h[37] == 4 and h[39] == 2
+    with open(os.path.join(p, "md.idx"), "rb") as fh:
+        idx = fh.read()
+    assert idx[38] == 0  # closed writer -> index table inactive
+    assert (len(idx) - 64) % 64 == 0
+
+
+def test_roundtrip_steps_attributes_selection(tmp_path):
+    p = str(tmp_path / "r.bp")
+    data = _write(p, 3)
+    with BP4Reader(p) as r:
+        assert r.steps == 3
+        assert r.attributes["F"] == 0.02
+        np.testing.assert_array_equal(r.attributes["arr"], [1.0, 2.0, 3.0])
+        assert r.attributes["name"] == "uniform"
+        assert r.attributes["list"] == ["U", "V"]
+        for s in range(3):
+            assert r.read("step", s) == 10 * s
+            np.testing.assert_array_equal(r.read("A", s), data[s])
+        np.testing.assert_array_equal(r.read("A", 1, (1, 2, 3), (2, 2, 2)), data[1][1:3, 2:4, 3:5])
+        vi = r.variables(2)["A"]
+        assert vi.blocks[0].vmin == data[2].min() and vi.blocks[0].vmax == data[2].max()
+        assert r.process_groups(1)[0]["step"] == 2
+        with pytest.raises(BP4Error):
+            r.read("nope")
+
+
+def test_fp64_and_multiple_blocks(tmp_path):
+    p = str(tmp_path / "m.bp")
+    shape = (6, 4, 4)
+    full = np.random.default_rng(0).random(shape)
+    w = BP4Writer(p, "Blocks", 0, 1)
+    w.define_variable("X", np.float64, shape, (0, 0, 0), (3, 4, 4))
+    w.begin_step()
+    w.put("X", full[:3])
+    w.set_selection("X", (3, 0, 0), (3, 4, 4))
+    w.put("X", full[3:])
+    w.write_metadata([w.end_step()])
+    w.close()
+    with BP4Reader(p) as r:
+        assert len(r.variables(0)["X"].blocks) == 2
+        np.testing.assert_array_equal(r.read("X"), full)
+        np.testing.assert_array_equal(r.read("X", 0, (2, 1, 0), (2, 3, 4)), full[2:4, 1:4, :])
+
+
+def _walk_data_file(path):
+    """Parse every process group of a data subfile; returns [(step, nvars, [var names])]."""
+    with open(path, "rb") as fh:
+        buf = fh.read()
+    pos, out = 64, []
+    while pos < len(buf):
+        pglen = struct.unpack_from("<Q", buf, pos)[0]
+        end = pos + 8 + pglen
+        p = pos + 8 + 1
+        n = struct.unpack_from("<H", buf, p)[0]
+        p += 2 + n + 4
+        n = struct.unpack_from("<H", buf, p)[0]
+        p += 2 + n
+        step = struct.unpack_from("<I", buf, p)[0]
+        p += 4
+        nmeth = buf[p]
+        mlen = struct.unpack_from("<H", buf, p + 1)[0]
+        p += 3 + mlen
+        assert mlen == 3 * nmeth
+        nvars, vlen = struct.unpack_from("<IQ", buf, p)
+        p += 12
+        vend = p + vlen
+        names = []
+        for _ in range(nvars):
+            vl = struct.unpack_from("<Q", buf, p)[0]
+            q = p + 8 + 4
+            n = struct.unpack_from("<H", buf, q)[0]
+            names.append(buf[q + 2:q + 2 + n].decode())
+            p += 8 + vl
+        assert p == vend
+        natt, alen = struct.unpack_from("<IQ", buf, p)
+        p += 12
+        for _ in range(natt):
+            al = struct.unpack_from("<I", buf, p)[0]
+            assert buf[p:p + al].find(b"[AMD") > 0 and buf[p + al - 4:p + al] == b"AMD]"
+            p += al
+        assert p == end, (p, end)
+        out.append((step, nvars, names, natt))
+        pos = end
+    return out
+
+
+def test_data_subfile_structure(tmp_path):
+    p = str(tmp_path / "d.bp")
+    _write(p, 2)
+    pgs = _walk_data_file(os.path.join(p, "data.0"))
+    assert [(s, n, names) for s, n, names, _ in pgs] == [(1, 2, ["step", "A"]), (2, 2, ["step", "A"])]
+    assert pgs[0][3] == 4 and pgs[1][3] == 0  # attributes only with the first step
+
+
+def test_simulation_output_schema(tmp_path):
+    s = Settings(L=12, precision="Float32", output=str(tmp_path / "gs.bp"), noise=0.1)
+    dom = init_domain(12, 1, 0)
+    out = SimulationOutput(s, dom)
+    u = np.random.default_rng(1).random((12, 12, 12)).astype(np.float32)
+    out.write_fields(10, u, 1 - u)
+    out.write_fields(20, u * 2, u)
+    out.close()
+    with BP4Reader(s.output) as r:
+        a = r.attributes
+        for key, val in (("F", 0.04), ("k", 0.0), ("dt", 0.2), ("Du", 0.05), ("Dv", 0.1),
+                         ("noise", 0.1)):
+            assert a[key] == pytest.approx(val)
+        assert a["Fides_Data_Model"] == "uniform"
+        np.testing.assert_array_equal(a["Fides_Origin"], [0, 0, 0])
+        np.testing.assert_array_equal(a["Fides_Spacing"], [0.1, 0.1, 0.1])
+        assert a["Fides_Dimension_Variable"] == "U"
+        assert a["Fides_Variable_List"] == ["U", "V"]
+        assert a["Fides_Variable_Associations"] == ["points", "points"]
+        assert 'WholeExtent="0 12 0 12 0 12"' in a["vtk.xml"] and "TIME" in a["vtk.xml"]
+        assert [r.read("step", i) for i in range(2)] == [10, 20]
+        assert r.variables(0)["U"].dtype == np.float32
+        assert r.variables(0)["U"].shape == (12, 12, 12)
+        np.testing.assert_array_equal(r.read("V", 0), 1 - u)
+        assert r.process_groups(0)[0]["io"] == "SimulationOutput"
+
+
+def test_vtk_schema_extent():
+    assert 'Extent="0 64 0 64 0 64"' in vtk_schema(64)
