@@ -83,7 +83,8 @@ def main(argv=None) -> int:
     if ctx.rank == 0:
         dims = "x".join(str(d) for d in dom.dims)
         rec = {
-            "metric": "MLUPS (cell-updates/sec, whole node) at L=512 fp32",
+            "metric": f"MLUPS (cell-updates/sec, whole node) at L={args.L} "
+                      f"{'fp32' if settings.dtype_name == 'float32' else 'fp64'}",
             "value": round(mlups, 1),
             "unit": "MLUPS",
             "n_gpus": ctx.world_size if backend == "hip" else 0,

@@ -339,7 +339,7 @@ inline int fused_cfg_env() {
     if (e) {
       static const char* names[] = {"",      "4x8:1",   "4x8:2",   "4x8:4",  "8x4:1",
                                     "8x4:2", "4x16:2",  "8x8:2",   "4x8:3",  "8x4:2w3",
-                                    "8x4:1w3", "4x8:2w4", "8x4:3"};
+                                    "8x4:1w3", "4x8:2w4", "8x4:3", "4x6:2", "4x12:2", "4x4:2", "4x12:3"};
       for (int i = 1; i < (int)(sizeof(names) / sizeof(names[0])); ++i)
         if (!strcmp(e, names[i])) v = i;
     }
@@ -363,6 +363,10 @@ void run_fused_cfg(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, c
       case 10: FusedLaunch<FCfg<T, TL, 8, 4, 1, PER, NZ, 3>, T>::run(s, d, a, p, st); return;
       case 11: FusedLaunch<FCfg<T, TL, 4, 8, 2, PER, NZ, 4>, T>::run(s, d, a, p, st); return;
       case 12: FusedLaunch<FCfg<T, TL, 8, 4, 3, PER, NZ>, T>::run(s, d, a, p, st); return;
+      case 13: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
+      case 14: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
+      case 15: FusedLaunch<FCfg<T, TL, 4, 4, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
+      case 16: FusedLaunch<FCfg<T, TL, 4, 12, 3, PER, NZ>, T>::run(s, d, a, p, st); return;
       default: break;
     }
   }
