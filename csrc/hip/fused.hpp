@@ -51,10 +51,14 @@ inline FoldCoef<T> make_fold(const gs::Params& p) {
 typedef unsigned int gs_u2 __attribute__((ext_vector_type(2)));
 typedef unsigned int gs_u4 __attribute__((ext_vector_type(4)));
 
+// Descriptor for the plane starting `off_bytes` into a buffer of `total_bytes`.  The range is
+// empty when the plane is disabled (total_bytes == 0) or starts outside the buffer, so every
+// access through it is dropped (loads return 0) -- never a wild address.
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const void* base, int64_t off_bytes,
                                                              int64_t total_bytes) {
   const int64_t rem = total_bytes - off_bytes;
-  const int nrec = (int)(rem > 0x7ffffff0LL ? 0x7ffffff0LL : (rem < 0 ? 0 : rem));
+  const bool inside = total_bytes > 0 && off_bytes >= 0 && rem > 0;
+  const int nrec = inside ? (int)(rem > 0x7ffffff0LL ? 0x7ffffff0LL : rem) : 0;
   return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)base + off_bytes), 0, nrec,
                                            0x00020000);
 }
@@ -85,15 +89,21 @@ __device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, int voff, int s
 // Compile-time configuration of one fused-kernel instantiation.
 //   ROWS x WAVES : rows per wave x waves per workgroup (tile height = ROWS*WAVES)
 //   PF           : level-0 prefetch distance in planes (register ring of PF+2 planes)
+//   SKEW         : level l consumes level l-1's output of the previous iteration, so all
+//                  levels share ONE workgroup barrier per plane (output ring of 3)
+constexpr int gs_gcd(int a, int b) { return b == 0 ? a : gs_gcd(b, a % b); }
+constexpr int gs_lcm(int a, int b) { return a / gs_gcd(a, b) * b; }
+
 template <typename T, int TL_, int ROWS_, int WAVES_, int PF_, bool PERIODIC_, bool NOISE_,
-          int MINW_ = 1>
+          int MINW_ = 1, bool SKEW_ = false>
 struct FCfg {
   static constexpr int MINW = MINW_;  // __launch_bounds__ min waves per SIMD
   using V2 = typename Vec2<T>::type;
   static constexpr int TL = TL_, ROWS = ROWS_, WAVES = WAVES_, PF = PF_;
-  static constexpr bool PERIODIC = PERIODIC_, NOISE = NOISE_;
-  static constexpr int R = PF + 2;                          // level-0 ring slots
-  static constexpr int PERIOD = (R % 2 == 0) ? R : 2 * R;  // lcm(R, 2)
+  static constexpr bool PERIODIC = PERIODIC_, NOISE = NOISE_, SKEW = SKEW_;
+  static constexpr int R = PF + 2;                    // level-0 ring slots
+  static constexpr int NS = SKEW ? 3 : 2;             // level-l output ring / xch buffers
+  static constexpr int PERIOD = gs_lcm(R, NS);
   static constexpr int NO = TL > 1 ? TL - 1 : 1;
 };
 
@@ -101,13 +111,13 @@ template <class C>
 struct FusedState {
   using V2 = typename C::V2;
   V2 LD[C::R][C::ROWS];
-  V2 OUT[C::NO][2][C::ROWS];
+  V2 OUT[C::NO][C::NS][C::ROWS];
   V2 A[C::TL][C::ROWS];
 };
 
 // Per-segment constants (wave-uniform values and the lane's offsets).
 struct FusedSeg {
-  int p, pend, z0;
+  int p, pend, ldend, z0;
   int lane, wave;
   int voff, svoff, pitchb;
   int srow0, srow1;
@@ -121,36 +131,56 @@ __device__ __forceinline__ int64_t gwrap(int64_t v, int64_t L) {
   else return v;
 }
 
-// One pipeline iteration p (i = p - pstart).  IR = i % R, I2 = i % 2.
-template <class C, typename T, int IR, int I2>
+// One pipeline iteration p (i = p - pstart).  IR = i % R, IS = i % NS.
+// Non-skewed: level l+1 is computed from level l of the SAME iteration (one barrier per level).
+// Skewed: level l+1 consumes level l's output of the PREVIOUS iteration, so every level's
+// input rows are published before a single barrier; level l produces plane p - (2l + 1).
+template <class C, typename T, int IR, int IS>
 __device__ __forceinline__ void fused_iter(FusedState<C>& S,
-                                           typename C::V2 (*xch)[2][C::WAVES][2][64],
+                                           typename C::V2 (*xch)[C::NS][C::WAVES][2][64],
                                            const FusedArgs& a, const FoldCoef<T>& f,
                                            uint64_t seed, const typename C::V2* src,
                                            typename C::V2* dst, const FusedSeg& sg) {
   using V2 = typename C::V2;
-  constexpr int ROWS = C::ROWS, WAVES = C::WAVES, TL = C::TL;
+  constexpr int ROWS = C::ROWS, WAVES = C::WAVES, TL = C::TL, NS = C::NS;
   const Geom& g = a.g;
   const int p = sg.p;
   const int64_t PZB = gs::plane_elems(g) * (int64_t)sizeof(V2);
-  // prefetch level-0 plane p+PF into the ring slot of plane p-2
-  if (p + C::PF < sg.pend) {
-    const __amdgpu_buffer_rsrc_t r = plane_rsrc(src, (int64_t)(p + C::PF + g.H) * PZB, a.buf_bytes);
+  // prefetch level-0 plane p+PF into the ring slot of plane p-2.  Issued unconditionally
+  // (an empty descriptor past the segment) so every iteration has the same VMEM count and
+  // the compiler's s_waitcnt vmcnt(N) can leave the prefetch in flight.
+  {
+    const bool pf_ok = p + C::PF < sg.ldend;
+    const __amdgpu_buffer_rsrc_t r =
+        plane_rsrc(src, (int64_t)(p + C::PF + g.H) * PZB, pf_ok ? a.buf_bytes : 0);
 #pragma unroll
     for (int j = 0; j < ROWS; ++j)
       S.LD[(IR + C::PF) % C::R][j] = bload(r, sg.voff + j * sg.pitchb, 0, (V2*)nullptr);
   }
+  if constexpr (C::SKEW) {
+#pragma unroll
+    for (int l = 0; l < TL; ++l) {
+      const V2* in = l == 0 ? S.LD[IR] : S.OUT[l == 0 ? 0 : l - 1][(IS + NS - 1) % NS];
+      xch[l][IS][sg.wave][0][sg.lane] = in[0];
+      xch[l][IS][sg.wave][1][sg.lane] = in[ROWS - 1];
+    }
+    __syncthreads();
+  }
 #pragma unroll
   for (int l = 0; l < TL; ++l) {
-    // input plane of level l (plane p-l) and the centre plane p-l-1
-    V2* in = l == 0 ? S.LD[IR] : S.OUT[l == 0 ? 0 : l - 1][I2];
-    V2* Cc = l == 0 ? S.LD[(IR + C::R - 1) % C::R] : S.OUT[l == 0 ? 0 : l - 1][1 - I2];
-    xch[l][I2][sg.wave][0][sg.lane] = in[0];
-    xch[l][I2][sg.wave][1][sg.lane] = in[ROWS - 1];
-    __syncthreads();
-    const V2 up = sg.wave > 0 ? xch[l][I2][sg.wave - 1][1][sg.lane] : in[0];
-    const V2 dn = sg.wave < WAVES - 1 ? xch[l][I2][sg.wave + 1][0][sg.lane] : in[ROWS - 1];
-    const int q = p - l - 1;  // plane produced by level l+1
+    // input plane of consumer l and the centre plane one before it
+    constexpr int kIn = C::SKEW ? (IS + NS - 1) % NS : IS;
+    constexpr int kC = C::SKEW ? (IS + NS - 2) % NS : (IS + NS - 1) % NS;
+    V2* in = l == 0 ? S.LD[IR] : S.OUT[l == 0 ? 0 : l - 1][kIn];
+    V2* Cc = l == 0 ? S.LD[(IR + C::R - 1) % C::R] : S.OUT[l == 0 ? 0 : l - 1][kC];
+    if constexpr (!C::SKEW) {
+      xch[l][IS][sg.wave][0][sg.lane] = in[0];
+      xch[l][IS][sg.wave][1][sg.lane] = in[ROWS - 1];
+      __syncthreads();
+    }
+    const V2 up = sg.wave > 0 ? xch[l][IS][sg.wave - 1][1][sg.lane] : in[0];
+    const V2 dn = sg.wave < WAVES - 1 ? xch[l][IS][sg.wave + 1][0][sg.lane] : in[ROWS - 1];
+    const int q = C::SKEW ? p - (2 * l + 1) : p - l - 1;  // plane produced by level l+1
     const int64_t gz = gwrap<C>(g.oz + q, g.Lz);
     const uint64_t tstep = (uint64_t)(a.t + l);
     V2 res[ROWS];
@@ -198,11 +228,12 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
         }
       }
 #pragma unroll
-      for (int j = 0; j < ROWS; ++j) S.OUT[l][I2][j] = res[j];
+      for (int j = 0; j < ROWS; ++j) S.OUT[l][IS][j] = res[j];
     } else {
-      const int zs = p - TL;
-      if (zs >= sg.z0) {
-        const __amdgpu_buffer_rsrc_t w = plane_rsrc(dst, (int64_t)(zs + g.H) * PZB, a.buf_bytes);
+      {  // unconditional stores: planes before the segment go to an empty descriptor
+        const bool st_ok = q >= sg.z0;
+        const __amdgpu_buffer_rsrc_t w =
+            plane_rsrc(dst, (int64_t)(q + g.H) * PZB, st_ok ? a.buf_bytes : 0);
 #pragma unroll
         for (int j = 0; j < ROWS; ++j) {
           const int off = (j >= sg.srow0 && j < sg.srow1) ? sg.svoff + j * sg.pitchb : (int)0x80000000;
@@ -216,14 +247,14 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
 // Unrolled walk over one ring period; returns false when the segment is done.
 template <class C, typename T, int I>
 __device__ __forceinline__ bool fused_period(FusedState<C>& S,
-                                             typename C::V2 (*xch)[2][C::WAVES][2][64],
+                                             typename C::V2 (*xch)[C::NS][C::WAVES][2][64],
                                              const FusedArgs& a, const FoldCoef<T>& f,
                                              uint64_t seed, const typename C::V2* src,
                                              typename C::V2* dst, FusedSeg& sg) {
   if constexpr (I == C::PERIOD) {
     return true;
   } else {
-    fused_iter<C, T, I % C::R, I % 2>(S, xch, a, f, seed, src, dst, sg);
+    fused_iter<C, T, I % C::R, I % C::NS>(S, xch, a, f, seed, src, dst, sg);
     if (++sg.p >= sg.pend) return false;
     return fused_period<C, T, I + 1>(S, xch, a, f, seed, src, dst, sg);
   }
@@ -237,7 +268,7 @@ __global__ __launch_bounds__(64 * C::WAVES, C::MINW) void k_fused(const typename
   using V2 = typename C::V2;
   constexpr int ROWS = C::ROWS, WAVES = C::WAVES, TL = C::TL;
   static_assert(ROWS % 4 == 0, "rows per wave must hold whole noise quads");
-  __shared__ V2 xch[TL][2][WAVES][2][64];  // [level][parity][wave][first/last row][lane]
+  __shared__ V2 xch[TL][C::NS][WAVES][2][64];  // [level][ring][wave][first/last row][lane]
   const Geom& g = a.g;
   FusedSeg sg;
   sg.lane = threadIdx.x & 63;
@@ -279,12 +310,14 @@ __global__ __launch_bounds__(64 * C::WAVES, C::MINW) void k_fused(const typename
 #pragma unroll
       for (int j = 0; j < ROWS; ++j) S.A[l][j].x = S.A[l][j].y = (T)0;
     sg.p = z0 - TL;
-    sg.pend = z1 + TL;
+    sg.ldend = z1 + TL;
+    sg.pend = C::SKEW ? z1 + 2 * TL - 1 : z1 + TL;
     const int64_t PZB = gs::plane_elems(g) * (int64_t)sizeof(V2);
 #pragma unroll
     for (int k = 0; k < C::PF; ++k) {
-      if (sg.p + k < sg.pend) {
-        const __amdgpu_buffer_rsrc_t r = plane_rsrc(s, (int64_t)(sg.p + k + g.H) * PZB, a.buf_bytes);
+      {
+        const __amdgpu_buffer_rsrc_t r = plane_rsrc(
+            s, (int64_t)(sg.p + k + g.H) * PZB, sg.p + k < sg.ldend ? a.buf_bytes : 0);
 #pragma unroll
         for (int j = 0; j < ROWS; ++j) S.LD[k][j] = bload(r, sg.voff + j * sg.pitchb, 0, (V2*)nullptr);
       }
@@ -339,7 +372,8 @@ inline int fused_cfg_env() {
     if (e) {
       static const char* names[] = {"",      "4x8:1",   "4x8:2",   "4x8:4",  "8x4:1",
                                     "8x4:2", "4x16:2",  "8x8:2",   "4x8:3",  "8x4:2w3",
-                                    "8x4:1w3", "4x8:2w4", "8x4:3", "4x6:2", "4x12:2", "4x4:2", "4x12:3"};
+                                    "8x4:1w3", "4x8:2w4", "8x4:3", "4x6:2", "4x12:2", "4x4:2", "4x12:3",
+                                    "8x4:1s", "8x4:4s", "4x8:1s", "4x8:4s"};
       for (int i = 1; i < (int)(sizeof(names) / sizeof(names[0])); ++i)
         if (!strcmp(e, names[i])) v = i;
     }
@@ -367,12 +401,21 @@ void run_fused_cfg(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, c
       case 14: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
       case 15: FusedLaunch<FCfg<T, TL, 4, 4, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
       case 16: FusedLaunch<FCfg<T, TL, 4, 12, 3, PER, NZ>, T>::run(s, d, a, p, st); return;
+      case 17: FusedLaunch<FCfg<T, TL, 8, 4, 1, PER, NZ, 1, true>, T>::run(s, d, a, p, st); return;
+      case 18: FusedLaunch<FCfg<T, TL, 8, 4, 4, PER, NZ, 1, true>, T>::run(s, d, a, p, st); return;
+      case 19: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, 1, true>, T>::run(s, d, a, p, st); return;
+      case 20: FusedLaunch<FCfg<T, TL, 4, 8, 4, PER, NZ, 1, true>, T>::run(s, d, a, p, st); return;
       default: break;
     }
   }
-  // measured defaults (L=512, MI355X): fp32 8x4 tile with a 2-plane prefetch; fp64 4x8
-  if constexpr (sizeof(T) == 4) FusedLaunch<FCfg<T, TL, 8, 4, 2, PER, NZ>, T>::run(s, d, a, p, st);
-  else FusedLaunch<FCfg<T, TL, 4, 8, 2, PER, NZ>, T>::run(s, d, a, p, st);
+  // measured defaults (L=512, MI355X, profiles/r1_tune_*): fp32 T=2 -> 8x4 tile with a 3-plane
+  // prefetch, T=3 -> 4x12 tile with a 2-plane prefetch; fp64 -> 4x8
+  if constexpr (sizeof(T) == 4) {
+    if constexpr (TL == 2) FusedLaunch<FCfg<T, TL, 8, 4, 3, PER, NZ>, T>::run(s, d, a, p, st);
+    else FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ>, T>::run(s, d, a, p, st);
+  } else {
+    FusedLaunch<FCfg<T, TL, 4, 8, 2, PER, NZ>, T>::run(s, d, a, p, st);
+  }
 }
 
 template <typename T, int TL>

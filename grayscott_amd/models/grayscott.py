@@ -36,7 +36,7 @@ def default_fuse(backend: str, domain: CartDomain) -> int:
         return 1
     # The temporally blocked kernel halves HBM traffic per step; a deeper halo also halves
     # the number of RCCL round trips.  Limited by the smallest local extent.
-    return max(1, min(2, min(domain.proc_sizes)))
+    return max(1, min(3, min(domain.proc_sizes)))
 
 
 class GrayScott:

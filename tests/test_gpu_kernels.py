@@ -146,3 +146,35 @@ def test_gpu_cli_run(tmp_path):
     assert np.abs(u - c.get_fields()[0]).max() < 1e-3
     with BP4Reader(s.checkpoint_output) as ck:
         assert ck.read("step") == 200
+
+
+_CFG_SNIPPET = r"""
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+from grayscott_amd.models.grayscott import GrayScott
+from grayscott_amd.parallel.decomp import init_domain
+from grayscott_amd.utils.config import Settings
+out = []
+for fused in (False, True):
+    s = Settings(L=70, precision="Float32", F=0.02, k=0.048, dt=1.0, Du=0.2, Dv=0.1, noise=0.1,
+                 backend="AMDGPU", seed=21)
+    sim = GrayScott(s, init_domain(70, 1, 0), fuse=int(sys.argv[2]), use_fused=fused)
+    sim.init_fields(); sim.iterate(17)
+    out.append(sim.get_fields())
+print(max(np.abs(out[0][0] - out[1][0]).max(), np.abs(out[0][1] - out[1][1]).max()))
+"""
+
+
+@pytest.mark.parametrize("cfg", ["4x8:1", "8x4:1", "4x12:2", "8x4:1s", "8x4:4s", "4x8:1s", "4x8:4s"])
+@pytest.mark.parametrize("fuse", [2, 3])
+def test_fused_tuning_configs_agree(cfg, fuse):
+    """Every selectable fused-kernel configuration reproduces the single-step path."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, GS_FUSED_CFG=cfg)
+    r = subprocess.run([sys.executable, "-c", _CFG_SNIPPET, root, str(fuse)], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert float(r.stdout.strip().splitlines()[-1]) < 1e-5
