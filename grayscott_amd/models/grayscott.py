@@ -91,7 +91,22 @@ class GrayScott:
     def _setup_transport(self, kind: str) -> None:
         kind = (kind or "auto").lower()
         if kind == "auto":
-            kind = "rccl" if self.backend == "hip" else "torch"
+            chain = ["rccl", "torch", "host"] if self.backend == "hip" else ["torch"]
+            errors = []
+            for k in chain:
+                try:
+                    self._setup_transport(k)
+                    ok = self.ctx.allreduce(1.0, "min") if self.ctx.is_distributed else 1.0
+                except Exception as ex:  # pragma: no cover - exercised on multi-GPU nodes
+                    errors.append(f"{k}: {ex}")
+                    ok = self.ctx.allreduce(0.0, "min") if self.ctx.is_distributed else 0.0
+                if ok > 0:
+                    if errors and self.ctx.rank == 0:
+                        import warnings
+                        warnings.warn("halo transport fell back to " + k + " (" +
+                                      "; ".join(errors) + ")")
+                    return
+            raise RuntimeError("no halo transport could be set up: " + "; ".join(errors))
         if kind == "rccl":
             if self.backend != "hip":
                 raise ValueError("the rccl transport needs backend = AMDGPU/HIP")
