@@ -202,3 +202,16 @@ int gs_rccl_init(gs_engine* e, const char* uid, int32_t nranks, int32_t rank, in
 }
 
 }  // extern "C"
+
+extern "C" {
+
+// Select the fused-kernel configuration for fp32 (tuning; "" = measured default).
+// Returns -1 for an unknown name.
+int gs_fused_select(const char* name) {
+  const int k = gsk::fused_cfg_lookup(name);
+  if (k < 0) return -1;
+  gsk::fused_cfg_slot() = k;
+  return 0;
+}
+
+}  // extern "C"

@@ -363,20 +363,36 @@ struct FusedLaunch {
   }
 };
 
-// Tuning hook: GS_FUSED_CFG=<rows>x<waves>:<pf> picks a non-default fp32 configuration.
-inline int fused_cfg_env() {
+// Tuning hook: a non-default fp32 configuration "<rows>x<waves>:<prefetch>[s|w<n>]" chosen by
+// GS_FUSED_CFG at load time or gs_fused_select() at run time (index 0 = measured default).
+inline const char* const* fused_cfg_names(int* n) {
+  static const char* names[] = {"",       "4x8:1",  "4x8:2",  "4x8:4",   "8x4:1",   "8x4:2",
+                                "4x16:2", "8x8:2",  "4x8:3",  "8x4:2w3", "8x4:1w3", "4x8:2w4",
+                                "8x4:3",  "4x6:2",  "4x12:2", "4x4:2",   "4x12:3",  "8x4:1s",
+                                "8x4:4s", "4x8:1s", "4x8:4s"};
+  *n = (int)(sizeof(names) / sizeof(names[0]));
+  return names;
+}
+
+inline int& fused_cfg_slot() {
   static int v = -1;
+  return v;
+}
+
+inline int fused_cfg_lookup(const char* e) {
+  int n = 0;
+  const char* const* names = fused_cfg_names(&n);
+  if (!e) return 0;
+  for (int i = 1; i < n; ++i)
+    if (!strcmp(e, names[i])) return i;
+  return e[0] ? -1 : 0;
+}
+
+inline int fused_cfg_env() {
+  int& v = fused_cfg_slot();
   if (v < 0) {
-    v = 0;
-    const char* e = getenv("GS_FUSED_CFG");
-    if (e) {
-      static const char* names[] = {"",      "4x8:1",   "4x8:2",   "4x8:4",  "8x4:1",
-                                    "8x4:2", "4x16:2",  "8x8:2",   "4x8:3",  "8x4:2w3",
-                                    "8x4:1w3", "4x8:2w4", "8x4:3", "4x6:2", "4x12:2", "4x4:2", "4x12:3",
-                                    "8x4:1s", "8x4:4s", "4x8:1s", "4x8:4s"};
-      for (int i = 1; i < (int)(sizeof(names) / sizeof(names[0])); ++i)
-        if (!strcmp(e, names[i])) v = i;
-    }
+    const int k = fused_cfg_lookup(getenv("GS_FUSED_CFG"));
+    v = k < 0 ? 0 : k;
   }
   return v;
 }
@@ -408,11 +424,10 @@ void run_fused_cfg(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, c
       default: break;
     }
   }
-  // measured defaults (L=512, MI355X, profiles/r1_tune_*): fp32 T=2 -> 8x4 tile with a 3-plane
-  // prefetch, T=3 -> 4x12 tile with a 2-plane prefetch; fp64 -> 4x8
+  // measured defaults (MI355X, in-process A/B, profiles/r1_tune_inproc.json): fp32 uses the
+  // 4x12 tile with a 2-plane prefetch (best at T=2 for 256^3 and at T=3 for 512^3); fp64 4x8
   if constexpr (sizeof(T) == 4) {
-    if constexpr (TL == 2) FusedLaunch<FCfg<T, TL, 8, 4, 3, PER, NZ>, T>::run(s, d, a, p, st);
-    else FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ>, T>::run(s, d, a, p, st);
+    FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ>, T>::run(s, d, a, p, st);
   } else {
     FusedLaunch<FCfg<T, TL, 4, 8, 2, PER, NZ>, T>::run(s, d, a, p, st);
   }

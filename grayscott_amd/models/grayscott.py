@@ -34,9 +34,11 @@ def default_fuse(backend: str, domain: CartDomain) -> int:
     """Steps fused per halo exchange when ``fuse_steps = 0`` (auto)."""
     if backend != "hip":
         return 1
-    # The temporally blocked kernel halves HBM traffic per step; a deeper halo also halves
-    # the number of RCCL round trips.  Limited by the smallest local extent.
-    return max(1, min(3, min(domain.proc_sizes)))
+    # The temporally blocked kernel cuts HBM traffic per step by T; a deeper halo also cuts
+    # the RCCL round trips.  Measured on MI355X (profiles/r1_tune_inproc.json): T=3 wins on
+    # 512^3 sub-domains, T=2 on <=320-cell ones (pipeline fill and tile rounding grow with T).
+    n = min(domain.proc_sizes)
+    return max(1, min(2 if n <= 320 else 3, n))
 
 
 class GrayScott:

@@ -264,3 +264,12 @@ def rccl_unique_id() -> bytes:
     if n < 0:
         raise RuntimeError(f"ncclGetUniqueId failed: {last_error(lib)}")
     return buf.raw[:n]
+
+
+def fused_select(name: str = "") -> None:
+    """Pick a fused-kernel tuning configuration for fp32 ("" = measured default)."""
+    lib = load("hip")
+    lib.gs_fused_select.argtypes = [ctypes.c_char_p]
+    lib.gs_fused_select.restype = c_int
+    if lib.gs_fused_select(name.encode()) != 0:
+        raise ValueError(f"unknown fused-kernel configuration {name!r}")
