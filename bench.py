@@ -105,6 +105,8 @@ def main(argv=None) -> int:
                 "dims": dom.dims,
                 "local_extent": dom.proc_sizes,
                 "fuse_steps": sim.fuse,
+                "fused_kernel": {str(n): {"tile": c[0] or "default", "sched": c[1]}
+                                 for n, c in sim.fused_choice().items()},
                 "transport": sim.transport,
                 "noise": args.noise,
                 "backend": backend,

@@ -38,6 +38,12 @@ namespace {
 using gs::Box;
 using gs::Geom;
 
+// set once a configuration is chosen explicitly through gs_fused_select / gs_fused_sched
+bool& fused_pinned() {
+  static bool v = false;
+  return v;
+}
+
 template <typename T>
 class HipBackend final : public gs::Backend {
  public:
@@ -79,9 +85,78 @@ class HipBackend final : public gs::Backend {
   }
 
   bool fused(int src, int dst, int n, int64_t t) override {
-    const bool ok = gsk::launch_fused<T>(buf_[src], buf_[dst], g_, p_, n, t, stream_);
+    if (n < 2 || n > 3) return false;
+    if (!tuned_[n]) autotune(src, dst, n, t);
+    // an explicit gs_fused_select / gs_fused_sched overrides the tuned choice at any time
+    const bool pin = fused_pinned();
+    const bool ok = gsk::launch_fused<T>(buf_[src], buf_[dst], g_, p_, n, t, stream_,
+                                         pin ? -1 : cfg_[n], pin ? -1 : sched_[n]);
     if (ok) HIP_CHECK(hipGetLastError());
     return ok;
+  }
+
+  void prepare_fused(int src, int dst, int n, int64_t t) override {
+    if (n >= 2 && n <= 3 && !tuned_[n]) autotune(src, dst, n, t);
+  }
+
+  // On-device autotuning of the fused kernel's tile shape and work schedule.  The kernel only
+  // reads `src` and writes `dst`, so every candidate can be timed on the live buffers without
+  // changing the simulation state, and all candidates produce bit-identical results.
+  // Disabled by GS_AUTOTUNE=0 or by an explicit GS_FUSED_CFG / GS_FUSED_SCHED.
+  void autotune(int src, int dst, int n, int64_t t) {
+    tuned_[n] = true;
+    const char* e = getenv("GS_AUTOTUNE");
+    if ((e && atoi(e) == 0) || getenv("GS_FUSED_CFG") || getenv("GS_FUSED_SCHED") ||
+        fused_pinned())
+      return;
+    struct Cand { int cfg, sched; };
+    std::vector<Cand> cands;
+    const bool variants = !g_.periodic && p_.noise != 0.0;  // tile variants instantiated here
+    if (!variants) cands = {{0, 0}, {0, 1}};
+    else if (sizeof(T) == 4)
+      cands = {{0, 0},  {0, 1},  {1, 0},  {2, 0},  {2, 1},  {3, 0},  {5, 0},  {5, 1},
+               {8, 0},  {12, 0}, {16, 0}, {17, 0}, {18, 0}, {19, 0}, {20, 0}, {20, 1}};
+    else
+      cands = {{0, 0}, {0, 1}, {1, 0}, {1, 1}, {13, 0}, {15, 0}, {15, 1}};
+    // interleaved rounds (box-to-box and launch-to-launch jitter is several %): first launch
+    // of each candidate is a warm-up, then the best of kRounds timed launches decides
+    constexpr int kRounds = 3;
+    std::vector<float> tbest(cands.size(), 1e30f);
+    for (size_t i = 0; i < cands.size(); ++i)
+      if (!gsk::launch_fused<T>(buf_[src], buf_[dst], g_, p_, n, t, stream_, cands[i].cfg,
+                                cands[i].sched))
+        return;
+    hipEvent_t e0, e1;
+    HIP_CHECK(hipEventCreate(&e0));
+    HIP_CHECK(hipEventCreate(&e1));
+    for (int r = 0; r < kRounds; ++r)
+      for (size_t i = 0; i < cands.size(); ++i) {
+        HIP_CHECK(hipEventRecord(e0, stream_));
+        gsk::launch_fused<T>(buf_[src], buf_[dst], g_, p_, n, t, stream_, cands[i].cfg,
+                             cands[i].sched);
+        HIP_CHECK(hipEventRecord(e1, stream_));
+        HIP_CHECK(hipEventSynchronize(e1));
+        HIP_CHECK(hipGetLastError());
+        float ms = 0.f;
+        HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+        if (ms < tbest[i]) tbest[i] = ms;
+      }
+    float best = 1e30f;
+    for (size_t i = 0; i < cands.size(); ++i)
+      if (tbest[i] < best) {
+        best = tbest[i];
+        cfg_[n] = cands[i].cfg;
+        sched_[n] = cands[i].sched;
+      }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    tuned_ms_[n] = best;
+  }
+
+  void fused_choice(int n, int* cfg, int* sched, float* ms) const {
+    *cfg = cfg_[n];
+    *sched = sched_[n];
+    *ms = tuned_ms_[n];
   }
 
   void pack(int b, const gs::HaloPlan& p) override {
@@ -161,6 +236,10 @@ class HipBackend final : public gs::Backend {
   int dev_ = 0;
   ncclComm_t comm_ = nullptr;
   int rank_ = 0;
+  bool tuned_[4] = {false, false, false, false};
+  int cfg_[4] = {-1, -1, -1, -1};
+  int sched_[4] = {-1, -1, -1, -1};
+  float tuned_ms_[4] = {0.f, 0.f, 0.f, 0.f};
 };
 
 }  // namespace
@@ -211,7 +290,44 @@ int gs_fused_select(const char* name) {
   const int k = gsk::fused_cfg_lookup(name);
   if (k < 0) return -1;
   gsk::fused_cfg_slot() = k;
+  fused_pinned() = true;
   return 0;
 }
 
 }  // extern "C"
+
+extern "C" {
+
+// Select the fused-kernel work schedule (0: even split, 1: XCD-grouped lockstep z-chunks).
+int gs_fused_sched(int32_t sched) {
+  if (sched < 0 || sched > 1) return -1;
+  gsk::fused_sched_slot() = sched;
+  fused_pinned() = true;
+  return 0;
+}
+
+}  // extern "C"
+
+extern "C" {
+
+// Fused-kernel choice made by the autotuner for depth n: out = {cfg, sched}, ms = timing.
+int gs_fused_choice(gs_engine* e, int32_t n, int32_t dtype, int32_t* out2, float* ms) {
+  if (n < 0 || n > 3) return -1;
+  gs::Backend* b = e->eng->backend();
+  int c = -1, s = -1;
+  float t = 0.f;
+  if (dtype == gs::kF32) static_cast<HipBackend<float>*>(b)->fused_choice(n, &c, &s, &t);
+  else static_cast<HipBackend<double>*>(b)->fused_choice(n, &c, &s, &t);
+  out2[0] = c;
+  out2[1] = s;
+  *ms = t;
+  return 0;
+}
+
+}  // extern "C"
+
+extern "C" const char* gs_fused_cfg_name(int32_t index) {
+  int n = 0;
+  const char* const* names = gsk::fused_cfg_names(&n);
+  return (index >= 0 && index < n) ? names[index] : nullptr;
+}

@@ -25,6 +25,11 @@ struct FusedArgs {
   int32_t ybase;
   int32_t bcfix;
   int64_t units;
+  int32_t sched;   // 0: units split evenly; 1: XCD-grouped z-chunks walked in lockstep
+  int32_t nchunk;  // sched 1: z-chunks per tile
+  int32_t ntiles;  // sched 1: ntx * nty
+  int32_t grpM;    // sched 1: workgroups per XCD group (grid = 8 * grpM)
+  int32_t cfg;     // tile/prefetch configuration index (fused_cfg_names)
   int64_t t;
   int64_t buf_bytes;  // bytes of one state buffer (descriptor range)
 };
@@ -95,12 +100,15 @@ constexpr int gs_gcd(int a, int b) { return b == 0 ? a : gs_gcd(b, a % b); }
 constexpr int gs_lcm(int a, int b) { return a / gs_gcd(a, b) * b; }
 
 template <typename T, int TL_, int ROWS_, int WAVES_, int PF_, bool PERIODIC_, bool NOISE_,
-          int MINW_ = 1, bool SKEW_ = false>
+          int MINW_ = 1, bool SKEW_ = false, int ABL_ = 0>
 struct FCfg {
   static constexpr int MINW = MINW_;  // __launch_bounds__ min waves per SIMD
   using V2 = typename Vec2<T>::type;
   static constexpr int TL = TL_, ROWS = ROWS_, WAVES = WAVES_, PF = PF_;
   static constexpr bool PERIODIC = PERIODIC_, NOISE = NOISE_, SKEW = SKEW_;
+  // ablation (timing experiments only, results are WRONG): bit0 = no workgroup barriers,
+  // bit1 = every level-0 load reads plane 0 (L2-resident)
+  static constexpr int ABL = ABL_;
   static constexpr int R = PF + 2;                    // level-0 ring slots
   static constexpr int NS = SKEW ? 3 : 2;             // level-l output ring / xch buffers
   static constexpr int PERIOD = gs_lcm(R, NS);
@@ -152,7 +160,7 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
   {
     const bool pf_ok = p + C::PF < sg.ldend;
     const __amdgpu_buffer_rsrc_t r =
-        plane_rsrc(src, (int64_t)(p + C::PF + g.H) * PZB, pf_ok ? a.buf_bytes : 0);
+        plane_rsrc(src, (C::ABL & 2) ? 0 : (int64_t)(p + C::PF + g.H) * PZB, pf_ok ? a.buf_bytes : 0);
 #pragma unroll
     for (int j = 0; j < ROWS; ++j)
       S.LD[(IR + C::PF) % C::R][j] = bload(r, sg.voff + j * sg.pitchb, 0, (V2*)nullptr);
@@ -164,7 +172,7 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
       xch[l][IS][sg.wave][0][sg.lane] = in[0];
       xch[l][IS][sg.wave][1][sg.lane] = in[ROWS - 1];
     }
-    __syncthreads();
+    if constexpr (!(C::ABL & 1)) __syncthreads();
   }
 #pragma unroll
   for (int l = 0; l < TL; ++l) {
@@ -176,7 +184,7 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
     if constexpr (!C::SKEW) {
       xch[l][IS][sg.wave][0][sg.lane] = in[0];
       xch[l][IS][sg.wave][1][sg.lane] = in[ROWS - 1];
-      __syncthreads();
+      if constexpr (!(C::ABL & 1)) __syncthreads();
     }
     const V2 up = sg.wave > 0 ? xch[l][IS][sg.wave - 1][1][sg.lane] : in[0];
     const V2 dn = sg.wave < WAVES - 1 ? xch[l][IS][sg.wave + 1][0][sg.lane] : in[ROWS - 1];
@@ -275,9 +283,23 @@ __global__ __launch_bounds__(64 * C::WAVES, C::MINW) void k_fused(const typename
   sg.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   sg.pitchb = g.px * (int)sizeof(V2);
   const int nz = g.nz;
-  const int64_t U = a.units;
-  int64_t u = (int64_t)blockIdx.x * U / gridDim.x;
-  const int64_t uend = (int64_t)(blockIdx.x + 1) * U / gridDim.x;
+  int64_t u, uend;
+  if (a.sched == 1) {
+    // Workgroups b, b+8, b+16, ... share an XCD (round-robin dispatch, speed only): give each
+    // XCD a contiguous range of logical units so spatially adjacent tiles sit on one L2, and
+    // let every tile's chunk start at the same z, so neighbours' shared halo lines are read
+    // while still resident.
+    const int b = blockIdx.x;
+    const int lu = (b % 8) * a.grpM + b / 8;
+    if (lu >= a.ntiles * a.nchunk) return;  // whole workgroup, before any barrier
+    const int chunk = lu / a.ntiles, tile = lu % a.ntiles;
+    u = (int64_t)tile * nz + (int64_t)chunk * nz / a.nchunk;
+    uend = (int64_t)tile * nz + (int64_t)(chunk + 1) * nz / a.nchunk;
+  } else {
+    const int64_t U = a.units;
+    u = (int64_t)blockIdx.x * U / gridDim.x;
+    uend = (int64_t)(blockIdx.x + 1) * U / gridDim.x;
+  }
   FusedState<C> S;
 
   while (u < uend) {
@@ -328,6 +350,8 @@ __global__ __launch_bounds__(64 * C::WAVES, C::MINW) void k_fused(const typename
 }
 
 // ------------------------------------------------------------------------------------------
+inline int& fused_sched_slot();
+
 template <class C, typename T>
 struct FusedLaunch {
   static int occupancy() {
@@ -356,8 +380,17 @@ struct FusedLaunch {
       (void)hipGetDevice(&dev);
       if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
     }
-    int64_t nwg = (int64_t)occupancy() * cus;
-    nwg = std::max<int64_t>(1, std::min<int64_t>(nwg, a.units / (4 * C::TL + 8)));
+    const int64_t slots = (int64_t)occupancy() * cus;
+    int64_t nwg = std::max<int64_t>(1, std::min<int64_t>(slots, a.units / (4 * C::TL + 8)));
+    if (a.sched == 1) {
+      a.ntiles = a.ntx * a.nty;
+      int nch = (int)((slots + a.ntiles / 2) / a.ntiles);
+      nch = std::max(1, std::min(nch, a.g.nz / (4 * C::TL + 4) > 0 ? a.g.nz / (4 * C::TL + 4) : 1));
+      a.nchunk = nch;
+      const int64_t nunits = (int64_t)a.ntiles * nch;
+      a.grpM = (int)((nunits + 7) / 8);
+      nwg = 8LL * a.grpM;
+    }
     const FoldCoef<T> f = make_fold<T>(p);
     k_fused<C, T><<<(unsigned)nwg, 64 * C::WAVES, 0, st>>>(s, d, a, f, p.seed);
   }
@@ -365,11 +398,20 @@ struct FusedLaunch {
 
 // Tuning hook: a non-default fp32 configuration "<rows>x<waves>:<prefetch>[s|w<n>]" chosen by
 // GS_FUSED_CFG at load time or gs_fused_select() at run time (index 0 = measured default).
+inline int& fused_sched_slot() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("GS_FUSED_SCHED");
+    v = e ? atoi(e) : 0;
+  }
+  return v;
+}
+
 inline const char* const* fused_cfg_names(int* n) {
   static const char* names[] = {"",       "4x8:1",  "4x8:2",  "4x8:4",   "8x4:1",   "8x4:2",
                                 "4x16:2", "8x8:2",  "4x8:3",  "8x4:2w3", "8x4:1w3", "4x8:2w4",
                                 "8x4:3",  "4x6:2",  "4x12:2", "4x4:2",   "4x12:3",  "8x4:1s",
-                                "8x4:4s", "4x8:1s", "4x8:4s"};
+                                "8x4:4s", "4x8:1s", "4x8:4s", "abl1",   "abl2",    "abl3"};
   *n = (int)(sizeof(names) / sizeof(names[0]));
   return names;
 }
@@ -400,8 +442,16 @@ inline int fused_cfg_env() {
 template <typename T, int TL, bool PER, bool NZ>
 void run_fused_cfg(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, const FusedArgs& a,
                    const gs::Params& p, hipStream_t st) {
+  if constexpr (sizeof(T) == 8 && !PER && NZ) {
+    switch (a.cfg) {  // fp64: only shapes that fit the register file without spills
+      case 1: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ>, T>::run(s, d, a, p, st); return;
+      case 13: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
+      case 15: FusedLaunch<FCfg<T, TL, 4, 4, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
+      default: break;
+    }
+  }
   if constexpr (sizeof(T) == 4 && !PER && NZ) {
-    switch (fused_cfg_env()) {
+    switch (a.cfg) {
       case 1: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ>, T>::run(s, d, a, p, st); return;
       case 3: FusedLaunch<FCfg<T, TL, 4, 8, 4, PER, NZ>, T>::run(s, d, a, p, st); return;
       case 4: FusedLaunch<FCfg<T, TL, 8, 4, 1, PER, NZ>, T>::run(s, d, a, p, st); return;
@@ -421,6 +471,9 @@ void run_fused_cfg(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, c
       case 18: FusedLaunch<FCfg<T, TL, 8, 4, 4, PER, NZ, 1, true>, T>::run(s, d, a, p, st); return;
       case 19: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, 1, true>, T>::run(s, d, a, p, st); return;
       case 20: FusedLaunch<FCfg<T, TL, 4, 8, 4, PER, NZ, 1, true>, T>::run(s, d, a, p, st); return;
+      case 21: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, 1, false, 1>, T>::run(s, d, a, p, st); return;
+      case 22: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, 1, false, 2>, T>::run(s, d, a, p, st); return;
+      case 23: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, 1, false, 3>, T>::run(s, d, a, p, st); return;
       default: break;
     }
   }
@@ -446,14 +499,19 @@ void run_fused_tl(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, co
   }
 }
 
+// cfg / sched < 0: the process-wide selection (GS_FUSED_CFG / GS_FUSED_SCHED or the
+// gs_fused_select / gs_fused_sched APIs).
 template <typename T>
 bool launch_fused(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, const Geom& g,
-                  const gs::Params& p, int n, int64_t t, hipStream_t st) {
+                  const gs::Params& p, int n, int64_t t, hipStream_t st, int cfg = -1,
+                  int sched = -1) {
   if (n < 2 || n > 3 || g.H < n) return false;
   if (g.periodic && (g.Ly % 4 != 0)) return false;  // noise quads would straddle the wrap
   FusedArgs a{};
   a.g = g;
   a.t = t;
+  a.cfg = cfg >= 0 ? cfg : fused_cfg_env();
+  a.sched = sched >= 0 ? sched : fused_sched_slot();
   a.bcfix = g.periodic ? 0 : 1;
   a.buf_bytes = gs::total_elems(g) * (int64_t)sizeof(typename Vec2<T>::type);
   if (n == 2) run_fused_tl<T, 2>(s, d, a, p, st);

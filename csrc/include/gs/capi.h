@@ -20,6 +20,7 @@ void gs_destroy(gs_engine* e);
 const char* gs_last_error(void);
 
 int gs_init_fields(gs_engine* e);
+int gs_prepare(gs_engine* e);  // autotune the fused kernel (state unchanged)
 int gs_advance(gs_engine* e, int64_t nsteps);
 int gs_exchange(gs_engine* e);
 int64_t gs_get_step(gs_engine* e);

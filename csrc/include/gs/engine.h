@@ -35,6 +35,9 @@ class Backend {
   // temporally blocked kernel: n steps over the interior, src at time t -> dst at t+n.
   // Returns false if unsupported for this n (the scheduler then falls back to step()).
   virtual bool fused(int src, int dst, int n, int64_t t) { (void)src; (void)dst; (void)n; (void)t; return false; }
+  // optional one-time preparation (autotuning) of the fused kernel for depth n; must not
+  // change the state held in buffer src
+  virtual void prepare_fused(int src, int dst, int n, int64_t t) { (void)src; (void)dst; (void)n; (void)t; }
   virtual void pack(int b, const HaloPlan& p) = 0;
   virtual void unpack(int b, const HaloPlan& p) = 0;
   // copy send-buffer cells [src_off, +n) to recv-buffer cells [dst_off, +n)
@@ -91,6 +94,18 @@ class Engine {
     t_ = 0;
     bc_parity_[0] = 0;  // u ghosts = 1 -> even time
     bc_parity_[1] = 1;  // u_temp ghosts = 0 -> odd time
+  }
+
+  // Tune every fused depth this engine can use, without changing the state.
+  void prepare() {
+    if (!cfg_.use_fused) return;
+    for (int n = 2; n <= cfg_.fuse; ++n) be_->prepare_fused(cur_, 1 - cur_, n, t_);
+    // the timing runs scribbled over the other buffer: restore the reference's zeroed
+    // u_temp/v_temp (ghosts included) so the ghost-parity bookkeeping stays exact
+    const Geom& g = cfg_.g;
+    Box all{-g.H, -g.H, -g.H, g.nx + 2 * g.H, g.ny + 2 * g.H, g.nz + 2 * g.H};
+    be_->fill_box(1 - cur_, all, 0.0, 0.0);
+    bc_parity_[1 - cur_] = 1;  // u ghosts = 0 <-> odd time
   }
 
   void exchange() {

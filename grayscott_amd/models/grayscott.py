@@ -128,6 +128,20 @@ class GrayScott:
     # ------------------------------------------------------------------------------------
     def init_fields(self) -> None:
         self.engine.init_fields()
+        # pick the fastest fused-kernel tile/schedule on this device for this sub-domain
+        # (timed on the live buffers; the state is unchanged) before any timed stepping
+        self.engine.prepare()
+
+    def fused_choice(self):
+        """{depth: (config, schedule, ms)} chosen by the on-device autotuner (HIP only)."""
+        if self.backend != "hip":
+            return {}
+        out = {}
+        for n in range(2, self.fuse + 1):
+            c = self.engine.fused_choice(n)
+            if c is not None:
+                out[n] = c
+        return out
 
     def iterate(self, nsteps: int = 1) -> None:
         """Advance ``nsteps`` steps (each = exchange! + calculate! + swap in the reference)."""

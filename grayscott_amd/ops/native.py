@@ -58,7 +58,7 @@ def _declare(lib) -> None:
     lib.gs_destroy.argtypes = [c_void_p]
     lib.gs_destroy.restype = None
     lib.gs_last_error.restype = c_char_p
-    for name in ("gs_init_fields", "gs_exchange", "gs_current_buffer", "gs_sync"):
+    for name in ("gs_init_fields", "gs_prepare", "gs_exchange", "gs_current_buffer", "gs_sync"):
         getattr(lib, name).argtypes = [c_void_p]
         getattr(lib, name).restype = c_int
     lib.gs_advance.argtypes = [c_void_p, c_int64]
@@ -96,8 +96,10 @@ def _declare(lib) -> None:
         lib.gs_rccl_unique_id.restype = c_int
         lib.gs_rccl_init.argtypes = [c_void_p, ctypes.c_char_p, c_int32, c_int32, c_int32]
         lib.gs_rccl_init.restype = c_int
-    if hasattr(lib, "gs_bp_version"):
-        pass
+    if hasattr(lib, "gs_fused_choice"):
+        lib.gs_fused_choice.argtypes = [c_void_p, c_int32, c_int32, POINTER(c_int32),
+                                        POINTER(ctypes.c_float)]
+        lib.gs_fused_choice.restype = c_int
 
 
 def load(name: str):
@@ -189,6 +191,22 @@ class Engine:
     def init_fields(self):
         self._chk(self.lib.gs_init_fields(self.h), "init_fields")
 
+    def prepare(self):
+        """Autotune the fused kernel on the live buffers (the state is left unchanged)."""
+        self._chk(self.lib.gs_prepare(self.h), "prepare")
+
+    def fused_choice(self, n: int):
+        """(config name, schedule, ms) the autotuner picked for fuse depth n, or None."""
+        if not hasattr(self.lib, "gs_fused_choice"):
+            return None
+        out = (c_int32 * 2)()
+        ms = ctypes.c_float()
+        self._chk(self.lib.gs_fused_choice(self.h, int(n), DTYPE_CODES[self.dtype], out,
+                                           ctypes.byref(ms)), "fused_choice")
+        if out[0] < 0:
+            return None
+        return fused_cfg_name(int(out[0])), int(out[1]), float(ms.value)
+
     def advance(self, n: int):
         self._chk(self.lib.gs_advance(self.h, int(n)), "advance")
 
@@ -273,3 +291,21 @@ def fused_select(name: str = "") -> None:
     lib.gs_fused_select.restype = c_int
     if lib.gs_fused_select(name.encode()) != 0:
         raise ValueError(f"unknown fused-kernel configuration {name!r}")
+
+
+def fused_sched(sched: int) -> None:
+    """Pick the fused-kernel work schedule (0 even split, 1 XCD-grouped lockstep chunks)."""
+    lib = load("hip")
+    lib.gs_fused_sched.argtypes = [c_int32]
+    lib.gs_fused_sched.restype = c_int
+    if lib.gs_fused_sched(int(sched)) != 0:
+        raise ValueError(f"unknown schedule {sched}")
+
+
+def fused_cfg_name(index: int) -> str:
+    """Name of fused-kernel configuration ``index`` ("" = measured default)."""
+    lib = load("hip")
+    lib.gs_fused_cfg_name.argtypes = [c_int32]
+    lib.gs_fused_cfg_name.restype = c_char_p
+    r = lib.gs_fused_cfg_name(int(index))
+    return r.decode() if r is not None else f"#{index}"

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--precision", default="Float32")
     ap.add_argument("--out", default="")
     ap.add_argument("--noise", type=float, default=0.1)
+    ap.add_argument("--sched", type=int, nargs="+", default=[0])
     a = ap.parse_args()
     import torch
     from grayscott_amd.models.grayscott import GrayScott
@@ -43,20 +44,23 @@ def main():
         for r in range(a.rounds):
             for fuse, sim in sims.items():
                 for cfg in a.cfg:
-                    native.fused_select(cfg)
-                    sim.iterate(12)
-                    torch.cuda.synchronize()
-                    t0 = time.perf_counter()
-                    sim.iterate(a.steps)
-                    torch.cuda.synchronize()
-                    dt = time.perf_counter() - t0
-                    key = f"L={L} fuse={fuse} cfg={cfg or 'default'}"
-                    results.setdefault(key, []).append(L ** 3 * a.steps / dt / 1e6)
+                    for sched in a.sched:
+                        native.fused_select(cfg)
+                        native.fused_sched(sched)
+                        sim.iterate(12)
+                        torch.cuda.synchronize()
+                        t0 = time.perf_counter()
+                        sim.iterate(a.steps)
+                        torch.cuda.synchronize()
+                        dt = time.perf_counter() - t0
+                        key = f"L={L} fuse={fuse} cfg={cfg or 'default'} sched={sched}"
+                        results.setdefault(key, []).append(L ** 3 * a.steps / dt / 1e6)
         for sim in sims.values():
             sim.close()
         del sims
         torch.cuda.empty_cache()
     native.fused_select("")
+    native.fused_sched(0)
     rows = []
     for k, v in results.items():
         rows.append({"config": k, "median_mlups": statistics.median(v), "min": min(v), "max": max(v)})

@@ -165,16 +165,36 @@ print(max(np.abs(out[0][0] - out[1][0]).max(), np.abs(out[0][1] - out[1][1]).max
 """
 
 
-@pytest.mark.parametrize("cfg", ["4x8:1", "8x4:1", "4x12:2", "8x4:1s", "8x4:4s", "4x8:1s", "4x8:4s"])
+@pytest.mark.parametrize("cfg,sched", [
+    ("4x8:1", 0), ("8x4:1", 0), ("4x12:2", 0), ("8x4:1s", 0), ("8x4:4s", 0), ("4x8:1s", 0),
+    ("4x8:4s", 0), ("", 1), ("8x4:2", 1), ("4x8:4s", 1)])
 @pytest.mark.parametrize("fuse", [2, 3])
-def test_fused_tuning_configs_agree(cfg, fuse):
-    """Every selectable fused-kernel configuration reproduces the single-step path."""
+def test_fused_tuning_configs_agree(cfg, sched, fuse):
+    """Every selectable fused-kernel configuration / schedule reproduces the single-step path."""
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, GS_FUSED_CFG=cfg)
+    env = dict(os.environ, GS_FUSED_CFG=cfg, GS_FUSED_SCHED=str(sched))
     r = subprocess.run([sys.executable, "-c", _CFG_SNIPPET, root, str(fuse)], env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     assert float(r.stdout.strip().splitlines()[-1]) < 1e-5
+
+
+@pytest.mark.parametrize("prec", ["Float32", "Float64"])
+def test_autotuner_choice_is_valid_and_state_unchanged(prec):
+    """prepare() (run by init_fields) times candidates on the live buffers: the initial state
+    must still match the CPU init, and the chosen kernel must reproduce single steps."""
+    g = _sim("AMDGPU", 72, prec, 0.1, fuse=3)
+    c = _sim("CPU", 72, prec, 0.1, fuse=1)
+    np.testing.assert_array_equal(g.get_fields()[0], c.get_fields()[0])
+    choice = g.fused_choice()
+    assert set(choice) == {2, 3}
+    for name, sched, ms in choice.values():
+        assert isinstance(name, str) and sched in (0, 1) and ms > 0
+    g.iterate(11)
+    c.iterate(11)
+    tol = 2e-5 if prec == "Float32" else 1e-12
+    assert np.abs(g.get_fields()[0] - c.get_fields()[0]).max() < tol
+    assert np.abs(g.get_fields()[1] - c.get_fields()[1]).max() < tol
