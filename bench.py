@@ -36,12 +36,14 @@ def main(argv=None) -> int:
     ap.add_argument("--no-fused-kernel", action="store_true")
     ap.add_argument("--noise", type=float, default=0.1)
     ap.add_argument("--backend", default="AMDGPU")
+    ap.add_argument("--decomposition", default="auto", help="auto | balanced | z")
+    ap.add_argument("--overlap", default="auto", help="auto | on | off")
     args = ap.parse_args(argv)
 
     import torch
 
     from grayscott_amd.models.grayscott import GrayScott
-    from grayscott_amd.parallel.decomp import init_domain
+    from grayscott_amd.parallel.decomp import choose_dims, init_domain
     from grayscott_amd.parallel.dist import init_from_env
     from grayscott_amd.utils.config import Settings, load_backend_and_lang
 
@@ -54,10 +56,12 @@ def main(argv=None) -> int:
     settings = Settings(L=args.L, steps=args.steps, plotgap=args.steps + args.warmup + 1,
                         F=0.02, k=0.048, dt=1.0, Du=0.2, Dv=0.1, noise=args.noise,
                         precision=args.precision, backend=args.backend, fuse_steps=args.fuse,
-                        transport=args.transport)
+                        transport=args.transport, decomposition=args.decomposition,
+                        overlap=args.overlap)
     backend, _ = load_backend_and_lang(settings)
     ctx = init_from_env("hip" if backend == "hip" else "cpu")
-    dom = init_domain(args.L, ctx.world_size, ctx.rank, periodic=False)
+    dims = choose_dims(args.L, ctx.world_size, args.decomposition, backend)
+    dom = init_domain(args.L, ctx.world_size, ctx.rank, periodic=False, dims=dims)
     sim = GrayScott(settings, dom, ctx, use_fused=not args.no_fused_kernel)
     sim.init_fields()
 
@@ -108,6 +112,7 @@ def main(argv=None) -> int:
                 "fused_kernel": {str(n): {"tile": c[0] or "default", "sched": c[1]}
                                  for n, c in sim.fused_choice().items()},
                 "transport": sim.transport,
+                "overlap": sim.overlapped,
                 "noise": args.noise,
                 "backend": backend,
             },

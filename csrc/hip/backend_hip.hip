@@ -60,11 +60,21 @@ class HipBackend final : public gs::Backend {
     HIP_CHECK(hipGetDevice(&dev_));
     HIP_CHECK(hipMalloc(&ws_, sizeof(double) * 6 * kStatBlocks));
     HIP_CHECK(hipEventCreateWithFlags(&ev_, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
+    // halo traffic on its own high-priority stream so it overlaps the inner-plane kernel
+    int lo = 0, hi = 0;
+    HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    HIP_CHECK(hipStreamCreateWithPriority(&comm_stream_, hipStreamNonBlocking, hi));
+    xs_ = stream_;
   }
   ~HipBackend() override {
     if (comm_) ncclCommDestroy(comm_);
     if (ws_) (void)hipFree(ws_);
     if (ev_) (void)hipEventDestroy(ev_);
+    if (ev_fork_) (void)hipEventDestroy(ev_fork_);
+    if (ev_join_) (void)hipEventDestroy(ev_join_);
+    if (comm_stream_) (void)hipStreamDestroy(comm_stream_);
   }
 
   void fill_box(int b, const Box& bx, double u, double v) override {
@@ -93,6 +103,54 @@ class HipBackend final : public gs::Backend {
                                          pin ? -1 : cfg_[n], pin ? -1 : sched_[n]);
     if (ok) HIP_CHECK(hipGetLastError());
     return ok;
+  }
+
+  bool fused_supported(int n) const override { return gsk::fused_supported(g_, n); }
+
+  bool fused_runs(int src, int dst, int n, int64_t t, int zlo0, int zlen0, int zlo1,
+                  int zlen1) override {
+    if (!gsk::fused_supported(g_, n)) return false;
+    if (!tuned_[n]) autotune(src, dst, n, t);
+    const bool pin = fused_pinned();
+    const bool ok = gsk::launch_fused<T>(buf_[src], buf_[dst], g_, p_, n, t, stream_,
+                                         pin ? -1 : cfg_[n], pin ? -1 : sched_[n], zlo0, zlen0,
+                                         zlo1, zlen1);
+    if (!ok) throw std::runtime_error("fused_runs: invalid z-runs");
+    HIP_CHECK(hipGetLastError());
+    return true;
+  }
+
+  bool has_comm_stream() const override { return comm_stream_ != nullptr; }
+  void comm_fork() override {
+    HIP_CHECK(hipEventRecord(ev_fork_, stream_));
+    HIP_CHECK(hipStreamWaitEvent(comm_stream_, ev_fork_, 0));
+  }
+  void comm_join() override {
+    HIP_CHECK(hipEventRecord(ev_join_, comm_stream_));
+    HIP_CHECK(hipStreamWaitEvent(stream_, ev_join_, 0));
+  }
+  void comm_select(bool on) override { xs_ = on ? comm_stream_ : stream_; }
+
+  // zplanes plan: every message is a contiguous run of storage planes of buffer b, so RCCL
+  // sends and receives them in place.  Same message order as the packed path (sends ascend
+  // in direction, receives descend), which keeps two messages to one peer matched.
+  bool native_exchange_inplace(int b, const gs::HaloPlan& p) override {
+    if (!comm_ || !p.zplanes || inplace_off_) return false;
+    for (int i = 0; i < p.nrecv; ++i)
+      if (p.recv[i].peer == rank_) return false;
+    NCCL_CHECK(ncclGroupStart());
+    for (int i = 0; i < p.nsend; ++i) {
+      const gs::HaloMsg& m = p.send[i];
+      NCCL_CHECK(ncclSend(buf_[b] + gs::box_start(g_, m.box),
+                          (size_t)gs::box_cells(m.box) * sizeof(V2), ncclUint8, m.peer, comm_, xs_));
+    }
+    for (int i = 0; i < p.nrecv; ++i) {
+      const gs::HaloMsg& m = p.recv[i];
+      NCCL_CHECK(ncclRecv(buf_[b] + gs::box_start(g_, m.box),
+                          (size_t)gs::box_cells(m.box) * sizeof(V2), ncclUint8, m.peer, comm_, xs_));
+    }
+    NCCL_CHECK(ncclGroupEnd());
+    return true;
   }
 
   void prepare_fused(int src, int dst, int n, int64_t t) override {
@@ -161,16 +219,16 @@ class HipBackend final : public gs::Backend {
 
   void pack(int b, const gs::HaloPlan& p) override {
     if (p.nsend == 0) return;
-    gsk::launch_pack<T, true>(buf_[b], send_, g_, p.send, p.nsend, stream_);
+    gsk::launch_pack<T, true>(buf_[b], send_, g_, p.send, p.nsend, xs_);
     HIP_CHECK(hipGetLastError());
   }
   void unpack(int b, const gs::HaloPlan& p) override {
     if (p.nrecv == 0) return;
-    gsk::launch_pack<T, false>(buf_[b], recv_, g_, p.recv, p.nrecv, stream_);
+    gsk::launch_pack<T, false>(buf_[b], recv_, g_, p.recv, p.nrecv, xs_);
     HIP_CHECK(hipGetLastError());
   }
   void self_copy(int64_t so, int64_t d, int64_t n) override {
-    HIP_CHECK(hipMemcpyAsync(recv_ + d, send_ + so, sizeof(V2) * n, hipMemcpyDeviceToDevice, stream_));
+    HIP_CHECK(hipMemcpyAsync(recv_ + d, send_ + so, sizeof(V2) * n, hipMemcpyDeviceToDevice, xs_));
   }
 
   bool native_exchange(const gs::HaloPlan& p) override {
@@ -180,19 +238,19 @@ class HipBackend final : public gs::Backend {
       const gs::HaloMsg& m = p.send[i];
       if (m.peer == rank_) continue;
       NCCL_CHECK(ncclSend(send_ + m.offset, (size_t)gs::box_cells(m.box) * sizeof(V2), ncclUint8,
-                          m.peer, comm_, stream_));
+                          m.peer, comm_, xs_));
     }
     for (int i = 0; i < p.nrecv; ++i) {
       const gs::HaloMsg& m = p.recv[i];
       if (m.peer == rank_) continue;
       NCCL_CHECK(ncclRecv(recv_ + m.offset, (size_t)gs::box_cells(m.box) * sizeof(V2), ncclUint8,
-                          m.peer, comm_, stream_));
+                          m.peer, comm_, xs_));
     }
     NCCL_CHECK(ncclGroupEnd());
     return true;
   }
 
-  void host_sync() override { HIP_CHECK(hipStreamSynchronize(stream_)); }
+  void host_sync() override { HIP_CHECK(hipStreamSynchronize(xs_)); }
 
   void extract(int b, void* u, void* v) override {
     gsk::launch_extract<T>(buf_[b], (T*)u, (T*)v, g_, stream_);
@@ -233,6 +291,10 @@ class HipBackend final : public gs::Backend {
   V2* recv_;
   void* ws_ = nullptr;
   hipEvent_t ev_ = nullptr;
+  hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
+  hipStream_t comm_stream_ = nullptr;
+  hipStream_t xs_ = nullptr;  // stream for halo traffic (compute or comm stream)
+  bool inplace_off_ = getenv("GS_INPLACE_HALO") && atoi(getenv("GS_INPLACE_HALO")) == 0;
   int dev_ = 0;
   ncclComm_t comm_ = nullptr;
   int rank_ = 0;

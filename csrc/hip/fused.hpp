@@ -32,6 +32,10 @@ struct FusedArgs {
   int32_t cfg;     // tile/prefetch configuration index (fused_cfg_names)
   int64_t t;
   int64_t buf_bytes;  // bytes of one state buffer (descriptor range)
+  // output z-runs [zlo[r], zlo[r] + zlen[r]) (zlen[1] may be 0); a tile's units enumerate the
+  // planes of run 0 then run 1 (nzv = zlen[0] + zlen[1] units per tile)
+  int32_t zlo[2], zlen[2];
+  int32_t nzv;
 };
 
 // Folded update coefficients: u' = au*u + asu*su + ac - dt*uvv + ar*r ; v' = bv*v + bsv*sv + dt*uvv
@@ -282,7 +286,7 @@ __global__ __launch_bounds__(64 * C::WAVES, C::MINW) void k_fused(const typename
   sg.lane = threadIdx.x & 63;
   sg.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   sg.pitchb = g.px * (int)sizeof(V2);
-  const int nz = g.nz;
+  const int nzv = a.nzv;
   int64_t u, uend;
   if (a.sched == 1) {
     // Workgroups b, b+8, b+16, ... share an XCD (round-robin dispatch, speed only): give each
@@ -293,8 +297,8 @@ __global__ __launch_bounds__(64 * C::WAVES, C::MINW) void k_fused(const typename
     const int lu = (b % 8) * a.grpM + b / 8;
     if (lu >= a.ntiles * a.nchunk) return;  // whole workgroup, before any barrier
     const int chunk = lu / a.ntiles, tile = lu % a.ntiles;
-    u = (int64_t)tile * nz + (int64_t)chunk * nz / a.nchunk;
-    uend = (int64_t)tile * nz + (int64_t)(chunk + 1) * nz / a.nchunk;
+    u = (int64_t)tile * nzv + (int64_t)chunk * nzv / a.nchunk;
+    uend = (int64_t)tile * nzv + (int64_t)(chunk + 1) * nzv / a.nchunk;
   } else {
     const int64_t U = a.units;
     u = (int64_t)blockIdx.x * U / gridDim.x;
@@ -303,10 +307,16 @@ __global__ __launch_bounds__(64 * C::WAVES, C::MINW) void k_fused(const typename
   FusedState<C> S;
 
   while (u < uend) {
-    const int tile = (int)(u / nz);
-    const int z0 = (int)(u % nz);
-    const int z1 = (int)std::min<int64_t>(nz, z0 + (uend - u));
-    u += z1 - z0;
+    const int tile = (int)(u / nzv);
+    const int zv = (int)(u % nzv);
+    // a segment never crosses from one z-run into the other
+    const int run = zv < a.zlen[0] ? 0 : 1;
+    const int rv0 = run ? a.zlen[0] : 0;
+    const int rv1 = run ? nzv : a.zlen[0];
+    const int zv1 = (int)std::min<int64_t>(rv1, zv + (uend - u));
+    const int z0 = a.zlo[run] + (zv - rv0);
+    const int z1 = z0 + (zv1 - zv);
+    u += zv1 - zv;
     const int tx = tile % a.ntx, ty = tile / a.ntx;
     const int X0 = tx * a.xstep - TL;
     const int Y0 = a.ybase + ty * a.ystep - TL;
@@ -373,7 +383,7 @@ struct FusedLaunch {
     a.ybase = -mod4(a.g.oy - C::TL);  // (oy + ybase - TL) % 4 == 0
     a.ntx = (a.g.nx + a.xstep - 1) / a.xstep;
     a.nty = (a.g.ny - a.ybase + a.ystep - 1) / a.ystep;
-    a.units = (int64_t)a.ntx * a.nty * a.g.nz;
+    a.units = (int64_t)a.ntx * a.nty * a.nzv;
     static int cus = 0;
     if (!cus) {
       int dev = 0;
@@ -381,11 +391,16 @@ struct FusedLaunch {
       if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
     }
     const int64_t slots = (int64_t)occupancy() * cus;
-    int64_t nwg = std::max<int64_t>(1, std::min<int64_t>(slots, a.units / (4 * C::TL + 8)));
+    // enough planes per workgroup to amortise the 2T-plane pipeline fill, but at least one
+    // workgroup per (tile, z-run) so short runs (comm/compute-overlap slabs) stay parallel
+    const int nruns = a.zlen[1] > 0 ? 2 : 1;
+    int64_t nwg = std::max<int64_t>(a.units / (4 * C::TL + 8),
+                                    nruns > 1 ? (int64_t)a.ntx * a.nty * nruns : 1);
+    nwg = std::max<int64_t>(1, std::min<int64_t>(slots, nwg));
     if (a.sched == 1) {
       a.ntiles = a.ntx * a.nty;
       int nch = (int)((slots + a.ntiles / 2) / a.ntiles);
-      nch = std::max(1, std::min(nch, a.g.nz / (4 * C::TL + 4) > 0 ? a.g.nz / (4 * C::TL + 4) : 1));
+      nch = std::max(1, std::min(nch, a.nzv / (4 * C::TL + 4) > 0 ? a.nzv / (4 * C::TL + 4) : 1));
       a.nchunk = nch;
       const int64_t nunits = (int64_t)a.ntiles * nch;
       a.grpM = (int)((nunits + 7) / 8);
@@ -499,19 +514,31 @@ void run_fused_tl(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, co
   }
 }
 
+inline bool fused_supported(const Geom& g, int n) {
+  if (n < 2 || n > 3 || g.H < n) return false;
+  return !(g.periodic && (g.Ly % 4 != 0));  // noise quads would straddle the wrap
+}
+
 // cfg / sched < 0: the process-wide selection (GS_FUSED_CFG / GS_FUSED_SCHED or the
 // gs_fused_select / gs_fused_sched APIs).
 template <typename T>
 bool launch_fused(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, const Geom& g,
                   const gs::Params& p, int n, int64_t t, hipStream_t st, int cfg = -1,
-                  int sched = -1) {
-  if (n < 2 || n > 3 || g.H < n) return false;
-  if (g.periodic && (g.Ly % 4 != 0)) return false;  // noise quads would straddle the wrap
+                  int sched = -1, int zlo0 = 0, int zlen0 = -1, int zlo1 = 0, int zlen1 = 0) {
+  if (!fused_supported(g, n)) return false;
   FusedArgs a{};
+  if (zlen0 < 0) zlen0 = g.nz;
+  if (zlen1 <= 0) zlen1 = 0;
+  if (zlen0 <= 0 || zlo0 < 0 || zlo0 + zlen0 > g.nz || (zlen1 && (zlo1 < 0 || zlo1 + zlen1 > g.nz)))
+    return false;
+  a.zlo[0] = zlo0; a.zlen[0] = zlen0;
+  a.zlo[1] = zlo1; a.zlen[1] = zlen1;
+  a.nzv = zlen0 + zlen1;
   a.g = g;
   a.t = t;
   a.cfg = cfg >= 0 ? cfg : fused_cfg_env();
   a.sched = sched >= 0 ? sched : fused_sched_slot();
+  if (zlen1) a.sched = 0;  // two short runs: one workgroup per (tile, run)
   a.bcfix = g.periodic ? 0 : 1;
   a.buf_bytes = gs::total_elems(g) * (int64_t)sizeof(typename Vec2<T>::type);
   if (n == 2) run_fused_tl<T, 2>(s, d, a, p, st);

@@ -63,6 +63,9 @@ void gs_destroy(gs_engine* e) {
 
 int gs_init_fields(gs_engine* e) { GS_TRY(e->eng->init_fields()) }
 int gs_prepare(gs_engine* e) { GS_TRY(e->eng->prepare()) }
+int gs_set_overlap(gs_engine* e, int32_t mode) { GS_TRY(e->eng->set_overlap(mode)) }
+int gs_overlapped(gs_engine* e, int32_t k) { return e->eng->overlapped(k) ? 1 : 0; }
+int gs_plan_zplanes(gs_engine* e) { return e->eng->plan().zplanes; }
 int gs_advance(gs_engine* e, int64_t n) { GS_TRY(e->eng->advance(n)) }
 int gs_exchange(gs_engine* e) { GS_TRY(e->eng->exchange()) }
 int64_t gs_get_step(gs_engine* e) { return e->eng->step(); }

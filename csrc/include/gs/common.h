@@ -183,6 +183,10 @@ struct HaloMsg {
 
 struct HaloPlan {
   int32_t nsend, nrecv;
+  // 1: the only neighbours are along z and every message is a run of whole storage planes
+  // (x/y ghosts and row padding included), i.e. one contiguous range of the field buffer that
+  // a transport can send / receive in place, without pack / unpack kernels
+  int32_t zplanes;
   HaloMsg send[kMaxMsgs];
   HaloMsg recv[kMaxMsgs];
   int64_t send_cells, recv_cells;
@@ -211,14 +215,31 @@ inline Box side_box(const Geom& g, int dx, int dy, int dz, bool ghost) {
 // nbr[27]: peer rank for each direction or -1.  Messages to the same peer are ordered so
 // that the k-th send from A to B matches the k-th receive at B from A: sends ascend in d,
 // receives descend in d (the matching send for recv d is the peer's send -d = 26-d).
+inline bool z_only_neighbours(const int32_t* nbr) {
+  for (int d = 0; d < 27; ++d) {
+    int dx, dy, dz; dir_of(d, dx, dy, dz);
+    if ((dx != 0 || dy != 0) && nbr[d] >= 0) return false;
+  }
+  return true;
+}
+
+// Storage-plane form of a z message box: the full padded plane extent in x and y.
+inline Box full_planes(const Geom& g, Box b) {
+  b.x0 = -g.xo; b.nx = g.px;
+  b.y0 = -g.H; b.ny = g.py;
+  return b;
+}
+
 inline HaloPlan make_halo_plan(const Geom& g, const int32_t* nbr, bool diagonals) {
   HaloPlan p{};
+  p.zplanes = z_only_neighbours(nbr) ? 1 : 0;
   int64_t off = 0;
   for (int d = 0; d < 27; ++d) {
     if (d == 13 || nbr[d] < 0) continue;
     int dx, dy, dz; dir_of(d, dx, dy, dz);
     if (!diagonals && (dx != 0) + (dy != 0) + (dz != 0) != 1) continue;
     HaloMsg m; m.dir = d; m.peer = nbr[d]; m.box = side_box(g, dx, dy, dz, false); m.offset = off;
+    if (p.zplanes) m.box = full_planes(g, m.box);
     off += box_cells(m.box);
     p.send[p.nsend++] = m;
   }
@@ -229,12 +250,16 @@ inline HaloPlan make_halo_plan(const Geom& g, const int32_t* nbr, bool diagonals
     int dx, dy, dz; dir_of(d, dx, dy, dz);
     if (!diagonals && (dx != 0) + (dy != 0) + (dz != 0) != 1) continue;
     HaloMsg m; m.dir = d; m.peer = nbr[d]; m.box = side_box(g, dx, dy, dz, true); m.offset = off;
+    if (p.zplanes) m.box = full_planes(g, m.box);
     off += box_cells(m.box);
     p.recv[p.nrecv++] = m;
   }
   p.recv_cells = off;
   return p;
 }
+
+// Element offset of a message box's first cell in the field buffer (contiguous for zplanes).
+inline int64_t box_start(const Geom& g, const Box& b) { return lin(g, b.x0, b.y0, b.z0); }
 
 // Region updated by fused step s (0-based) of an n-step pass: the interior grown by
 // (n-1-s) cells on every side that has a neighbour (ghost data valid there), never on a

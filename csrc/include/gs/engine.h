@@ -38,6 +38,24 @@ class Backend {
   // optional one-time preparation (autotuning) of the fused kernel for depth n; must not
   // change the state held in buffer src
   virtual void prepare_fused(int src, int dst, int n, int64_t t) { (void)src; (void)dst; (void)n; (void)t; }
+  // fused() restricted to the output z-runs [zlo0, +zlen0) and [zlo1, +zlen1) (zlen1 may be 0).
+  // Supported exactly when fused_supported(n); reads level-0 planes zlo-n .. zend+n-1 only.
+  virtual bool fused_supported(int n) const { (void)n; return false; }
+  virtual bool fused_runs(int src, int dst, int n, int64_t t, int zlo0, int zlen0, int zlo1,
+                          int zlen1) {
+    (void)src; (void)dst; (void)n; (void)t; (void)zlo0; (void)zlen0; (void)zlo1; (void)zlen1;
+    return false;
+  }
+  // in-place transport of a zplanes plan straight from / into field buffer b (no pack)
+  virtual bool native_exchange_inplace(int b, const HaloPlan& p) { (void)b; (void)p; return false; }
+  // asynchronous communication stream.  comm_fork: the comm stream waits for the compute
+  // work issued so far; comm_join: the compute stream waits for the comm work issued so far;
+  // comm_select(true) routes pack / unpack / self_copy / native_exchange* / host_sync to the
+  // comm stream, comm_select(false) back to the compute stream.
+  virtual bool has_comm_stream() const { return false; }
+  virtual void comm_fork() {}
+  virtual void comm_join() {}
+  virtual void comm_select(bool on) { (void)on; }
   virtual void pack(int b, const HaloPlan& p) = 0;
   virtual void unpack(int b, const HaloPlan& p) = 0;
   // copy send-buffer cells [src_off, +n) to recv-buffer cells [dst_off, +n)
@@ -67,7 +85,11 @@ class Engine {
   Engine(const EngineConfig& c, Backend* be) : cfg_(c), be_(be) {
     if (c.fuse < 1 || c.fuse > c.g.H) throw std::runtime_error("fuse must be in [1, H]");
     int nb = 0;
-    for (int d = 0; d < 27; ++d) if (d != 13 && c.nbr[d] >= 0) ++nb;
+    for (int d = 0; d < 27; ++d) {
+      if (d == 13 || c.nbr[d] < 0) continue;
+      ++nb;
+      if (c.nbr[d] != c.rank) has_remote_ = true;
+    }
     has_nbr_ = nb > 0;
     plan_ = make_halo_plan(c.g, c.nbr, c.g.H > 1 || c.fuse > 1);
     bc_parity_[0] = bc_parity_[1] = -1;
@@ -80,6 +102,14 @@ class Engine {
   int64_t step() const { return t_; }
   void set_step(int64_t t) { t_ = t; bc_parity_[0] = bc_parity_[1] = -1; }
   void set_transport(TransportFn fn, void* user) { tfn_ = fn; tuser_ = user; }
+  // comm/compute overlap: -1 auto (on when the plan is zplanes and a comm stream exists),
+  // 0 off, 1 on where possible
+  void set_overlap(int mode) { overlap_ = mode; }
+  // whether a pass of k steps runs with the halo exchange overlapped with the inner planes
+  bool overlapped(int k) const {
+    return overlap_ != 0 && cfg_.use_fused && k > 1 && has_remote_ && plan_.zplanes &&
+           be_->has_comm_stream() && be_->fused_supported(k) && cfg_.g.nz >= 2 * k + 1;
+  }
   double comm_calls() const { return (double)ncomm_; }
 
   // Reference init (Simulation_CPU.jl:14-65): u = 1 everywhere (ghosts included), v = 0,
@@ -109,7 +139,19 @@ class Engine {
   }
 
   void exchange() {
+    exchange_start();
+    exchange_finish();
+  }
+
+  // Stage 1 of a halo exchange: everything that can be issued without blocking the host
+  // (pack, periodic self copies, RCCL send/recv -- in place for a zplanes plan).
+  void exchange_start() {
+    xpending_ = kNone;
     if (!has_nbr_) return;
+    if (plan_.zplanes && has_remote_ && be_->native_exchange_inplace(cur_, plan_)) {
+      ++ncomm_;
+      return;  // nothing to unpack
+    }
     be_->pack(cur_, plan_);
     // self messages (periodic wrap onto the same rank)
     bool remote = false;
@@ -124,15 +166,26 @@ class Engine {
         remote = true;
       }
     }
+    xpending_ = kUnpack;
     if (remote) {
       ++ncomm_;
       if (!be_->native_exchange(plan_)) {
         if (!tfn_) throw std::runtime_error("halo exchange needs a transport (RCCL or callback)");
-        be_->host_sync();
-        if (tfn_(tuser_) != 0) throw std::runtime_error("transport callback failed");
+        xpending_ = kCallback;
       }
     }
-    be_->unpack(cur_, plan_);
+  }
+
+  // Stage 2: host-side transports (callback) and the unpack.
+  void exchange_finish(bool on_comm = false) {
+    if (xpending_ == kCallback) {
+      be_->host_sync();
+      if (tfn_(tuser_) != 0) throw std::runtime_error("transport callback failed");
+      // the callback's device copies were issued on the compute stream
+      if (on_comm) be_->comm_fork();
+    }
+    if (xpending_ != kNone) be_->unpack(cur_, plan_);
+    xpending_ = kNone;
   }
 
   // Fill the outer (global-boundary) ghost shells of buffer b with the boundary value of
@@ -163,8 +216,28 @@ class Engine {
   void advance(int64_t nsteps) {
     while (nsteps > 0) {
       const int k = (int)(nsteps < cfg_.fuse ? nsteps : cfg_.fuse);
-      exchange();
       const int oth = 1 - cur_;
+      if (overlapped(k)) {
+        // Inner planes [k, nz-k) need no halo: run them while the exchange is in flight on
+        // the comm stream, then the two k-plane boundary slabs once it has landed.
+        const int nz = cfg_.g.nz;
+        ensure_bc(cur_, t_);  // before the fork: the exchanged planes carry these ghosts
+        be_->comm_fork();
+        be_->comm_select(true);
+        exchange_start();
+        be_->comm_select(false);
+        be_->fused_runs(cur_, oth, k, t_, k, nz - 2 * k, 0, 0);
+        be_->comm_select(true);
+        exchange_finish(true);
+        be_->comm_select(false);
+        be_->comm_join();
+        be_->fused_runs(cur_, oth, k, t_, 0, k, nz - k, k);
+        cur_ = oth;
+        t_ += k;
+        nsteps -= k;
+        continue;
+      }
+      exchange();
       if (k > 1 && cfg_.use_fused) {
         ensure_bc(cur_, t_);
         if (be_->fused(cur_, oth, k, t_)) {
@@ -190,6 +263,10 @@ class Engine {
   Backend* be_;
   HaloPlan plan_;
   bool has_nbr_ = false;
+  bool has_remote_ = false;
+  int overlap_ = -1;
+  enum { kNone, kUnpack, kCallback };
+  int xpending_ = kNone;
   int cur_ = 0;
   int64_t t_ = 0;
   int bc_parity_[2];

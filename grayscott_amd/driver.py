@@ -28,7 +28,7 @@ from .io.checkpoint import restart as do_restart
 from .io.checkpoint import write_checkpoint
 from .io.output import SimulationOutput
 from .models.grayscott import GrayScott
-from .parallel.decomp import init_domain
+from .parallel.decomp import choose_dims, init_domain
 from .parallel.dist import init_from_env
 from .utils.config import Settings, get_settings, load_backend_and_lang
 from .utils.timers import PerfLog, PhaseTimer
@@ -43,7 +43,9 @@ def initialization(args: Sequence[str]):
 def initialize_from_settings(settings: Settings):
     backend, _ = load_backend_and_lang(settings)
     ctx = init_from_env(backend)
-    domain = init_domain(settings.L, ctx.world_size, ctx.rank, periodic=settings.periodic)
+    dims = choose_dims(settings.L, ctx.world_size, settings.decomposition, backend)
+    domain = init_domain(settings.L, ctx.world_size, ctx.rank, periodic=settings.periodic,
+                         dims=dims)
     sim = GrayScott(settings, domain, ctx)
     sim.init_fields()
     return ctx, settings, domain, sim

@@ -84,6 +84,10 @@ class GrayScott:
                                     domain.rank, fuse, use_fused, self.buffers[0].data_ptr(),
                                     self.buffers[1].data_ptr(), self.sendbuf.data_ptr(),
                                     self.recvbuf.data_ptr(), stream)
+        ov = str(getattr(settings, "overlap", "auto")).lower()
+        if ov not in ("auto", "on", "off", "true", "false", "1", "0"):
+            raise ValueError(f"overlap must be auto | on | off, not {ov!r}")
+        self.engine.set_overlap(-1 if ov == "auto" else (1 if ov in ("on", "true", "1") else 0))
         self.transport = "none"
         if domain.has_neighbors and any(r != domain.rank for i, r in enumerate(domain.nbr27)
                                         if i != 13 and r >= 0):
@@ -124,6 +128,11 @@ class GrayScott:
         else:
             raise ValueError(f"unknown transport {kind!r}")
         self.transport = kind
+
+    @property
+    def overlapped(self) -> bool:
+        """Whether full-depth passes overlap their halo exchange with the inner planes."""
+        return self.engine.overlapped(self.fuse)
 
     # ------------------------------------------------------------------------------------
     def init_fields(self) -> None:

@@ -63,6 +63,12 @@ def _declare(lib) -> None:
         getattr(lib, name).restype = c_int
     lib.gs_advance.argtypes = [c_void_p, c_int64]
     lib.gs_advance.restype = c_int
+    lib.gs_plan_zplanes.argtypes = [c_void_p]
+    lib.gs_plan_zplanes.restype = c_int
+    lib.gs_set_overlap.argtypes = [c_void_p, c_int32]
+    lib.gs_set_overlap.restype = c_int
+    lib.gs_overlapped.argtypes = [c_void_p, c_int32]
+    lib.gs_overlapped.restype = c_int
     lib.gs_get_step.argtypes = [c_void_p]
     lib.gs_get_step.restype = c_int64
     lib.gs_set_step.argtypes = [c_void_p, c_int64]
@@ -207,6 +213,13 @@ class Engine:
             return None
         return fused_cfg_name(int(out[0])), int(out[1]), float(ms.value)
 
+    def set_overlap(self, mode: int):
+        """-1 auto, 0 off, 1 on (where the plan and backend allow it)."""
+        self._chk(self.lib.gs_set_overlap(self.h, int(mode)), "set_overlap")
+
+    def overlapped(self, k: int) -> bool:
+        return bool(self.lib.gs_overlapped(self.h, int(k)))
+
     def advance(self, n: int):
         self._chk(self.lib.gs_advance(self.h, int(n)), "advance")
 
@@ -259,7 +272,8 @@ class Engine:
         ns, nr = c_int32(), c_int32()
         self.lib.gs_plan_info(self.h, ctypes.byref(sc), ctypes.byref(rc), ctypes.byref(ns),
                               ctypes.byref(nr))
-        out = {"send_cells": sc.value, "recv_cells": rc.value, "send": [], "recv": []}
+        out = {"send_cells": sc.value, "recv_cells": rc.value, "send": [], "recv": [],
+               "zplanes": bool(self.lib.gs_plan_zplanes(self.h))}
         buf = (c_int64 * 4)()
         for which, key, n in ((0, "send", ns.value), (1, "recv", nr.value)):
             for i in range(n):

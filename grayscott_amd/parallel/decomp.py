@@ -162,5 +162,28 @@ def init_domain(L, nprocs: int, rank: int, periodic: bool = False,
                       proc_offsets=offsets, periodic=periodic, proc_neighbors=names, nbr27=nbr27)
 
 
+def choose_dims(L, nprocs: int, mode: str = "auto", backend: str = "cpu") -> List[int]:
+    """Process grid for ``nprocs`` ranks.
+
+    * ``"balanced"`` -- MPI_Dims_create (the reference's choice, communication.jl:36-40);
+    * ``"z"``        -- 1 x 1 x nprocs slabs along z (the slowest storage axis);
+    * ``"auto"``     -- z slabs on the MI355X backend while every slab keeps >= 32 planes,
+      else balanced.  Slabs keep the full 64-lane x extent of the fused kernel's tiles, need
+      no pack / unpack (each halo is a contiguous run of whole storage planes sent in place by
+      RCCL) and let the exchange overlap the inner planes' update (engine.h, ``overlapped``).
+    """
+    mode = (mode or "auto").lower()
+    Lz = L if isinstance(L, int) else int(L[2])
+    if mode == "balanced" or nprocs == 1:
+        return dims_create(nprocs)
+    if mode == "z":
+        return [1, 1, nprocs]
+    if mode != "auto":
+        raise ValueError(f"unknown decomposition {mode!r} (auto | balanced | z)")
+    if backend == "hip" and Lz // nprocs >= 32:
+        return [1, 1, nprocs]
+    return dims_create(nprocs)
+
+
 def all_domains(L, nprocs: int, periodic: bool = False) -> List[CartDomain]:
     return [init_domain(L, nprocs, r, periodic) for r in range(nprocs)]

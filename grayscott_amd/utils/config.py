@@ -13,7 +13,9 @@ Deliberate fixes: ``precision`` is whitelisted instead of ``ev
 Extension keys (not in the reference, all optional, documented in README):
   ``periodic`` (bool), ``seed`` (int, noise stream key), ``fuse_steps`` (int, steps fused per
   halo exchange / temporal blocking depth, 0 = auto), ``transport`` ("auto"|"rccl"|"torch"),
-  ``output_engine`` ("bp4"), ``perf_log`` (path of a JSON-lines perf log), ``diagnostics`` (bool).
+  ``output_engine`` ("bp4"), ``perf_log`` (path of a JSON-lines perf log), ``diagnostics`` (bool),
+  ``decomposition`` ("auto"|"balanced"|"z": process grid, see parallel/decomp.choose_dims),
+  ``overlap`` ("auto"|"on"|"off": overlap the halo exchange with the inner-plane update).
 """
 from __future__ import annotations
 
@@ -72,6 +74,8 @@ class Settings:
     output_engine: str = "bp4"
     perf_log: str = ""
     diagnostics: bool = False
+    decomposition: str = "auto"
+    overlap: str = "auto"
 
     # -------------------------------------------------------------------------------------
     @property
@@ -114,6 +118,8 @@ EXTENSION_KEYS: Dict[str, str] = {
     "output_engine": _STRING,
     "perf_log": _STRING,
     "diagnostics": _BOOL,
+    "decomposition": _STRING,
+    "overlap": _STRING,
 }
 
 # Keys present in reference configs but commented out of the struct (Structs.jl:20-22):

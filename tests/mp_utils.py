@@ -31,13 +31,14 @@ def _worker(rank, world, port, outdir, cfg):
                            "OMP_NUM_THREADS": "1"})
         from grayscott_amd.models.grayscott import GrayScott
         from grayscott_amd.parallel import dist as gdist
-        from grayscott_amd.parallel.decomp import init_domain
+        from grayscott_amd.parallel.decomp import choose_dims, init_domain
         from grayscott_amd.utils.config import Settings
 
         settings = Settings(**cfg["settings"])
         backend = "hip" if settings.backend.lower() in ("amdgpu", "hip", "gpu") else "cpu"
         ctx = gdist.init_from_env(backend)
-        dom = init_domain(settings.L, world, rank, periodic=settings.periodic)
+        dims = choose_dims(settings.L, world, settings.decomposition, backend)
+        dom = init_domain(settings.L, world, rank, periodic=settings.periodic, dims=dims)
         sim = GrayScott(settings, dom, ctx, fuse=cfg.get("fuse"), transport=cfg.get("transport"),
                         use_fused=cfg.get("use_fused", True))
         sim.init_fields()
@@ -45,7 +46,8 @@ def _worker(rank, world, port, outdir, cfg):
         u, v = sim.get_fields()
         np.savez(os.path.join(outdir, f"rank{rank}.npz"), u=u, v=v,
                  offsets=np.array(dom.proc_offsets), sizes=np.array(dom.proc_sizes),
-                 step=sim.step, transport=sim.transport)
+                 step=sim.step, transport=sim.transport, overlapped=sim.overlapped,
+                 zplanes=sim.engine.plan()["zplanes"])
         sim.close()
         ctx.barrier()
         ctx.finalize()
@@ -78,5 +80,6 @@ def run_ranks(world: int, cfg: dict, timeout: float = 240.0):
             sl = (slice(o[2], o[2] + s[2]), slice(o[1], o[1] + s[1]), slice(o[0], o[0] + s[0]))
             u[sl] = d["u"]
             v[sl] = d["v"]
-            meta.append({"step": int(d["step"]), "transport": str(d["transport"])})
+            meta.append({"step": int(d["step"]), "transport": str(d["transport"]),
+                         "overlapped": bool(d["overlapped"]), "zplanes": bool(d["zplanes"])})
         return u, v, meta

@@ -98,3 +98,33 @@ def test_decomposed_run_matches_single_rank(world, L, fuse, periodic):
     assert meta[0]["transport"] == "torch"
     np.testing.assert_array_equal(un, u1)
     np.testing.assert_array_equal(vn, v1)
+
+
+@pytest.mark.parametrize("world,L,fuse,periodic", [
+    (2, 16, 2, False),
+    (4, 21, 3, False),   # uneven slabs
+    (3, 17, 1, False),
+    (2, 12, 2, True),    # periodic: x/y wrap onto self, so the generic 26-direction plan
+])
+def test_z_slab_decomposition_matches_single_rank(world, L, fuse, periodic):
+    """1 x 1 x N slabs: halos are whole storage planes (zplanes plan) -- same answer."""
+    steps = 7
+    u1, v1, _ = run_ranks(1, _cfg(L, steps, 1, periodic))
+    cfg = _cfg(L, steps, fuse, periodic)
+    cfg["settings"]["decomposition"] = "z"
+    un, vn, meta = run_ranks(world, cfg)
+    assert all(m["zplanes"] == (not periodic) for m in meta)
+    np.testing.assert_array_equal(un, u1)
+    np.testing.assert_array_equal(vn, v1)
+
+
+def test_choose_dims():
+    from grayscott_amd.parallel.decomp import choose_dims
+    assert choose_dims(512, 8, "auto", "hip") == [1, 1, 8]
+    assert choose_dims(512, 8, "auto", "cpu") == dims_create(8)
+    assert choose_dims(64, 8, "auto", "hip") == dims_create(8)   # 8-plane slabs: balanced
+    assert choose_dims(64, 4, "balanced", "hip") == dims_create(4)
+    assert choose_dims(64, 4, "z", "cpu") == [1, 1, 4]
+    assert choose_dims(64, 1, "z", "hip") == [1, 1, 1]
+    with pytest.raises(ValueError):
+        choose_dims(64, 4, "diagonal", "hip")

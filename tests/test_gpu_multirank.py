@@ -41,3 +41,23 @@ def test_gpu_decomposed_matches_single_rank(world, L, fuse, periodic, prec):
     tol = 0 if prec == "Float64" else 0
     np.testing.assert_allclose(un, u1, rtol=0, atol=tol)
     np.testing.assert_allclose(vn, v1, rtol=0, atol=tol)
+
+
+@pytest.mark.parametrize("world,L,fuse,prec,overlap", [
+    (2, 48, 2, "Float32", "on"),
+    (4, 64, 3, "Float32", "on"),
+    (3, 40, 2, "Float64", "on"),
+    (2, 48, 3, "Float32", "off"),
+])
+def test_gpu_z_slabs_overlap_matches_single_rank(world, L, fuse, prec, overlap):
+    """z-slab decomposition: the inner planes run while the halo exchange is in flight on the
+    comm stream, the boundary slabs after it lands -- bit-identical to one rank."""
+    steps = 11
+    u1, v1, _ = run_ranks(1, _cfg(L, steps, fuse, False, prec))
+    cfg = _cfg(L, steps, fuse, False, prec)
+    cfg["settings"].update(decomposition="z", overlap=overlap)
+    un, vn, meta = run_ranks(world, cfg)
+    assert all(m["zplanes"] for m in meta)
+    assert all(m["overlapped"] == (overlap == "on") for m in meta)
+    np.testing.assert_array_equal(un, u1)
+    np.testing.assert_array_equal(vn, v1)
