@@ -10,8 +10,10 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <chrono>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "gs/capi_impl.h"
@@ -108,13 +110,13 @@ class HipBackend final : public gs::Backend {
   bool fused_supported(int n) const override { return gsk::fused_supported(g_, n); }
 
   bool fused_runs(int src, int dst, int n, int64_t t, int zlo0, int zlen0, int zlo1,
-                  int zlen1) override {
+                  int zlen1, bool leave_room) override {
     if (!gsk::fused_supported(g_, n)) return false;
     if (!tuned_[n]) autotune(src, dst, n, t);
     const bool pin = fused_pinned();
     const bool ok = gsk::launch_fused<T>(buf_[src], buf_[dst], g_, p_, n, t, stream_,
                                          pin ? -1 : cfg_[n], pin ? -1 : sched_[n], zlo0, zlen0,
-                                         zlo1, zlen1);
+                                         zlo1, zlen1, leave_room ? reserve_ : 0);
     if (!ok) throw std::runtime_error("fused_runs: invalid z-runs");
     HIP_CHECK(hipGetLastError());
     return true;
@@ -252,6 +254,42 @@ class HipBackend final : public gs::Backend {
 
   void host_sync() override { HIP_CHECK(hipStreamSynchronize(xs_)); }
 
+  // Watchdog wait: poll both streams and RCCL's asynchronous error state; a
+  // transport error or no completion within timeout_s aborts the communicator and throws, so
+  // one failed rank ends the job instead of hanging it.
+  void wait_all(double timeout_s) override {
+    if (!comm_) {
+      HIP_CHECK(hipStreamSynchronize(stream_));
+      HIP_CHECK(hipStreamSynchronize(comm_stream_));
+      return;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    int sleep_us = 20;
+    for (;;) {
+      const hipError_t a = hipStreamQuery(stream_);
+      const hipError_t b = hipStreamQuery(comm_stream_);
+      if (a == hipSuccess && b == hipSuccess) return;
+      if (a != hipErrorNotReady) HIP_CHECK(a);
+      if (b != hipErrorNotReady) HIP_CHECK(b);
+      ncclResult_t async = ncclSuccess;
+      NCCL_CHECK(ncclCommGetAsyncError(comm_, &async));
+      if (async != ncclSuccess) {
+        ncclCommAbort(comm_);
+        comm_ = nullptr;
+        throw std::runtime_error(std::string("RCCL asynchronous error: ") + ncclGetErrorString(async));
+      }
+      const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (timeout_s > 0 && el > timeout_s) {
+        ncclCommAbort(comm_);
+        comm_ = nullptr;
+        throw std::runtime_error("halo exchange watchdog: device work not finished after " +
+                                 std::to_string(timeout_s) + " s (GS_COMM_TIMEOUT)");
+      }
+      std::this_thread::sleep_for(std::chrono::microseconds(sleep_us));
+      if (sleep_us < 100) sleep_us *= 2;  // bounded latency: timed regions end in this wait
+    }
+  }
+
   void extract(int b, void* u, void* v) override {
     gsk::launch_extract<T>(buf_[b], (T*)u, (T*)v, g_, stream_);
     HIP_CHECK(hipGetLastError());
@@ -294,6 +332,8 @@ class HipBackend final : public gs::Backend {
   hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
   hipStream_t comm_stream_ = nullptr;
   hipStream_t xs_ = nullptr;  // stream for halo traffic (compute or comm stream)
+  // workgroup slots left free for RCCL while the inner-plane kernel runs (GS_OVERLAP_RESERVE)
+  int reserve_ = getenv("GS_OVERLAP_RESERVE") ? atoi(getenv("GS_OVERLAP_RESERVE")) : 16;
   bool inplace_off_ = getenv("GS_INPLACE_HALO") && atoi(getenv("GS_INPLACE_HALO")) == 0;
   int dev_ = 0;
   ncclComm_t comm_ = nullptr;

@@ -32,6 +32,7 @@ struct FusedArgs {
   int32_t cfg;     // tile/prefetch configuration index (fused_cfg_names)
   int64_t t;
   int64_t buf_bytes;  // bytes of one state buffer (descriptor range)
+  int32_t reserve;    // workgroup slots to leave free (comm kernels running alongside)
   // output z-runs [zlo[r], zlo[r] + zlen[r]) (zlen[1] may be 0); a tile's units enumerate the
   // planes of run 0 then run 1 (nzv = zlen[0] + zlen[1] units per tile)
   int32_t zlo[2], zlen[2];
@@ -390,7 +391,7 @@ struct FusedLaunch {
       (void)hipGetDevice(&dev);
       if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
     }
-    const int64_t slots = (int64_t)occupancy() * cus;
+    const int64_t slots = std::max<int64_t>(1, (int64_t)occupancy() * cus - a.reserve);
     // enough planes per workgroup to amortise the 2T-plane pipeline fill, but at least one
     // workgroup per (tile, z-run) so short runs (comm/compute-overlap slabs) stay parallel
     const int nruns = a.zlen[1] > 0 ? 2 : 1;
@@ -524,7 +525,8 @@ inline bool fused_supported(const Geom& g, int n) {
 template <typename T>
 bool launch_fused(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, const Geom& g,
                   const gs::Params& p, int n, int64_t t, hipStream_t st, int cfg = -1,
-                  int sched = -1, int zlo0 = 0, int zlen0 = -1, int zlo1 = 0, int zlen1 = 0) {
+                  int sched = -1, int zlo0 = 0, int zlen0 = -1, int zlo1 = 0, int zlen1 = 0,
+                  int reserve = 0) {
   if (!fused_supported(g, n)) return false;
   FusedArgs a{};
   if (zlen0 < 0) zlen0 = g.nz;
@@ -534,6 +536,7 @@ bool launch_fused(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, co
   a.zlo[0] = zlo0; a.zlen[0] = zlen0;
   a.zlo[1] = zlo1; a.zlen[1] = zlen1;
   a.nzv = zlen0 + zlen1;
+  a.reserve = reserve > 0 ? reserve : 0;
   a.g = g;
   a.t = t;
   a.cfg = cfg >= 0 ? cfg : fused_cfg_env();

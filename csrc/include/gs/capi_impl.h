@@ -6,6 +6,8 @@
 //   void gs_backend_post_create(gs::Engine* e);   // optional hook (may be empty)
 #pragma once
 
+#include <stdlib.h>
+
 #include <exception>
 #include <string>
 
@@ -66,12 +68,27 @@ int gs_prepare(gs_engine* e) { GS_TRY(e->eng->prepare()) }
 int gs_set_overlap(gs_engine* e, int32_t mode) { GS_TRY(e->eng->set_overlap(mode)) }
 int gs_overlapped(gs_engine* e, int32_t k) { return e->eng->overlapped(k) ? 1 : 0; }
 int gs_plan_zplanes(gs_engine* e) { return e->eng->plan().zplanes; }
+// Timing primitive: one fused k-step update of the given z-runs from the current buffer into
+// the other one (interior planes only, so the next pass overwrites it; state unchanged).
+int gs_fused_runs_raw(gs_engine* e, int32_t k, int32_t zlo0, int32_t zlen0, int32_t zlo1,
+                      int32_t zlen1) {
+  GS_TRY({
+    gs::Engine& g = *e->eng;
+    if (!g.backend()->fused_runs(g.cur(), 1 - g.cur(), k, g.step(), zlo0, zlen0, zlo1, zlen1))
+      throw std::runtime_error("fused runs unsupported for this k / backend");
+  })
+}
 int gs_advance(gs_engine* e, int64_t n) { GS_TRY(e->eng->advance(n)) }
 int gs_exchange(gs_engine* e) { GS_TRY(e->eng->exchange()) }
 int64_t gs_get_step(gs_engine* e) { return e->eng->step(); }
 int gs_set_step(gs_engine* e, int64_t t) { GS_TRY(e->eng->set_step(t)) }
 int gs_current_buffer(gs_engine* e) { return e->eng->cur(); }
-int gs_sync(gs_engine* e) { GS_TRY(e->eng->backend()->host_sync()) }
+// Waits for all queued work.  GS_COMM_TIMEOUT (seconds, default 900) bounds the wait when a
+// device transport is active: a hung or failed halo exchange becomes an error, not a hang.
+int gs_sync(gs_engine* e) {
+  static const double timeout = getenv("GS_COMM_TIMEOUT") ? atof(getenv("GS_COMM_TIMEOUT")) : 900.0;
+  GS_TRY(e->eng->backend()->wait_all(timeout))
+}
 int gs_extract(gs_engine* e, void* u, void* v) {
   GS_TRY(e->eng->backend()->extract(e->eng->cur(), u, v))
 }

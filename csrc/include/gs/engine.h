@@ -16,6 +16,7 @@
 #include <string>
 
 #include "gs/common.h"
+#include "gs/trace.h"
 
 namespace gs {
 
@@ -41,9 +42,12 @@ class Backend {
   // fused() restricted to the output z-runs [zlo0, +zlen0) and [zlo1, +zlen1) (zlen1 may be 0).
   // Supported exactly when fused_supported(n); reads level-0 planes zlo-n .. zend+n-1 only.
   virtual bool fused_supported(int n) const { (void)n; return false; }
+  // leave_room: launch fewer workgroups than the device holds so concurrently running
+  // communication kernels (RCCL) find free slots instead of waiting for this kernel to end
   virtual bool fused_runs(int src, int dst, int n, int64_t t, int zlo0, int zlen0, int zlo1,
-                          int zlen1) {
+                          int zlen1, bool leave_room = false) {
     (void)src; (void)dst; (void)n; (void)t; (void)zlo0; (void)zlen0; (void)zlo1; (void)zlen1;
+    (void)leave_room;
     return false;
   }
   // in-place transport of a zplanes plan straight from / into field buffer b (no pack)
@@ -63,6 +67,9 @@ class Backend {
   // native transport (RCCL); returns false if not configured
   virtual bool native_exchange(const HaloPlan& p) { (void)p; return false; }
   virtual void host_sync() {}
+  // wait for all queued device work; a backend with a device transport turns a hang or an
+  // asynchronous transport error into an exception after `timeout_s` seconds (watchdog)
+  virtual void wait_all(double timeout_s) { (void)timeout_s; host_sync(); }
   virtual void extract(int b, void* u, void* v) = 0;
   virtual void insert(int b, const void* u, const void* v) = 0;
   // seed cube into buffer b
@@ -146,6 +153,7 @@ class Engine {
   // Stage 1 of a halo exchange: everything that can be issued without blocking the host
   // (pack, periodic self copies, RCCL send/recv -- in place for a zplanes plan).
   void exchange_start() {
+    TraceRange tr("gs.exchange_start");
     xpending_ = kNone;
     if (!has_nbr_) return;
     if (plan_.zplanes && has_remote_ && be_->native_exchange_inplace(cur_, plan_)) {
@@ -178,6 +186,7 @@ class Engine {
 
   // Stage 2: host-side transports (callback) and the unpack.
   void exchange_finish(bool on_comm = false) {
+    TraceRange tr("gs.exchange_finish");
     if (xpending_ == kCallback) {
       be_->host_sync();
       if (tfn_(tuser_) != 0) throw std::runtime_error("transport callback failed");
@@ -191,6 +200,7 @@ class Engine {
   // Fill the outer (global-boundary) ghost shells of buffer b with the boundary value of
   // time t.  Faces cover the full ghost-extended range so edges/corners are covered too.
   void ensure_bc(int b, int64_t t) {
+    TraceRange tr("gs.ensure_bc");
     const Geom& g = cfg_.g;
     if (g.periodic) return;
     const int par = (int)(t & 1);
@@ -226,12 +236,18 @@ class Engine {
         be_->comm_select(true);
         exchange_start();
         be_->comm_select(false);
-        be_->fused_runs(cur_, oth, k, t_, k, nz - 2 * k, 0, 0);
+        {
+          TraceRange tr("gs.fused_inner");
+          be_->fused_runs(cur_, oth, k, t_, k, nz - 2 * k, 0, 0, true);
+        }
         be_->comm_select(true);
         exchange_finish(true);
         be_->comm_select(false);
         be_->comm_join();
-        be_->fused_runs(cur_, oth, k, t_, 0, k, nz - k, k);
+        {
+          TraceRange tr("gs.fused_shell");
+          be_->fused_runs(cur_, oth, k, t_, 0, k, nz - k, k);
+        }
         cur_ = oth;
         t_ += k;
         nsteps -= k;
@@ -240,6 +256,7 @@ class Engine {
       exchange();
       if (k > 1 && cfg_.use_fused) {
         ensure_bc(cur_, t_);
+        TraceRange tr("gs.fused");
         if (be_->fused(cur_, oth, k, t_)) {
           cur_ = oth;
           t_ += k;
@@ -250,6 +267,7 @@ class Engine {
       for (int s = 0; s < k; ++s) {
         ensure_bc(cur_, t_);
         const Box r = pass_region(cfg_.g, cfg_.nbr, k, s);
+        TraceRange tr("gs.step");
         be_->step(cur_, 1 - cur_, r, t_);
         cur_ = 1 - cur_;
         ++t_;

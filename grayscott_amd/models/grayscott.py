@@ -208,6 +208,24 @@ class GrayScott:
         b = self.buffers[self.engine.current if which is None else which]
         return b.view(g.pz, g.py, g.px, 2)
 
+    def poison_ghosts(self, value: float = float("nan")) -> None:
+        """Debug aid (SURVEY.md §5.2 halo poisoning): overwrite every non-interior cell of both
+        buffers -- ghost shells, row padding, neighbour halos -- with ``value`` and forget the
+        outer-boundary ghost parity.  A correct exchange / boundary refresh never lets the
+        poison reach the interior, so a following run must equal an unpoisoned one."""
+        g = self.geom
+        H, xo = g.H, g.xo
+        nx, ny, nz = self.domain.proc_sizes
+        self.engine.sync()
+        for b in self.buffers:
+            full = b.view(g.pz, g.py, g.px, 2)
+            keep = full[H:H + nz, H:H + ny, xo:xo + nx].clone()
+            full.fill_(value)
+            full[H:H + nz, H:H + ny, xo:xo + nx] = keep
+        if self.backend == "hip":
+            torch.cuda.synchronize(self.device)
+        self.engine.set_step(self.engine.step)  # outer ghosts are refilled before next use
+
     def stats(self):
         """Local [sum_u, min_u, max_u, sum_v, min_v, max_v]."""
         return self.engine.stats()

@@ -42,6 +42,8 @@ def _worker(rank, world, port, outdir, cfg):
         sim = GrayScott(settings, dom, ctx, fuse=cfg.get("fuse"), transport=cfg.get("transport"),
                         use_fused=cfg.get("use_fused", True))
         sim.init_fields()
+        if cfg.get("poison"):
+            sim.poison_ghosts()
         sim.iterate(cfg["steps"])
         u, v = sim.get_fields()
         np.savez(os.path.join(outdir, f"rank{rank}.npz"), u=u, v=v,

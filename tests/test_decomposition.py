@@ -128,3 +128,23 @@ def test_choose_dims():
     assert choose_dims(64, 1, "z", "hip") == [1, 1, 1]
     with pytest.raises(ValueError):
         choose_dims(64, 4, "diagonal", "hip")
+
+
+@pytest.mark.parametrize("world,L,fuse,periodic,decomp", [
+    (1, 14, 2, False, "balanced"),
+    (1, 12, 3, True, "balanced"),
+    (4, 16, 2, False, "balanced"),
+    (2, 16, 3, False, "z"),
+    (8, 16, 2, True, "balanced"),
+])
+def test_halo_poisoning(world, L, fuse, periodic, decomp):
+    """NaN in every ghost / padding cell before the run never reaches the interior."""
+    steps = 6
+    u1, v1, _ = run_ranks(1, _cfg(L, steps, 1, periodic))
+    cfg = _cfg(L, steps, fuse, periodic)
+    cfg["settings"]["decomposition"] = decomp
+    cfg["poison"] = True
+    un, vn, _ = run_ranks(world, cfg)
+    assert np.isfinite(un).all() and np.isfinite(vn).all()
+    np.testing.assert_array_equal(un, u1)
+    np.testing.assert_array_equal(vn, v1)

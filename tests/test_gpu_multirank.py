@@ -61,3 +61,22 @@ def test_gpu_z_slabs_overlap_matches_single_rank(world, L, fuse, prec, overlap):
     assert all(m["overlapped"] == (overlap == "on") for m in meta)
     np.testing.assert_array_equal(un, u1)
     np.testing.assert_array_equal(vn, v1)
+
+
+@pytest.mark.parametrize("world,L,fuse,decomp,overlap", [
+    (1, 40, 3, "balanced", "auto"),
+    (4, 40, 2, "balanced", "auto"),
+    (2, 48, 2, "z", "on"),
+])
+def test_gpu_halo_poisoning(world, L, fuse, decomp, overlap):
+    """NaN in every ghost / padding cell (incl. the fused kernel's masked lanes) never
+    reaches the interior, with the fused kernel, the z-slab overlap and packed halos."""
+    steps = 9
+    u1, v1, _ = run_ranks(1, _cfg(L, steps, fuse))
+    cfg = _cfg(L, steps, fuse)
+    cfg["settings"].update(decomposition=decomp, overlap=overlap)
+    cfg["poison"] = True
+    un, vn, _ = run_ranks(world, cfg)
+    assert np.isfinite(un).all() and np.isfinite(vn).all()
+    np.testing.assert_array_equal(un, u1)
+    np.testing.assert_array_equal(vn, v1)
