@@ -96,6 +96,46 @@ __device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, int voff, int s
   __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, soff, 0);
 }
 
+// a ^ b ^ c in one gfx950 instruction (the compiler does not form v_bitop3 from xor chains)
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(c));
+  return r;
+}
+
+// Device form of gs::noise_block (same stream, bit for bit).
+//  * The 10-round key schedule is rebuilt from an opaque copy of the seed at every call:
+//    otherwise the compiler hoists the 20 loop-invariant key words out of the plane loop, runs
+//    out of SGPRs and spills them to VGPR lanes (one v_readlane per use in the hot loop).
+//    Rebuilt, they are 20 SALU adds.
+//  * Rounds 1-2 still see wave-uniform counter words (step, and its products), which the
+//    compiler folds on the SALU; from round 3 on every word varies per lane and each output
+//    word's two xors become one v_bitop3.
+__device__ __forceinline__ gs::U4 noise_block_dev(int64_t gx, int64_t gy4, int64_t gz, int64_t Lx,
+                                                  int64_t Ly, uint64_t step, uint64_t seed) {
+  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+  asm volatile("" : "+s"(k0), "+s"(k1));
+  const uint64_t Ly4 = ((uint64_t)Ly + 3) >> 2;
+  const uint64_t q = (uint64_t)gx + (uint64_t)Lx * ((uint64_t)gy4 + Ly4 * (uint64_t)gz);
+  uint32_t c0 = (uint32_t)q, c1 = (uint32_t)(q >> 32), c2 = (uint32_t)step,
+           c3 = (uint32_t)(step >> 32);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r < 2) {
+      gs::philox_round(c0, c1, c2, c3, k0, k1);
+    } else {
+      const uint64_t m0 = (uint64_t)0xD2511F53u * c0;
+      const uint64_t m1 = (uint64_t)0xCD9E8D57u * c2;
+      const uint32_t n0 = xor3((uint32_t)(m1 >> 32), c1, k0);
+      const uint32_t n2 = xor3((uint32_t)(m0 >> 32), c3, k1);
+      c0 = n0; c1 = (uint32_t)m1; c2 = n2; c3 = (uint32_t)m0;
+    }
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return gs::U4{c0, c1, c2, c3};
+}
+
 // Compile-time configuration of one fused-kernel instantiation.
 //   ROWS x WAVES : rows per wave x waves per workgroup (tile height = ROWS*WAVES)
 //   PF           : level-0 prefetch distance in planes (register ring of PF+2 planes)
@@ -112,7 +152,8 @@ struct FCfg {
   static constexpr int TL = TL_, ROWS = ROWS_, WAVES = WAVES_, PF = PF_;
   static constexpr bool PERIODIC = PERIODIC_, NOISE = NOISE_, SKEW = SKEW_;
   // ablation (timing experiments only, results are WRONG): bit0 = no workgroup barriers,
-  // bit1 = every level-0 load reads plane 0 (L2-resident)
+  // bit1 = every level-0 load reads plane 0 (L2-resident); bit2 (results exact) = hoistable
+  // Philox key schedule (the pre-noise_block_dev code generation)
   static constexpr int ABL = ABL_;
   static constexpr int R = PF + 2;                    // level-0 ring slots
   static constexpr int NS = SKEW ? 3 : 2;             // level-l output ring / xch buffers
@@ -202,7 +243,8 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
       gs::U4 blk{0, 0, 0, 0};
       if constexpr (C::NOISE) {
         const int64_t gyq = gwrap<C>(sg.gy0 + 4 * m, g.Ly);
-        blk = gs::noise_block(sg.gx, gyq >> 2, gz, g.Lx, g.Ly, tstep, seed);
+        if constexpr (C::ABL & 4) blk = gs::noise_block(sg.gx, gyq >> 2, gz, g.Lx, g.Ly, tstep, seed);
+        else blk = noise_block_dev(sg.gx, gyq >> 2, gz, g.Lx, g.Ly, tstep, seed);
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -427,7 +469,8 @@ inline const char* const* fused_cfg_names(int* n) {
   static const char* names[] = {"",       "4x8:1",  "4x8:2",  "4x8:4",   "8x4:1",   "8x4:2",
                                 "4x16:2", "8x8:2",  "4x8:3",  "8x4:2w3", "8x4:1w3", "4x8:2w4",
                                 "8x4:3",  "4x6:2",  "4x12:2", "4x4:2",   "4x12:3",  "8x4:1s",
-                                "8x4:4s", "4x8:1s", "4x8:4s", "abl1",   "abl2",    "abl3"};
+                                "8x4:4s", "4x8:1s", "4x8:4s", "abl1",   "abl2",    "abl3",
+                                "4x8:1w4", "4x16:1", "4x16:2w4", "4x8:2w3", "abl4", "4x8:1abl4"};
   *n = (int)(sizeof(names) / sizeof(names[0]));
   return names;
 }
@@ -469,6 +512,7 @@ void run_fused_cfg(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, c
   if constexpr (sizeof(T) == 4 && !PER && NZ) {
     switch (a.cfg) {
       case 1: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ>, T>::run(s, d, a, p, st); return;
+      case 2: FusedLaunch<FCfg<T, TL, 4, 8, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
       case 3: FusedLaunch<FCfg<T, TL, 4, 8, 4, PER, NZ>, T>::run(s, d, a, p, st); return;
       case 4: FusedLaunch<FCfg<T, TL, 8, 4, 1, PER, NZ>, T>::run(s, d, a, p, st); return;
       case 5: FusedLaunch<FCfg<T, TL, 8, 4, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
@@ -490,6 +534,12 @@ void run_fused_cfg(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, c
       case 21: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, 1, false, 1>, T>::run(s, d, a, p, st); return;
       case 22: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, 1, false, 2>, T>::run(s, d, a, p, st); return;
       case 23: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, 1, false, 3>, T>::run(s, d, a, p, st); return;
+      case 24: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, 4>, T>::run(s, d, a, p, st); return;
+      case 25: FusedLaunch<FCfg<T, TL, 4, 16, 1, PER, NZ>, T>::run(s, d, a, p, st); return;
+      case 26: FusedLaunch<FCfg<T, TL, 4, 16, 2, PER, NZ, 4>, T>::run(s, d, a, p, st); return;
+      case 27: FusedLaunch<FCfg<T, TL, 4, 8, 2, PER, NZ, 3>, T>::run(s, d, a, p, st); return;
+      case 28: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, 1, false, 4>, T>::run(s, d, a, p, st); return;
+      case 29: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, 1, false, 4>, T>::run(s, d, a, p, st); return;
       default: break;
     }
   }

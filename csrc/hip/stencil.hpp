@@ -23,10 +23,10 @@
 // Lanes without a source receive 0 (they only ever feed tile-halo cells).
 // ------------------------------------------------------------------------------------------
 __device__ __forceinline__ float lane_from_left(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, false));
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, true));
 }
 __device__ __forceinline__ float lane_from_right(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, false));
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, true));
 }
 __device__ __forceinline__ double lane_from_left(double v) {
   const long long b = __double_as_longlong(v);
