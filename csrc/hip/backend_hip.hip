@@ -172,12 +172,12 @@ class HipBackend final : public gs::Backend {
     struct Cand { int cfg, sched; };
     std::vector<Cand> cands;
     const bool variants = !g_.periodic && p_.noise != 0.0;  // tile variants instantiated here
-    if (!variants) cands = {{0, 0}, {0, 1}};
-    else if (sizeof(T) == 4)
-      cands = {{0, 0},  {0, 1},  {1, 0},  {2, 0},  {2, 1},  {3, 0},  {5, 0},  {5, 1},
-               {8, 0},  {12, 0}, {16, 0}, {17, 0}, {18, 0}, {19, 0}, {20, 0}, {20, 1}};
-    else
-      cands = {{0, 0}, {0, 1}, {1, 0}, {1, 1}, {13, 0}, {15, 0}, {15, 1}};
+    std::vector<int> cfgs;
+    if (!variants) cfgs = {0};
+    else if (sizeof(T) == 4) cfgs = {0, 1, 2, 3, 5, 8, 12, 16, 17, 19, 20};
+    else cfgs = {0, 1, 13, 15};
+    for (int c : cfgs)
+      for (int sc = 0; sc <= 2; ++sc) cands.push_back({c, sc});
     // interleaved rounds (box-to-box and launch-to-launch jitter is several %): first launch
     // of each candidate is a warm-up, then the best of kRounds timed launches decides
     constexpr int kRounds = 3;
@@ -402,7 +402,7 @@ extern "C" {
 
 // Select the fused-kernel work schedule (0: even split, 1: XCD-grouped lockstep z-chunks).
 int gs_fused_sched(int32_t sched) {
-  if (sched < 0 || sched > 1) return -1;
+  if (sched < 0 || sched > 2) return -1;
   gsk::fused_sched_slot() = sched;
   fused_pinned() = true;
   return 0;

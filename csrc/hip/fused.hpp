@@ -330,76 +330,92 @@ __global__ __launch_bounds__(64 * C::WAVES, C::MINW) void k_fused(const typename
   sg.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   sg.pitchb = g.px * (int)sizeof(V2);
   const int nzv = a.nzv;
-  int64_t u, uend;
+  // Work list of this workgroup: logical units lu = chunk * ntiles + tile, lu0, lu0 + lstep, ...
+  // (sched 0: one "unit", the even share [u, uend) of all tile-planes).
+  // Workgroups b, b+8, b+16, ... share an XCD (round-robin dispatch; speed only, never
+  // correctness): sched 1/2 give each XCD a contiguous range of units, i.e. spatially adjacent
+  // tiles at the same z-chunk, so neighbours' shared halo lines are read while still resident
+  // in that XCD's L2.  sched 1: one unit per workgroup; sched 2: the XCD's workgroups sweep
+  // its range in lockstep rounds.
+  const int b = blockIdx.x;
+  const int nunits = a.ntiles * a.nchunk;
+  int lu0 = 0, lu1 = 1, lstep = 1;
   if (a.sched == 1) {
-    // Workgroups b, b+8, b+16, ... share an XCD (round-robin dispatch, speed only): give each
-    // XCD a contiguous range of logical units so spatially adjacent tiles sit on one L2, and
-    // let every tile's chunk start at the same z, so neighbours' shared halo lines are read
-    // while still resident.
-    const int b = blockIdx.x;
-    const int lu = (b % 8) * a.grpM + b / 8;
-    if (lu >= a.ntiles * a.nchunk) return;  // whole workgroup, before any barrier
-    const int chunk = lu / a.ntiles, tile = lu % a.ntiles;
-    u = (int64_t)tile * nzv + (int64_t)chunk * nzv / a.nchunk;
-    uend = (int64_t)tile * nzv + (int64_t)(chunk + 1) * nzv / a.nchunk;
-  } else {
-    const int64_t U = a.units;
-    u = (int64_t)blockIdx.x * U / gridDim.x;
-    uend = (int64_t)(blockIdx.x + 1) * U / gridDim.x;
+    lu0 = (b % 8) * a.grpM + b / 8;
+    lu1 = lu0 + 1;
+    if (lu0 >= nunits) return;  // whole workgroup, before any barrier
+  } else if (a.sched == 2) {
+    const int per = (nunits + 7) / 8;
+    lu0 = (b % 8) * per + b / 8;
+    lu1 = min((b % 8 + 1) * per, nunits);
+    lstep = gridDim.x / 8;
+    if (lu0 >= lu1) return;
   }
   FusedState<C> S;
 
-  while (u < uend) {
-    const int tile = (int)(u / nzv);
-    const int zv = (int)(u % nzv);
-    // a segment never crosses from one z-run into the other
-    const int run = zv < a.zlen[0] ? 0 : 1;
-    const int rv0 = run ? a.zlen[0] : 0;
-    const int rv1 = run ? nzv : a.zlen[0];
-    const int zv1 = (int)std::min<int64_t>(rv1, zv + (uend - u));
-    const int z0 = a.zlo[run] + (zv - rv0);
-    const int z1 = z0 + (zv1 - zv);
-    u += zv1 - zv;
-    const int tx = tile % a.ntx, ty = tile / a.ntx;
-    const int X0 = tx * a.xstep - TL;
-    const int Y0 = a.ybase + ty * a.ystep - TL;
-    const int x = X0 + sg.lane;
-    const int ylo = Y0 + sg.wave * ROWS;
-    // lane byte offset inside a plane (row ylo); negative values are out of range
-    sg.voff = ((ylo + g.H) * g.px + x + g.xo) * (int)sizeof(V2);
-    sg.gxu = g.ox + x;
-    sg.gx = gwrap<C>(sg.gxu, g.Lx);
-    sg.gy0 = g.oy + ylo;
-    const int ox1 = min(X0 + TL + a.xstep, g.nx);
-    const int oy0 = max(Y0 + TL, 0), oy1 = min(Y0 + TL + a.ystep, g.ny);
-    const bool xin = x >= max(X0 + TL, 0) && x < ox1;
-    sg.svoff = xin ? sg.voff : (int)0x80000000;  // masked lanes store out of range
-    sg.srow0 = max(oy0 - ylo, 0);
-    sg.srow1 = min(oy1 - ylo, ROWS);
-    sg.edge = a.bcfix &&
-        (g.ox + X0 < 0 || g.ox + X0 + 64 > g.Lx || g.oy + Y0 < 0 ||
-         g.oy + Y0 + WAVES * ROWS > g.Ly || g.oz + z0 - TL < 0 || g.oz + z1 + TL > g.Lz);
-    sg.z0 = z0;
-#pragma unroll
-    for (int l = 0; l < TL; ++l)
-#pragma unroll
-      for (int j = 0; j < ROWS; ++j) S.A[l][j].x = S.A[l][j].y = (T)0;
-    sg.p = z0 - TL;
-    sg.ldend = z1 + TL;
-    sg.pend = C::SKEW ? z1 + 2 * TL - 1 : z1 + TL;
-    const int64_t PZB = gs::plane_elems(g) * (int64_t)sizeof(V2);
-#pragma unroll
-    for (int k = 0; k < C::PF; ++k) {
-      {
-        const __amdgpu_buffer_rsrc_t r = plane_rsrc(
-            s, (int64_t)(sg.p + k + g.H) * PZB, sg.p + k < sg.ldend ? a.buf_bytes : 0);
-#pragma unroll
-        for (int j = 0; j < ROWS; ++j) S.LD[k][j] = bload(r, sg.voff + j * sg.pitchb, 0, (V2*)nullptr);
+  for (int lu = lu0; lu < lu1; lu += lstep) {
+    int64_t u, uend;
+    if (a.sched == 0) {
+      const int64_t U = a.units;
+      u = (int64_t)blockIdx.x * U / gridDim.x;
+      uend = (int64_t)(blockIdx.x + 1) * U / gridDim.x;
+    } else {
+      const int chunk = lu / a.ntiles, tile = lu % a.ntiles;
+      u = (int64_t)tile * nzv + (int64_t)chunk * nzv / a.nchunk;
+      uend = (int64_t)tile * nzv + (int64_t)(chunk + 1) * nzv / a.nchunk;
+    }
+    while (u < uend) {
+      const int tile = (int)(u / nzv);
+      const int zv = (int)(u % nzv);
+      // a segment never crosses from one z-run into the other
+      const int run = zv < a.zlen[0] ? 0 : 1;
+      const int rv0 = run ? a.zlen[0] : 0;
+      const int rv1 = run ? nzv : a.zlen[0];
+      const int zv1 = (int)std::min<int64_t>(rv1, zv + (uend - u));
+      const int z0 = a.zlo[run] + (zv - rv0);
+      const int z1 = z0 + (zv1 - zv);
+      u += zv1 - zv;
+      const int tx = tile % a.ntx, ty = tile / a.ntx;
+      const int X0 = tx * a.xstep - TL;
+      const int Y0 = a.ybase + ty * a.ystep - TL;
+      const int x = X0 + sg.lane;
+      const int ylo = Y0 + sg.wave * ROWS;
+      // lane byte offset inside a plane (row ylo); negative values are out of range
+      sg.voff = ((ylo + g.H) * g.px + x + g.xo) * (int)sizeof(V2);
+      sg.gxu = g.ox + x;
+      sg.gx = gwrap<C>(sg.gxu, g.Lx);
+      sg.gy0 = g.oy + ylo;
+      const int ox1 = min(X0 + TL + a.xstep, g.nx);
+      const int oy0 = max(Y0 + TL, 0), oy1 = min(Y0 + TL + a.ystep, g.ny);
+      const bool xin = x >= max(X0 + TL, 0) && x < ox1;
+      sg.svoff = xin ? sg.voff : (int)0x80000000;  // masked lanes store out of range
+      sg.srow0 = max(oy0 - ylo, 0);
+      sg.srow1 = min(oy1 - ylo, ROWS);
+      sg.edge = a.bcfix &&
+          (g.ox + X0 < 0 || g.ox + X0 + 64 > g.Lx || g.oy + Y0 < 0 ||
+           g.oy + Y0 + WAVES * ROWS > g.Ly || g.oz + z0 - TL < 0 || g.oz + z1 + TL > g.Lz);
+      sg.z0 = z0;
+  #pragma unroll
+      for (int l = 0; l < TL; ++l)
+  #pragma unroll
+        for (int j = 0; j < ROWS; ++j) S.A[l][j].x = S.A[l][j].y = (T)0;
+      sg.p = z0 - TL;
+      sg.ldend = z1 + TL;
+      sg.pend = C::SKEW ? z1 + 2 * TL - 1 : z1 + TL;
+      const int64_t PZB = gs::plane_elems(g) * (int64_t)sizeof(V2);
+  #pragma unroll
+      for (int k = 0; k < C::PF; ++k) {
+        {
+          const __amdgpu_buffer_rsrc_t r = plane_rsrc(
+              s, (int64_t)(sg.p + k + g.H) * PZB, sg.p + k < sg.ldend ? a.buf_bytes : 0);
+  #pragma unroll
+          for (int j = 0; j < ROWS; ++j) S.LD[k][j] = bload(r, sg.voff + j * sg.pitchb, 0, (V2*)nullptr);
+        }
+      }
+      while (fused_period<C, T, 0>(S, xch, a, f, seed, s, d, sg)) {
       }
     }
-    while (fused_period<C, T, 0>(S, xch, a, f, seed, s, d, sg)) {
-    }
-  }
+  }  // work list
 }
 
 // ------------------------------------------------------------------------------------------
@@ -440,14 +456,33 @@ struct FusedLaunch {
     int64_t nwg = std::max<int64_t>(a.units / (4 * C::TL + 8),
                                     nruns > 1 ? (int64_t)a.ntx * a.nty * nruns : 1);
     nwg = std::max<int64_t>(1, std::min<int64_t>(slots, nwg));
+    a.ntiles = a.ntx * a.nty;
+    a.nchunk = 1;
     if (a.sched == 1) {
-      a.ntiles = a.ntx * a.nty;
-      int nch = (int)((slots + a.ntiles / 2) / a.ntiles);
+      // one unit per workgroup: never more units than resident slots (a second, partial
+      // round of workgroups would double the time)
+      int nch = (int)(slots / a.ntiles);
       nch = std::max(1, std::min(nch, a.nzv / (4 * C::TL + 4) > 0 ? a.nzv / (4 * C::TL + 4) : 1));
       a.nchunk = nch;
       const int64_t nunits = (int64_t)a.ntiles * nch;
       a.grpM = (int)((nunits + 7) / 8);
       nwg = 8LL * a.grpM;
+    } else if (a.sched == 2) {
+      // persistent grid (8 XCD groups of M workgroups); pick the chunk count minimising
+      // rounds x (planes per chunk + 2T pipeline fill)
+      const int64_t M = std::max<int64_t>(1, slots / 8);
+      int best = 1;
+      int64_t bcost = INT64_MAX;
+      const int maxch = std::max(1, a.nzv / (2 * C::TL + 2));
+      for (int nch = 1; nch <= maxch; ++nch) {
+        const int64_t per = ((int64_t)a.ntiles * nch + 7) / 8;
+        const int64_t rounds = (per + M - 1) / M;
+        const int64_t cost = rounds * ((a.nzv + nch - 1) / nch + 2 * C::TL);
+        if (cost < bcost) { bcost = cost; best = nch; }
+      }
+      a.nchunk = best;
+      a.grpM = (int)M;
+      nwg = 8 * M;
     }
     const FoldCoef<T> f = make_fold<T>(p);
     k_fused<C, T><<<(unsigned)nwg, 64 * C::WAVES, 0, st>>>(s, d, a, f, p.seed);

@@ -308,7 +308,8 @@ def fused_select(name: str = "") -> None:
 
 
 def fused_sched(sched: int) -> None:
-    """Pick the fused-kernel work schedule (0 even split, 1 XCD-grouped lockstep chunks)."""
+    """Pick the fused-kernel work schedule: 0 even split, 1 XCD-grouped lockstep chunks (one
+    per workgroup), 2 XCD-grouped chunks swept in rounds by a persistent grid."""
     lib = load("hip")
     lib.gs_fused_sched.argtypes = [c_int32]
     lib.gs_fused_sched.restype = c_int

@@ -167,7 +167,8 @@ print(max(np.abs(out[0][0] - out[1][0]).max(), np.abs(out[0][1] - out[1][1]).max
 
 @pytest.mark.parametrize("cfg,sched", [
     ("4x8:1", 0), ("8x4:1", 0), ("4x12:2", 0), ("8x4:1s", 0), ("8x4:4s", 0), ("4x8:1s", 0),
-    ("4x8:4s", 0), ("", 1), ("8x4:2", 1), ("4x8:4s", 1)])
+    ("4x8:4s", 0), ("", 1), ("8x4:2", 1), ("4x8:4s", 1), ("", 2), ("4x8:1", 2), ("4x8:2", 0),
+    ("4x12:3", 2)])
 @pytest.mark.parametrize("fuse", [2, 3])
 def test_fused_tuning_configs_agree(cfg, sched, fuse):
     """Every selectable fused-kernel configuration / schedule reproduces the single-step path."""
@@ -192,7 +193,7 @@ def test_autotuner_choice_is_valid_and_state_unchanged(prec):
     choice = g.fused_choice()
     assert set(choice) == {2, 3}
     for name, sched, ms in choice.values():
-        assert isinstance(name, str) and sched in (0, 1) and ms > 0
+        assert isinstance(name, str) and sched in (0, 1, 2) and ms > 0
     g.iterate(11)
     c.iterate(11)
     tol = 2e-5 if prec == "Float32" else 1e-12
