@@ -1,7 +1,9 @@
 # Native build for the MI355X Gray-Scott framework.
 #   make            -> grayscott_amd/_lib/libgs_core.so (CPU/OpenMP backend, BP4 I/O)
 #                      grayscott_amd/_lib/libgs_hip.so  (gfx950 kernels + RCCL transport)
-#   make tools      -> build/bin/* native CLI helpers
+#   make selftest   -> build/bin/core_selftest (threads-as-ranks runtime self-test)
+#   make asan/tsan  -> the same self-test under AddressSanitizer+UBSan / ThreadSanitizer (host
+#                      code only: GPU sanitizers are not available on the MI355X pool)
 ROCM     ?= /opt/rocm
 ARCH     ?= gfx950
 HIPCC    ?= $(ROCM)/bin/hipcc
@@ -26,7 +28,32 @@ $(OUT)/libgs_hip.so: $(HIP_SRC) $(HDRS)
 	@mkdir -p $(OUT)
 	$(HIPCC) $(HIPFLAGS) $(INC) -shared -o $@ $(HIP_SRC) -L$(ROCM)/lib -lrccl -Wl,-rpath,$(ROCM)/lib
 
+SELFTEST_TMP ?= /tmp
+SELFTEST_SRC := csrc/tools/core_selftest.cpp $(CORE_SRC)
+
+build/bin/core_selftest: $(SELFTEST_SRC) $(HDRS)
+	@mkdir -p build/bin
+	$(CXX) -O2 -g -std=c++17 -fopenmp $(INC) -o $@ $(SELFTEST_SRC) -lpthread
+
+build/asan/core_selftest: $(SELFTEST_SRC) $(HDRS)
+	@mkdir -p build/asan
+	$(CXX) -O1 -g -std=c++17 -fopenmp -fsanitize=address,undefined -fno-omit-frame-pointer \
+	  -fno-sanitize-recover=undefined $(INC) -o $@ $(SELFTEST_SRC) -lpthread
+
+# no -fopenmp: libgomp is not TSan-instrumented; the rank threads are what is checked
+build/tsan/core_selftest: $(SELFTEST_SRC) $(HDRS)
+	@mkdir -p build/tsan
+	$(CXX) -O1 -g -std=c++17 -Wno-unknown-pragmas -fsanitize=thread $(INC) -o $@ $(SELFTEST_SRC) -lpthread
+
+selftest: build/bin/core_selftest
+	build/bin/core_selftest $(SELFTEST_TMP)
+asan: build/asan/core_selftest
+	ASAN_OPTIONS=detect_leaks=1 build/asan/core_selftest $(SELFTEST_TMP)
+tsan: build/tsan/core_selftest
+	build/tsan/core_selftest $(SELFTEST_TMP)
+
 clean:
 	rm -f $(OUT)/*.so
+	rm -rf build
 
-.PHONY: all clean tools
+.PHONY: all clean selftest asan tsan

@@ -35,10 +35,13 @@ def default_fuse(backend: str, domain: CartDomain) -> int:
     if backend != "hip":
         return 1
     # The temporally blocked kernel cuts HBM traffic per step by T; a deeper halo also cuts
-    # the RCCL round trips.  Measured on MI355X (profiles/r1_tune_inproc.json): T=3 wins on
-    # 512^3 sub-domains, T=2 on <=320-cell ones (pipeline fill and tile rounding grow with T).
-    n = min(domain.proc_sizes)
-    return max(1, min(2 if n <= 320 else 3, n))
+    # the RCCL round trips.  Measured on MI355X (profiles/r1_tune_sched012.txt,
+    # profiles/r1_overlap_split_1gpu.json): T=3 wins once the x-y tile grid is large
+    # (512^2 planes, even for 64-plane z slabs); T=2 on <=320-cell x-y extents, where the
+    # 2T-cell tile halo costs more than the saved traffic.
+    nx, ny, nz = domain.proc_sizes
+    t = 2 if min(nx, ny) <= 320 else 3
+    return max(1, min(t, nx, ny, nz))
 
 
 class GrayScott:
