@@ -38,6 +38,8 @@ def main(argv=None) -> int:
     ap.add_argument("--backend", default="AMDGPU")
     ap.add_argument("--decomposition", default="auto", help="auto | balanced | z")
     ap.add_argument("--overlap", default="auto", help="auto | on | off")
+    ap.add_argument("--init", default="random", choices=["random", "seed"],
+                    help="random: u, v ~ U[0,1) (BASELINE.json); seed: the reference's seed cube")
     args = ap.parse_args(argv)
 
     import torch
@@ -64,6 +66,8 @@ def main(argv=None) -> int:
     dom = init_domain(args.L, ctx.world_size, ctx.rank, periodic=False, dims=dims)
     sim = GrayScott(settings, dom, ctx, use_fused=not args.no_fused_kernel)
     sim.init_fields()
+    if args.init == "random":
+        sim.randomize_fields(seed=2024)
 
     def sync():
         sim.synchronize()
@@ -99,13 +103,16 @@ def main(argv=None) -> int:
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "fp32" if settings.dtype_name == "float32" else "fp64",
-            "data": "synthetic (reference seed-cube init + Philox noise, examples/settings-files.toml physics)",
+            "data": ("synthetic: random-init u, v ~ U[0,1) on device" if args.init == "random"
+                     else "synthetic: reference seed-cube init") +
+                    " + in-kernel Philox noise, examples/settings-files.toml physics",
             "config": {
                 "model": "gray-scott-3d-7pt",
                 "L": args.L,
                 "global_batch": 1,
                 "seq_len": args.L,
-                "parallelism": f"spatial-3d {dims}",
+                "parallelism": (f"spatial-z-slabs {dims} (in-place RCCL plane halos, overlapped)"
+                                if sim.overlapped else f"spatial-3d {dims}"),
                 "dims": dom.dims,
                 "local_extent": dom.proc_sizes,
                 "fuse_steps": sim.fuse,

@@ -205,6 +205,21 @@ class GrayScott:
         self.engine.insert(tu.data_ptr(), tv.data_ptr())
         self.engine.sync()
 
+    def randomize_fields(self, seed: int = 0, lo: float = 0.0, hi: float = 1.0) -> None:
+        """Random-init the interior: u, v ~ U[lo, hi) drawn on the field device (benchmarks on
+        "random-init u/v fields", BASELINE.json).  Per-rank streams keyed by ``seed`` and rank."""
+        tdt = _TORCH_DTYPES[self.dtype]
+        gen = torch.Generator(device=self.device).manual_seed(int(seed) * 1000003 + self.domain.rank)
+        u = torch.rand(self.local_shape, generator=gen, device=self.device, dtype=tdt)
+        v = torch.rand(self.local_shape, generator=gen, device=self.device, dtype=tdt)
+        if (lo, hi) != (0.0, 1.0):
+            u.mul_(hi - lo).add_(lo)
+            v.mul_(hi - lo).add_(lo)
+        if self.backend == "hip":
+            torch.cuda.synchronize(self.device)
+        self.engine.insert(u.data_ptr(), v.data_ptr())
+        self.engine.sync()
+
     def full_state(self, which: Optional[int] = None) -> torch.Tensor:
         """View of a raw state buffer as (pz, py, px, 2) including ghosts and padding."""
         g = self.geom
