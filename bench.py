@@ -24,6 +24,38 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 
+def distributed_selfcheck(ctx, backend, dims, fuse, transport, overlap, L=64, steps=9):
+    """Before timing a multi-rank run, check the exact data path it will use (decomposition,
+    transport, in-place halos, overlap, fuse depth) on a small grid against the numpy/torch
+    golden model computed by every rank.  Returns (ok, max_abs_err, transport)."""
+    import numpy as np
+
+    from grayscott_amd.models.grayscott import GrayScott
+    from grayscott_amd.ops import reference as ref
+    from grayscott_amd.parallel.decomp import init_domain
+    from grayscott_amd.utils.config import Settings
+
+    L = max(L, 8 * max(dims))
+    s = Settings(L=L, precision="Float32", F=0.02, k=0.048, dt=1.0, Du=0.2, Dv=0.1, noise=0.1,
+                 backend="AMDGPU" if backend == "hip" else "CPU", seed=77, transport=transport,
+                 overlap=overlap)
+    dom = init_domain(L, ctx.world_size, ctx.rank, periodic=False, dims=dims)
+    sim = GrayScott(s, dom, ctx, fuse=min(fuse, min(dom.proc_sizes)))
+    try:
+        sim.init_fields()
+        sim.iterate(steps)
+        u, v = sim.get_fields()
+        used = sim.transport
+    finally:
+        sim.close()
+    ru, rv = ref.run(L, steps, noise_amp=0.1, seed=77, dtype=np.float32, backend="torch")
+    (ox, oy, oz), (nx, ny, nz) = dom.proc_offsets, dom.proc_sizes
+    blk = (slice(oz, oz + nz), slice(oy, oy + ny), slice(ox, ox + nx))
+    err = float(max(np.abs(u - ru[blk]).max(), np.abs(v - rv[blk]).max()))
+    err = ctx.allreduce(err, "max")
+    return err < 1e-4, err, used
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
@@ -64,6 +96,25 @@ def main(argv=None) -> int:
     ctx = init_from_env("hip" if backend == "hip" else "cpu")
     dims = choose_dims(args.L, ctx.world_size, args.decomposition, backend)
     dom = init_domain(args.L, ctx.world_size, ctx.rank, periodic=False, dims=dims)
+    selfcheck = None
+    if ctx.world_size > 1:
+        # verify the multi-rank data path first; fall back to safer paths if it is wrong
+        from grayscott_amd.models.grayscott import default_fuse
+        fuse0 = args.fuse if args.fuse > 0 else default_fuse(backend, dom)
+        attempts = [(args.transport, args.overlap, None), (args.transport, "off", "0"),
+                    ("torch", "off", "0")]
+        for tr, ov, inplace in attempts:
+            if inplace is not None:
+                os.environ["GS_INPLACE_HALO"] = inplace
+            ok, err, used = distributed_selfcheck(ctx, backend, dims, fuse0, tr, ov)
+            selfcheck = {"ok": ok, "max_abs_err": err, "transport": used, "overlap": ov,
+                         "inplace_halos": inplace is None}
+            if ok:
+                settings.transport, settings.overlap = tr, ov
+                break
+            if ctx.rank == 0:
+                print(f"bench.py: multi-rank self-check FAILED ({selfcheck}); trying a safer "
+                      f"data path", file=sys.stderr)
     sim = GrayScott(settings, dom, ctx, use_fused=not args.no_fused_kernel)
     sim.init_fields()
     if args.init == "random":
@@ -123,6 +174,7 @@ def main(argv=None) -> int:
                 "noise": args.noise,
                 "backend": backend,
             },
+            "selfcheck": selfcheck,
             "check": {"mean_u": stats["mean_u"], "mean_v": stats["mean_v"],
                       "finite": all(map(lambda x: x == x, stats.values()))},
         }

@@ -506,7 +506,8 @@ inline const char* const* fused_cfg_names(int* n) {
                                 "8x4:3",  "4x6:2",  "4x12:2", "4x4:2",   "4x12:3",  "8x4:1s",
                                 "8x4:4s", "4x8:1s", "4x8:4s", "abl1",   "abl2",    "abl3",
                                 "4x8:1w4", "4x16:1", "4x16:2w4", "4x8:2w3", "abl4", "4x8:1abl4",
-                                "4x12:2s", "4x12:1s", "4x6:2s", "4x12:1"};
+                                "4x12:2s", "4x12:1s", "4x6:2s", "4x12:1", "4x12:1s-abl1",
+                                "4x12:1s-abl2"};
   *n = (int)(sizeof(names) / sizeof(names[0]));
   return names;
 }
@@ -580,6 +581,8 @@ void run_fused_cfg(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, c
       case 31: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, 1, true>, T>::run(s, d, a, p, st); return;
       case 32: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, 1, true>, T>::run(s, d, a, p, st); return;
       case 33: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ>, T>::run(s, d, a, p, st); return;
+      case 34: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, 1, true, 1>, T>::run(s, d, a, p, st); return;
+      case 35: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, 1, true, 2>, T>::run(s, d, a, p, st); return;
       default: break;
     }
   }
