@@ -162,7 +162,7 @@ def main(argv=None) -> int:
                 "L": args.L,
                 "global_batch": 1,
                 "seq_len": args.L,
-                "parallelism": (f"spatial-z-slabs {dims} (in-place RCCL plane halos, overlapped)"
+                "parallelism": (f"spatial-z-slabs {dims} ({sim.transport} plane halos, overlapped)"
                                 if sim.overlapped else f"spatial-3d {dims}"),
                 "dims": dom.dims,
                 "local_extent": dom.proc_sizes,

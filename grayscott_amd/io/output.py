@@ -95,6 +95,8 @@ class SimulationOutput:
         self.w.define_variable("U", dtype, (Lz, Ly, Lx), (oz, oy, ox), (nz, ny, nx))
         self.w.define_variable("V", dtype, (Lz, Ly, Lx), (oz, oy, ox), (nz, ny, nx))
         self.steps_written = 0
+        self.async_io = bool(getattr(settings, "async_output", False))
+        self._pending = None
 
     def define_attribute(self, name, value) -> None:
         if self.ctx.rank == 0:
@@ -112,10 +114,64 @@ class SimulationOutput:
         self.steps_written += 1
 
     def write_step(self, step: int, sim) -> None:
-        """IO.jl:82-96."""
-        u, v = sim.get_fields()
-        self.write_fields(step, u, v)
+        """IO.jl:82-96.  With ``async_output`` (default) the step is written behind the
+        simulation: device snapshot + D2H on an I/O stream, data write on a host thread; the
+        collective metadata gather of step n happens on the main thread at step n+1 (or at
+        close), so no collective ever runs off the main thread."""
+        if not self.async_io:
+            u, v = sim.get_fields()
+            self.write_fields(step, u, v)
+            return
+        self.flush()
+        u, v, wait = sim.snapshot_fields()
+
+        def job():
+            wait()
+            self.w.begin_step()
+            self.w.put("step", np.int32(step))
+            self.w.put("U", u)
+            self.w.put("V", v)
+            return self.w.end_step()
+
+        self._pending = _Job(job)
+
+    def flush(self) -> None:
+        """Finish the in-flight asynchronous step: wait for its data write, gather the
+        per-rank metadata blobs and let rank 0 append them to the index."""
+        job, self._pending = self._pending, None
+        if job is None:
+            return
+        blob = job.result()
+        blobs = self.ctx.gather_object(blob, dst=0)
+        if self.ctx.rank == 0:
+            self.w.write_metadata(blobs)
+        self.steps_written += 1
 
     def close(self) -> None:
+        self.flush()
         self.w.close()
         self.ctx.barrier()
+
+
+class _Job:
+    """A function running on a host thread (ctypes releases the GIL during the BP4 writes)."""
+
+    def __init__(self, fn):
+        import threading
+        self._out = None
+        self._err = None
+
+        def run():
+            try:
+                self._out = fn()
+            except BaseException as ex:  # re-raised on the main thread
+                self._err = ex
+
+        self._t = threading.Thread(target=run, name="gs-async-output", daemon=True)
+        self._t.start()
+
+    def result(self):
+        self._t.join()
+        if self._err is not None:
+            raise self._err
+        return self._out

@@ -195,6 +195,32 @@ class GrayScott:
             return u.cpu().numpy(), v.cpu().numpy()
         return u.numpy(), v.numpy()
 
+    def snapshot_fields(self):
+        """Asynchronous ghost-stripped copy of u, v for output: the compaction
+        kernel runs in stream order on the compute stream, the D2H copy into pinned host
+        buffers on a separate I/O stream, so stepping continues while the copy (and the file
+        write that follows it) is in flight.  Returns ``(u, v, wait)``: numpy views of the host
+        buffers and a callable that blocks until they are filled.  The buffers are reused by
+        the next call, so consume them (``wait`` + write) before snapshotting again."""
+        if self.backend != "hip":
+            u, v = self.get_fields()
+            return u, v, lambda: None
+        tdt = _TORCH_DTYPES[self.dtype]
+        if getattr(self, "_snap", None) is None:
+            dev = [torch.empty(self.local_shape, dtype=tdt, device=self.device) for _ in range(2)]
+            host = [torch.empty(self.local_shape, dtype=tdt, pin_memory=True) for _ in range(2)]
+            self._snap = (dev, host, torch.cuda.Stream(self.device), torch.cuda.Event(),
+                          torch.cuda.Event())
+        dev, host, io_stream, ready, done = self._snap
+        self.engine.extract(dev[0].data_ptr(), dev[1].data_ptr())
+        ready.record(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(io_stream):
+            io_stream.wait_event(ready)
+            host[0].copy_(dev[0], non_blocking=True)
+            host[1].copy_(dev[1], non_blocking=True)
+            done.record(io_stream)
+        return host[0].numpy(), host[1].numpy(), done.synchronize
+
     def set_fields(self, u, v) -> None:
         """Overwrite the interior of the current state (restart)."""
         tdt = _TORCH_DTYPES[self.dtype]

@@ -15,7 +15,8 @@ Extension keys (not in the reference, all optional, documented in README):
   halo exchange / temporal blocking depth, 0 = auto), ``transport`` ("auto"|"rccl"|"torch"),
   ``output_engine`` ("bp4"), ``perf_log`` (path of a JSON-lines perf log), ``diagnostics`` (bool),
   ``decomposition`` ("auto"|"balanced"|"z": process grid, see parallel/decomp.choose_dims),
-  ``overlap`` ("auto"|"on"|"off": overlap the halo exchange with the inner-plane update).
+  ``overlap`` ("auto"|"on"|"off": overlap the halo exchange with the inner-plane update),
+  ``async_output`` (bool, default true: output steps are written behind the simulation).
 """
 from __future__ import annotations
 
@@ -76,6 +77,7 @@ class Settings:
     diagnostics: bool = False
     decomposition: str = "auto"
     overlap: str = "auto"
+    async_output: bool = True
 
     # -------------------------------------------------------------------------------------
     @property
@@ -120,6 +122,7 @@ EXTENSION_KEYS: Dict[str, str] = {
     "diagnostics": _BOOL,
     "decomposition": _STRING,
     "overlap": _STRING,
+    "async_output": _BOOL,
 }
 
 # Keys present in reference configs but commented out of the struct (Structs.jl:20-22):

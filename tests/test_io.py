@@ -169,3 +169,24 @@ def test_simulation_output_schema(tmp_path):
 
 def test_vtk_schema_extent():
     assert 'Extent="0 64 0 64 0 64"' in vtk_schema(64)
+
+
+def test_async_output_matches_sync(tmp_path):
+    """async_output (snapshot + background data write, metadata gathered one step later) writes
+    the same steps and bytes as the synchronous path."""
+    from grayscott_amd import driver
+
+    out = {}
+    for mode in (False, True):
+        s = Settings(L=20, steps=12, plotgap=3, noise=0.1, F=0.02, k=0.048, dt=1.0, Du=0.2,
+                     Dv=0.1, precision="Float32", backend="CPU", async_output=mode,
+                     output=str(tmp_path / f"gs_{mode}.bp"))
+        driver.run(s, out=open(os.devnull, "w"))
+        with BP4Reader(s.output) as r:
+            out[mode] = [(int(r.read("step", i)), r.read("U", i), r.read("V", i))
+                         for i in range(r.steps)]
+    assert len(out[True]) == len(out[False]) == 4
+    for (sa, ua, va), (sb, ub, vb) in zip(out[False], out[True]):
+        assert sa == sb
+        np.testing.assert_array_equal(ua, ub)
+        np.testing.assert_array_equal(va, vb)
