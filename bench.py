@@ -100,7 +100,7 @@ def main(argv=None) -> int:
     if ctx.world_size > 1:
         # verify the multi-rank data path first; fall back to safer paths if it is wrong
         from grayscott_amd.models.grayscott import default_fuse
-        fuse0 = args.fuse if args.fuse > 0 else default_fuse(backend, dom)
+        fuse0 = args.fuse if args.fuse > 0 else default_fuse(backend, dom, settings.dtype_name)
         attempts = [(args.transport, args.overlap, None), (args.transport, "off", "0"),
                     ("torch", "off", "0")]
         for tr, ov, inplace in attempts:

@@ -175,7 +175,7 @@ class HipBackend final : public gs::Backend {
     std::vector<int> cfgs;
     if (!variants) cfgs = {0};
     else if (sizeof(T) == 4) cfgs = {0, 1, 2, 3, 5, 8, 12, 16, 17, 19, 20, 30, 31, 33};
-    else cfgs = {0, 1, 13, 15};
+    else cfgs = {0, 1, 13, 15, 19, 32, 33};
     for (int c : cfgs)
       for (int sc = 0; sc <= 2; ++sc) cands.push_back({c, sc});
     // interleaved rounds (box-to-box and launch-to-launch jitter is several %): first launch

@@ -543,6 +543,9 @@ void run_fused_cfg(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, c
       case 1: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ>, T>::run(s, d, a, p, st); return;
       case 13: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
       case 15: FusedLaunch<FCfg<T, TL, 4, 4, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
+      case 19: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, 1, true>, T>::run(s, d, a, p, st); return;
+      case 32: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, 1, true>, T>::run(s, d, a, p, st); return;
+      case 33: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ>, T>::run(s, d, a, p, st); return;
       default: break;
     }
   }

@@ -30,10 +30,15 @@ _TORCH_DTYPES = {"float32": torch.float32, "float64": torch.float64}
 _NP_DTYPES = {"float32": np.float32, "float64": np.float64}
 
 
-def default_fuse(backend: str, domain: CartDomain) -> int:
+def default_fuse(backend: str, domain: CartDomain, dtype: str = "float32") -> int:
     """Steps fused per halo exchange when ``fuse_steps = 0`` (auto)."""
     if backend != "hip":
         return 1
+    if dtype == "float64":
+        # fp64 doubles the per-cell register footprint: T=3 tiles lose occupancy, T=2 with the
+        # XCD-grouped schedule is fastest (L=512: 263k vs 224k MLUPS, profiles/r1_tune_f64.txt)
+        nx, ny, nz = domain.proc_sizes
+        return max(1, min(2, nx, ny, nz))
     # The temporally blocked kernel cuts HBM traffic per step by T; a deeper halo also cuts
     # the RCCL round trips.  Measured on MI355X (profiles/r1_tune_sched012.txt,
     # profiles/r1_overlap_split_1gpu.json): T=3 wins once the x-y tile grid is large
@@ -62,7 +67,8 @@ class GrayScott:
         else:
             self.device = torch.device("cpu")
         if fuse is None or fuse <= 0:
-            fuse = settings.fuse_steps if settings.fuse_steps > 0 else default_fuse(self.backend, domain)
+            fuse = (settings.fuse_steps if settings.fuse_steps > 0
+                    else default_fuse(self.backend, domain, parse_precision(settings.precision)))
         fuse = int(max(1, min(fuse, min(domain.proc_sizes))))
         self.fuse = fuse
         self.H = fuse
