@@ -138,8 +138,9 @@ class HipBackend final : public gs::Backend {
   // in direction, receives descend), which keeps two messages to one peer matched.
   bool native_exchange_inplace(int b, const gs::HaloPlan& p) override {
     if (!comm_ || !p.zplanes || inplace_off_) return false;
-    for (int i = 0; i < p.nrecv; ++i)
-      if (p.recv[i].peer == rank_) return false;
+    if (!loopback_)
+      for (int i = 0; i < p.nrecv; ++i)
+        if (p.recv[i].peer == rank_) return false;
     NCCL_CHECK(ncclGroupStart());
     for (int i = 0; i < p.nsend; ++i) {
       const gs::HaloMsg& m = p.send[i];
@@ -238,19 +239,21 @@ class HipBackend final : public gs::Backend {
     NCCL_CHECK(ncclGroupStart());
     for (int i = 0; i < p.nsend; ++i) {
       const gs::HaloMsg& m = p.send[i];
-      if (m.peer == rank_) continue;
+      if (m.peer == rank_ && !loopback_) continue;
       NCCL_CHECK(ncclSend(send_ + m.offset, (size_t)gs::box_cells(m.box) * sizeof(V2), ncclUint8,
                           m.peer, comm_, xs_));
     }
     for (int i = 0; i < p.nrecv; ++i) {
       const gs::HaloMsg& m = p.recv[i];
-      if (m.peer == rank_) continue;
+      if (m.peer == rank_ && !loopback_) continue;
       NCCL_CHECK(ncclRecv(recv_ + m.offset, (size_t)gs::box_cells(m.box) * sizeof(V2), ncclUint8,
                           m.peer, comm_, xs_));
     }
     NCCL_CHECK(ncclGroupEnd());
     return true;
   }
+
+  void set_loopback(bool on) override { loopback_ = on; }
 
   void host_sync() override { HIP_CHECK(hipStreamSynchronize(xs_)); }
 
@@ -338,6 +341,7 @@ class HipBackend final : public gs::Backend {
   int dev_ = 0;
   ncclComm_t comm_ = nullptr;
   int rank_ = 0;
+  bool loopback_ = false;
   bool tuned_[4] = {false, false, false, false};
   int cfg_[4] = {-1, -1, -1, -1};
   int sched_[4] = {-1, -1, -1, -1};

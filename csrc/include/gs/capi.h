@@ -22,6 +22,7 @@ const char* gs_last_error(void);
 int gs_init_fields(gs_engine* e);
 int gs_prepare(gs_engine* e);  // autotune the fused kernel (state unchanged)
 int gs_set_overlap(gs_engine* e, int32_t mode);  // -1 auto, 0 off, 1 on
+int gs_set_loopback(gs_engine* e, int32_t on);  // self messages via the device transport
 int gs_overlapped(gs_engine* e, int32_t k);      // 1 if a k-step pass overlaps its exchange
 int gs_plan_zplanes(gs_engine* e);               // 1 if halos are whole contiguous z planes
 int gs_fused_runs_raw(gs_engine* e, int32_t k, int32_t zlo0, int32_t zlen0, int32_t zlo1,

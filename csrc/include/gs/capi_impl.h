@@ -66,6 +66,7 @@ void gs_destroy(gs_engine* e) {
 int gs_init_fields(gs_engine* e) { GS_TRY(e->eng->init_fields()) }
 int gs_prepare(gs_engine* e) { GS_TRY(e->eng->prepare()) }
 int gs_set_overlap(gs_engine* e, int32_t mode) { GS_TRY(e->eng->set_overlap(mode)) }
+int gs_set_loopback(gs_engine* e, int32_t on) { GS_TRY(e->eng->set_loopback(on != 0)) }
 int gs_overlapped(gs_engine* e, int32_t k) { return e->eng->overlapped(k) ? 1 : 0; }
 int gs_plan_zplanes(gs_engine* e) { return e->eng->plan().zplanes; }
 // Timing primitive: one fused k-step update of the given z-runs from the current buffer into

@@ -66,6 +66,8 @@ class Backend {
   virtual void self_copy(int64_t src_off, int64_t dst_off, int64_t n) = 0;
   // native transport (RCCL); returns false if not configured
   virtual bool native_exchange(const HaloPlan& p) { (void)p; return false; }
+  // loopback: messages to this rank also go through the native transport (tests)
+  virtual void set_loopback(bool on) { (void)on; }
   virtual void host_sync() {}
   // wait for all queued device work; a backend with a device transport turns a hang or an
   // asynchronous transport error into an exception after `timeout_s` seconds (watchdog)
@@ -112,6 +114,16 @@ class Engine {
   // comm/compute overlap: -1 auto (on when the plan is zplanes and a comm stream exists),
   // 0 off, 1 on where possible
   void set_overlap(int mode) { overlap_ = mode; }
+  // Loopback (tests): periodic wraps onto this rank travel through the device transport
+  // (RCCL send/recv to self) instead of self copies, so a single GPU exercises the whole
+  // multi-rank data path: packed and in-place messages, the comm stream and the overlap.
+  void set_loopback(bool on) {
+    loopback_ = on;
+    be_->set_loopback(on);
+    has_remote_ = false;
+    for (int d = 0; d < 27; ++d)
+      if (d != 13 && cfg_.nbr[d] >= 0 && (on || cfg_.nbr[d] != cfg_.rank)) has_remote_ = true;
+  }
   // whether a pass of k steps runs with the halo exchange overlapped with the inner planes
   bool overlapped(int k) const {
     return overlap_ != 0 && cfg_.use_fused && k > 1 && has_remote_ && plan_.zplanes &&
@@ -165,7 +177,7 @@ class Engine {
     bool remote = false;
     for (int i = 0; i < plan_.nrecv; ++i) {
       const HaloMsg& r = plan_.recv[i];
-      if (r.peer == cfg_.rank) {
+      if (r.peer == cfg_.rank && !loopback_) {
         const int sd = 26 - r.dir;  // my send towards -d lands in my ghost d
         for (int j = 0; j < plan_.nsend; ++j)
           if (plan_.send[j].dir == sd && plan_.send[j].peer == cfg_.rank)
@@ -283,6 +295,7 @@ class Engine {
   bool has_nbr_ = false;
   bool has_remote_ = false;
   int overlap_ = -1;
+  bool loopback_ = false;
   enum { kNone, kUnpack, kCallback };
   int xpending_ = kNone;
   int cur_ = 0;

@@ -54,7 +54,7 @@ class GrayScott:
 
     def __init__(self, settings: Settings, domain: CartDomain, ctx: Optional[DistContext] = None,
                  fuse: Optional[int] = None, transport: Optional[str] = None,
-                 use_fused: bool = True):
+                 use_fused: bool = True, loopback: bool = False):
         self.settings = settings
         self.domain = domain
         self.ctx = ctx or DistContext()
@@ -98,7 +98,14 @@ class GrayScott:
             raise ValueError(f"overlap must be auto | on | off, not {ov!r}")
         self.engine.set_overlap(-1 if ov == "auto" else (1 if ov in ("on", "true", "1") else 0))
         self.transport = "none"
-        if domain.has_neighbors and any(r != domain.rank for i, r in enumerate(domain.nbr27)
+        if loopback:
+            # single-GPU test mode: the periodic wraps onto this rank go through RCCL
+            # send/recv-to-self, exercising the multi-rank data path (engine.h set_loopback)
+            if not domain.has_neighbors:
+                raise ValueError("loopback needs a domain with (periodic) neighbours")
+            self.engine.set_loopback(True)
+            self._setup_transport(transport or "rccl")
+        elif domain.has_neighbors and any(r != domain.rank for i, r in enumerate(domain.nbr27)
                                         if i != 13 and r >= 0):
             self._setup_transport(transport or settings.transport)
 

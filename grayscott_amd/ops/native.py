@@ -67,6 +67,8 @@ def _declare(lib) -> None:
     lib.gs_plan_zplanes.restype = c_int
     lib.gs_set_overlap.argtypes = [c_void_p, c_int32]
     lib.gs_set_overlap.restype = c_int
+    lib.gs_set_loopback.argtypes = [c_void_p, c_int32]
+    lib.gs_set_loopback.restype = c_int
     lib.gs_overlapped.argtypes = [c_void_p, c_int32]
     lib.gs_overlapped.restype = c_int
     lib.gs_get_step.argtypes = [c_void_p]
@@ -216,6 +218,10 @@ class Engine:
     def set_overlap(self, mode: int):
         """-1 auto, 0 off, 1 on (where the plan and backend allow it)."""
         self._chk(self.lib.gs_set_overlap(self.h, int(mode)), "set_overlap")
+
+    def set_loopback(self, on: bool):
+        """Send messages to this rank through the device transport too (single-GPU tests)."""
+        self._chk(self.lib.gs_set_loopback(self.h, 1 if on else 0), "set_loopback")
 
     def overlapped(self, k: int) -> bool:
         return bool(self.lib.gs_overlapped(self.h, int(k)))
