@@ -111,6 +111,7 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 //  * Rounds 1-2 still see wave-uniform counter words (step, and its products), which the
 //    compiler folds on the SALU; from round 3 on every word varies per lane and each output
 //    word's two xors become one v_bitop3.
+template <bool kOpaqueStep = true>
 __device__ __forceinline__ gs::U4 noise_block_dev(int64_t gx, int64_t gy4, int64_t gz, int64_t Lx,
                                                   int64_t Ly, uint64_t step, uint64_t seed) {
   uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
@@ -119,6 +120,10 @@ __device__ __forceinline__ gs::U4 noise_block_dev(int64_t gx, int64_t gy4, int64
   const uint64_t q = (uint64_t)gx + (uint64_t)Lx * ((uint64_t)gy4 + Ly4 * (uint64_t)gz);
   uint32_t c0 = (uint32_t)q, c1 = (uint32_t)(q >> 32), c2 = (uint32_t)step,
            c3 = (uint32_t)(step >> 32);
+  // the step words are wave-uniform and loop-invariant per time level: without this the
+  // compiler hoists their round-1/2 products out of the plane loop and spills them to VGPR
+  // lanes (a v_readlane per use); recomputed they are a few SALU ops
+  if constexpr (kOpaqueStep) asm volatile("" : "+s"(c2), "+s"(c3));
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
     if (r < 2) {
@@ -153,7 +158,8 @@ struct FCfg {
   static constexpr bool PERIODIC = PERIODIC_, NOISE = NOISE_, SKEW = SKEW_;
   // ablation (timing experiments only, results are WRONG): bit0 = no workgroup barriers,
   // bit1 = every level-0 load reads plane 0 (L2-resident); bit2 (results exact) = hoistable
-  // Philox key schedule (the pre-noise_block_dev code generation)
+  // Philox key schedule (the pre-noise_block_dev code generation); bit3 (results exact) =
+  // hoistable step words in the Philox counter (before the opaque-step change)
   static constexpr int ABL = ABL_;
   static constexpr int R = PF + 2;                    // level-0 ring slots
   static constexpr int NS = SKEW ? 3 : 2;             // level-l output ring / xch buffers
@@ -244,7 +250,7 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
       if constexpr (C::NOISE) {
         const int64_t gyq = gwrap<C>(sg.gy0 + 4 * m, g.Ly);
         if constexpr (C::ABL & 4) blk = gs::noise_block(sg.gx, gyq >> 2, gz, g.Lx, g.Ly, tstep, seed);
-        else blk = noise_block_dev(sg.gx, gyq >> 2, gz, g.Lx, g.Ly, tstep, seed);
+        else blk = noise_block_dev<!(C::ABL & 8)>(sg.gx, gyq >> 2, gz, g.Lx, g.Ly, tstep, seed);
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -259,6 +265,8 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
         const T uvv = cu * cv * cv;
         T ru = f.ac;
         if constexpr (C::NOISE) {
+          // (folding the 2^-31 of uniform_pm1 into ar saves a v_mul but costs an SGPR; the
+          // extra spill reloads made it 2 % slower: profiles/r1_ab_noise_fold.txt)
           const uint32_t w = k == 0 ? blk.x : (k == 1 ? blk.y : (k == 2 ? blk.z : blk.w));
           ru = fma(f.ar, gs::uniform_pm1<T>(w), ru);
         }
@@ -507,7 +515,7 @@ inline const char* const* fused_cfg_names(int* n) {
                                 "8x4:4s", "4x8:1s", "4x8:4s", "abl1",   "abl2",    "abl3",
                                 "4x8:1w4", "4x16:1", "4x16:2w4", "4x8:2w3", "abl4", "4x8:1abl4",
                                 "4x12:2s", "4x12:1s", "4x6:2s", "4x12:1", "4x12:1s-abl1",
-                                "4x12:1s-abl2"};
+                                "4x12:1s-abl2", "4x12:1s-abl8", "4x12:2s-abl8"};
   *n = (int)(sizeof(names) / sizeof(names[0]));
   return names;
 }
@@ -586,6 +594,8 @@ void run_fused_cfg(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, c
       case 33: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ>, T>::run(s, d, a, p, st); return;
       case 34: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, 1, true, 1>, T>::run(s, d, a, p, st); return;
       case 35: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, 1, true, 2>, T>::run(s, d, a, p, st); return;
+      case 36: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, 1, true, 8>, T>::run(s, d, a, p, st); return;
+      case 37: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, 1, true, 8>, T>::run(s, d, a, p, st); return;
       default: break;
     }
   }
