@@ -3,10 +3,12 @@
 
 BASELINE.json metric: "MLUPS (cell-updates/sec, whole node) at L=512 fp32, 1/2/4/8 MI355X".
 Config: the reference example physics (examples/settings-files.toml: F=0.02, k=0.048, dt=1,
-Du=0.2, Dv=0.1, noise=0.1) on an L^3 = 512^3 fp32 grid, decomposed over the N GPUs with the
-reference's Dims_create factorisation (2 -> 2x1x1, 4 -> 2x2x1, 8 -> 2x2x2).  The global grid is
-fixed as N grows (strong scaling).  Every timed step is a full update of all L^3 cells
-including the Philox noise and the RCCL halo exchange.
+Du=0.2, Dv=0.1, noise=0.1) on an L^3 = 512^3 fp32 grid, decomposed over the N GPUs (z slabs
+1x1xN or the reference's Dims_create grid 2x2x2, whichever runs faster here).  The global grid
+is fixed as N grows (strong scaling).  Every timed step is a full update of all L^3 cells
+including the Philox noise and the RCCL halo exchange.  With N > 1 the multi-rank data path
+(z slabs or the balanced grid, fuse depth, transport) is verified against the golden model and
+then picked by a short timed run of each candidate before the timed region.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--L 512] [--precision Float32]
   torchrun --nproc-per-node N bench.py --gpus N ...
@@ -22,38 +24,6 @@ import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-
-
-def distributed_selfcheck(ctx, backend, dims, fuse, transport, overlap, L=64, steps=9):
-    """Before timing a multi-rank run, check the exact data path it will use (decomposition,
-    transport, in-place halos, overlap, fuse depth) on a small grid against the numpy/torch
-    golden model computed by every rank.  Returns (ok, max_abs_err, transport)."""
-    import numpy as np
-
-    from grayscott_amd.models.grayscott import GrayScott
-    from grayscott_amd.ops import reference as ref
-    from grayscott_amd.parallel.decomp import init_domain
-    from grayscott_amd.utils.config import Settings
-
-    L = max(L, 8 * max(dims))
-    s = Settings(L=L, precision="Float32", F=0.02, k=0.048, dt=1.0, Du=0.2, Dv=0.1, noise=0.1,
-                 backend="AMDGPU" if backend == "hip" else "CPU", seed=77, transport=transport,
-                 overlap=overlap)
-    dom = init_domain(L, ctx.world_size, ctx.rank, periodic=False, dims=dims)
-    sim = GrayScott(s, dom, ctx, fuse=min(fuse, min(dom.proc_sizes)))
-    try:
-        sim.init_fields()
-        sim.iterate(steps)
-        u, v = sim.get_fields()
-        used = sim.transport
-    finally:
-        sim.close()
-    ru, rv = ref.run(L, steps, noise_amp=0.1, seed=77, dtype=np.float32, backend="torch")
-    (ox, oy, oz), (nx, ny, nz) = dom.proc_offsets, dom.proc_sizes
-    blk = (slice(oz, oz + nz), slice(oy, oy + ny), slice(ox, ox + nx))
-    err = float(max(np.abs(u - ru[blk]).max(), np.abs(v - rv[blk]).max()))
-    err = ctx.allreduce(err, "max")
-    return err < 1e-4, err, used
 
 
 def main(argv=None) -> int:
@@ -95,26 +65,23 @@ def main(argv=None) -> int:
     backend, _ = load_backend_and_lang(settings)
     ctx = init_from_env("hip" if backend == "hip" else "cpu")
     dims = choose_dims(args.L, ctx.world_size, args.decomposition, backend)
-    dom = init_domain(args.L, ctx.world_size, ctx.rank, periodic=False, dims=dims)
-    selfcheck = None
+    tuning = None
     if ctx.world_size > 1:
-        # verify the multi-rank data path first; fall back to safer paths if it is wrong
-        from grayscott_amd.models.grayscott import default_fuse
-        fuse0 = args.fuse if args.fuse > 0 else default_fuse(backend, dom, settings.dtype_name)
-        attempts = [(args.transport, args.overlap, None), (args.transport, "off", "0"),
-                    ("torch", "off", "0")]
-        for tr, ov, inplace in attempts:
-            if inplace is not None:
-                os.environ["GS_INPLACE_HALO"] = inplace
-            ok, err, used = distributed_selfcheck(ctx, backend, dims, fuse0, tr, ov)
-            selfcheck = {"ok": ok, "max_abs_err": err, "transport": used, "overlap": ov,
-                         "inplace_halos": inplace is None}
-            if ok:
-                settings.transport, settings.overlap = tr, ov
-                break
-            if ctx.rank == 0:
-                print(f"bench.py: multi-rank self-check FAILED ({selfcheck}); trying a safer "
-                      f"data path", file=sys.stderr)
+        # Verify every candidate multi-rank data path against the golden model, then time a
+        # short run of each on this problem and keep the fastest (parallel/autotune.py): the
+        # z-slab vs balanced trade-off depends on this node's xGMI / RCCL rates.
+        from grayscott_amd.parallel.autotune import tune_data_path
+        cands = None
+        if args.decomposition != "auto" or args.fuse > 0:
+            cands = [(dims, args.fuse)]
+        log = (lambda m: print(f"bench.py: {m}", file=sys.stderr, flush=True))
+        tuning = tune_data_path(settings, ctx, args.L, backend, cands=cands, log=log)
+        dims = tuning["dims"]
+        settings.fuse_steps = tuning["fuse"]
+        settings.transport, settings.overlap = tuning["transport"], tuning["overlap"]
+        if not tuning["inplace_halos"]:
+            os.environ["GS_INPLACE_HALO"] = "0"
+    dom = init_domain(args.L, ctx.world_size, ctx.rank, periodic=False, dims=dims)
     sim = GrayScott(settings, dom, ctx, use_fused=not args.no_fused_kernel)
     sim.init_fields()
     if args.init == "random":
@@ -174,7 +141,7 @@ def main(argv=None) -> int:
                 "noise": args.noise,
                 "backend": backend,
             },
-            "selfcheck": selfcheck,
+            "data_path_tuning": tuning and tuning["table"],
             "check": {"mean_u": stats["mean_u"], "mean_v": stats["mean_v"],
                       "finite": all(map(lambda x: x == x, stats.values()))},
         }

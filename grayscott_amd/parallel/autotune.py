@@ -1,0 +1,178 @@
+"""Multi-rank data-path selection: verify, then time, the candidate decompositions.
+
+The reference has one data path (MPI_Dims_create grid + blocking host Sendrecv,
+communication.jl:59-199).  Here several exist and the best one depends on the xGMI link rate
+and RCCL's point-to-point latency, which differ between machines and cannot be measured on a
+one-GPU box:
+
+* z slabs ``1 x 1 x N``: halos are whole storage planes sent in place by RCCL and overlapped
+  with the inner planes' update, but each rank moves ``2 * fuse`` full L x L planes per pass
+  over just two links;
+* the balanced ``MPI_Dims_create`` grid (2x2x2 on 8 GPUs): 4x less halo per link, spread over
+  up to six links, but packed (pack / RCCL / unpack) and not overlapped;
+* the fuse depth T (steps per exchange): the same bytes per step, fewer messages at larger T.
+
+``tune_data_path`` first checks every candidate's exact data path against the golden model on
+a small grid (``selfcheck``), then times a short run of each on the real problem, with every
+rank agreeing on the winner (the time that counts is the slowest rank's).
+"""
+from __future__ import annotations
+
+import contextlib
+import copy
+import os
+import time
+from typing import Dict, List, Optional, Sequence, Tuple
+
+from .decomp import choose_dims, dims_create, init_domain
+
+
+def selfcheck(ctx, backend: str, dims, fuse: int, transport: str, overlap: str, L: int = 64,
+              steps: int = 9):
+    """Run the exact data path (decomposition, transport, in-place halos, overlap, fuse depth)
+    on a small grid and compare with the numpy/torch golden model computed by every rank.
+    Returns ``(ok, max_abs_err, transport_used)``; ``ok`` is agreed by all ranks."""
+    import numpy as np
+
+    from ..models.grayscott import GrayScott
+    from ..ops import reference as ref
+    from ..utils.config import Settings
+
+    L = max(L, 8 * max(dims))
+    s = Settings(L=L, precision="Float32", F=0.02, k=0.048, dt=1.0, Du=0.2, Dv=0.1, noise=0.1,
+                 backend="AMDGPU" if backend == "hip" else "CPU", seed=77, transport=transport,
+                 overlap=overlap)
+    dom = init_domain(L, ctx.world_size, ctx.rank, periodic=False, dims=dims)
+    sim = GrayScott(s, dom, ctx, fuse=min(fuse, min(dom.proc_sizes)))
+    try:
+        sim.init_fields()
+        sim.iterate(steps)
+        u, v = sim.get_fields()
+        used = sim.transport
+    finally:
+        sim.close()
+    ru, rv = ref.run(L, steps, noise_amp=0.1, seed=77, dtype=np.float32, backend="torch")
+    (ox, oy, oz), (nx, ny, nz) = dom.proc_offsets, dom.proc_sizes
+    blk = (slice(oz, oz + nz), slice(oy, oy + ny), slice(ox, ox + nx))
+    err = float(max(np.abs(u - ru[blk]).max(), np.abs(v - rv[blk]).max()))
+    err = ctx.allreduce(err, "max")
+    return err < 1e-4, err, used
+
+
+def candidates(L: int, nprocs: int, backend: str) -> List[Tuple[List[int], int]]:
+    """(dims, fuse) pairs worth timing for ``nprocs`` ranks on an L^3 grid (fuse 0 = auto)."""
+    out: List[Tuple[List[int], int]] = []
+
+    def add(d, f):
+        if (list(d), f) not in out:
+            out.append((list(d), f))
+
+    if nprocs == 1:
+        return [([1, 1, 1], 0)]
+    z = choose_dims(L, nprocs, "z", backend)
+    bal = dims_create(nprocs)
+    if backend == "hip" and L // nprocs >= 8:
+        add(z, 0)
+        add(z, 2)
+    add(bal, 0)
+    if backend == "hip":
+        add(bal, 3)
+    return out
+
+
+def time_data_path(settings, ctx, L: int, dims, fuse: int, steps: int = 30, warmup: int = 6,
+                   seed: int = 2024) -> float:
+    """Seconds for ``steps`` steps of the real problem on this data path (max over ranks)."""
+    import torch
+
+    from ..models.grayscott import GrayScott
+
+    s = copy.copy(settings)
+    s.fuse_steps = int(fuse)
+    dom = init_domain(L, ctx.world_size, ctx.rank, periodic=False, dims=dims)
+    sim = GrayScott(s, dom, ctx)
+    try:
+        sim.init_fields()
+        sim.randomize_fields(seed=seed)
+
+        def sync():
+            sim.synchronize()
+            if sim.backend == "hip":
+                torch.cuda.synchronize()
+
+        sim.iterate(warmup)
+        sync()
+        ctx.barrier()
+        t0 = time.perf_counter()
+        sim.iterate(steps)
+        sync()
+        el = time.perf_counter() - t0
+    finally:
+        sim.close()
+    return ctx.allreduce(el, "max")
+
+
+def tune_data_path(settings, ctx, L: int, backend: str,
+                   cands: Optional[Sequence[Tuple[List[int], int]]] = None,
+                   steps: int = 30, warmup: int = 6, log=None) -> Dict:
+    """Self-check and time every candidate; returns ``{"dims", "fuse", "transport",
+    "overlap", "table"}`` for the fastest correct one (identical on every rank)."""
+    from ..models.grayscott import default_fuse
+
+    cands = list(cands) if cands is not None else candidates(L, ctx.world_size, backend)
+    table = []
+    best = None
+    for dims, fuse in cands:
+        dom = init_domain(L, ctx.world_size, ctx.rank, periodic=False, dims=dims)
+        f = fuse if fuse > 0 else default_fuse(backend, dom, settings.dtype_name)
+        f = max(1, min(f, min(dom.proc_sizes)))
+        if any(r["dims"] == list(dims) and r["fuse"] == f for r in table):
+            continue  # "auto" resolved to a depth already in the list
+        row = {"dims": list(dims), "fuse": f}
+        chosen = None
+        for tr, ov, inplace in ((settings.transport, settings.overlap, None),
+                                (settings.transport, "off", "0"), ("torch", "off", "0")):
+            with _inplace_env(inplace):
+                try:
+                    ok, err, used = selfcheck(ctx, backend, dims, f, tr, ov)
+                except Exception:  # a path that cannot even be set up is skipped
+                    ok, used = False, None
+            ok = ctx.allreduce(1.0 if ok else 0.0, "min") > 0
+            if ok:
+                chosen = (used, ov, inplace)
+                break
+        if chosen is None:
+            row.update(ok=False)
+            table.append(row)
+            continue
+        s = copy.copy(settings)
+        s.transport, s.overlap = chosen[0], chosen[1]
+        with _inplace_env(chosen[2]):
+            el = time_data_path(s, ctx, L, dims, f, steps=steps, warmup=warmup)
+        row.update(ok=True, transport=chosen[0], overlap=chosen[1],
+                   inplace_halos=chosen[2] is None, ms_per_step=round(1e3 * el / steps, 4))
+        table.append(row)
+        if log is not None and ctx.rank == 0:
+            log(f"data path {row}")
+        if best is None or el < best[0]:
+            best = (el, list(dims), f, chosen)
+    if best is None:
+        raise RuntimeError(f"no multi-rank data path passed its self-check: {table}")
+    return {"dims": best[1], "fuse": best[2], "transport": best[3][0], "overlap": best[3][1],
+            "inplace_halos": best[3][2] is None, "table": table}
+
+
+@contextlib.contextmanager
+def _inplace_env(inplace: Optional[str]):
+    """GS_INPLACE_HALO=0 turns the in-place RCCL plane halos off (read at engine creation)."""
+    old = os.environ.get("GS_INPLACE_HALO")
+    if inplace is not None:
+        os.environ["GS_INPLACE_HALO"] = inplace
+    try:
+        yield
+    finally:
+        if inplace is not None:
+            if old is None:
+                os.environ.pop("GS_INPLACE_HALO", None)
+            else:
+                os.environ["GS_INPLACE_HALO"] = old

@@ -1,5 +1,4 @@
 set -e
 mkdir -p gpurun_out
-cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof64 -o run -- python3 bench.py --L 64 --steps 200 --warmup 20 > gpurun_out/prof64.log 2>&1
-find gpurun_out/prof64 -type f | head
+timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 2 --L 128 --steps 60 --warmup 6 --transport host > gpurun_out/bench2_host.json 2> gpurun_out/bench2_host.err
+cut -c1-400 gpurun_out/bench2_host.json; python -c "import json; d=json.load(open('gpurun_out/bench2_host.json')); print(json.dumps(d['data_path_tuning'], indent=0))"
