@@ -110,13 +110,13 @@ class HipBackend final : public gs::Backend {
   bool fused_supported(int n) const override { return gsk::fused_supported(g_, n); }
 
   bool fused_runs(int src, int dst, int n, int64_t t, int zlo0, int zlen0, int zlo1,
-                  int zlen1, bool leave_room) override {
+                  int zlen1, bool leave_room, int tiles, int sides) override {
     if (!gsk::fused_supported(g_, n)) return false;
     if (!tuned_[n]) autotune(src, dst, n, t);
     const bool pin = fused_pinned();
     const bool ok = gsk::launch_fused<T>(buf_[src], buf_[dst], g_, p_, n, t, stream_,
                                          pin ? -1 : cfg_[n], pin ? -1 : sched_[n], zlo0, zlen0,
-                                         zlo1, zlen1, leave_room ? reserve_ : 0);
+                                         zlo1, zlen1, leave_room ? reserve_ : 0, tiles, sides);
     if (!ok) throw std::runtime_error("fused_runs: invalid z-runs");
     HIP_CHECK(hipGetLastError());
     return true;

@@ -72,10 +72,11 @@ int gs_plan_zplanes(gs_engine* e) { return e->eng->plan().zplanes; }
 // Timing primitive: one fused k-step update of the given z-runs from the current buffer into
 // the other one (interior planes only, so the next pass overwrites it; state unchanged).
 int gs_fused_runs_raw(gs_engine* e, int32_t k, int32_t zlo0, int32_t zlen0, int32_t zlo1,
-                      int32_t zlen1) {
+                      int32_t zlen1, int32_t tiles, int32_t sides) {
   GS_TRY({
     gs::Engine& g = *e->eng;
-    if (!g.backend()->fused_runs(g.cur(), 1 - g.cur(), k, g.step(), zlo0, zlen0, zlo1, zlen1))
+    if (!g.backend()->fused_runs(g.cur(), 1 - g.cur(), k, g.step(), zlo0, zlen0, zlo1, zlen1,
+                                 false, tiles, sides))
       throw std::runtime_error("fused runs unsupported for this k / backend");
   })
 }

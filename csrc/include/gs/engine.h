@@ -43,11 +43,13 @@ class Backend {
   // Supported exactly when fused_supported(n); reads level-0 planes zlo-n .. zend+n-1 only.
   virtual bool fused_supported(int n) const { (void)n; return false; }
   // leave_room: launch fewer workgroups than the device holds so concurrently running
-  // communication kernels (RCCL) find free slots instead of waiting for this kernel to end
+  // communication kernels (RCCL) find free slots instead of waiting for this kernel to end.
+  // tiles: 0 all x-y tiles; 1 only the inner tiles, whose inputs stay clear of the x / y
+  // halos flagged in `sides` (bit0 -x, bit1 +x, bit2 -y, bit3 +y); 2 the remaining ring.
   virtual bool fused_runs(int src, int dst, int n, int64_t t, int zlo0, int zlen0, int zlo1,
-                          int zlen1, bool leave_room = false) {
+                          int zlen1, bool leave_room = false, int tiles = 0, int sides = 0) {
     (void)src; (void)dst; (void)n; (void)t; (void)zlo0; (void)zlen0; (void)zlo1; (void)zlen1;
-    (void)leave_room;
+    (void)leave_room; (void)tiles; (void)sides;
     return false;
   }
   // in-place transport of a zplanes plan straight from / into field buffer b (no pack)
@@ -124,10 +126,11 @@ class Engine {
     for (int d = 0; d < 27; ++d)
       if (d != 13 && cfg_.nbr[d] >= 0 && (on || cfg_.nbr[d] != cfg_.rank)) has_remote_ = true;
   }
-  // whether a pass of k steps runs with the halo exchange overlapped with the inner planes
+  // whether a pass of k steps runs with the halo exchange overlapped with the inner update:
+  // z-slab plans (in-place planes) split z only; packed plans split z and the x-y tile grid
   bool overlapped(int k) const {
-    return overlap_ != 0 && cfg_.use_fused && k > 1 && has_remote_ && plan_.zplanes &&
-           be_->has_comm_stream() && be_->fused_supported(k) && cfg_.g.nz >= 2 * k + 1;
+    return overlap_ != 0 && cfg_.use_fused && k > 1 && has_remote_ && be_->has_comm_stream() &&
+           be_->fused_supported(k) && cfg_.g.nz >= 2 * k + 1;
   }
   double comm_calls() const { return (double)ncomm_; }
 
@@ -248,9 +251,18 @@ class Engine {
         be_->comm_select(true);
         exchange_start();
         be_->comm_select(false);
-        {
+        // packed plans: the inner box is clear of every face with a neighbour (z by planes,
+        // x / y by whole tiles); z-slab plans keep all tiles and split z only
+        const int* nb = cfg_.nbr;
+        const bool zm = plan_.zplanes || nb[dir_index(0, 0, -1)] >= 0;
+        const bool zp = plan_.zplanes || nb[dir_index(0, 0, 1)] >= 0;
+        const int z0 = zm ? k : 0, z1 = zp ? nz - k : nz;
+        const int sides = plan_.zplanes ? 0
+            : (nb[dir_index(-1, 0, 0)] >= 0 ? 1 : 0) | (nb[dir_index(1, 0, 0)] >= 0 ? 2 : 0) |
+              (nb[dir_index(0, -1, 0)] >= 0 ? 4 : 0) | (nb[dir_index(0, 1, 0)] >= 0 ? 8 : 0);
+        if (z1 > z0) {
           TraceRange tr("gs.fused_inner");
-          be_->fused_runs(cur_, oth, k, t_, k, nz - 2 * k, 0, 0, true);
+          be_->fused_runs(cur_, oth, k, t_, z0, z1 - z0, 0, 0, true, sides ? 1 : 0, sides);
         }
         be_->comm_select(true);
         exchange_finish(true);
@@ -258,7 +270,11 @@ class Engine {
         be_->comm_join();
         {
           TraceRange tr("gs.fused_shell");
-          be_->fused_runs(cur_, oth, k, t_, 0, k, nz - k, k);
+          // z end slabs over all tiles, then (packed plans) the ring tiles of the inner planes
+          const int la = z0, lb = nz - (z1 > z0 ? z1 : z0);
+          if (la > 0) be_->fused_runs(cur_, oth, k, t_, 0, la, nz - lb, lb);
+          else if (lb > 0) be_->fused_runs(cur_, oth, k, t_, nz - lb, lb, 0, 0);
+          if (sides && z1 > z0) be_->fused_runs(cur_, oth, k, t_, z0, z1 - z0, 0, 0, false, 2, sides);
         }
         cur_ = oth;
         t_ += k;

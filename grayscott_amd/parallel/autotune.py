@@ -59,16 +59,17 @@ def selfcheck(ctx, backend: str, dims, fuse: int, transport: str, overlap: str, 
     return err < 1e-4, err, used
 
 
-def candidates(L: int, nprocs: int, backend: str) -> List[Tuple[List[int], int]]:
-    """(dims, fuse) pairs worth timing for ``nprocs`` ranks on an L^3 grid (fuse 0 = auto)."""
-    out: List[Tuple[List[int], int]] = []
+def candidates(L: int, nprocs: int, backend: str) -> List[Tuple[List[int], int, str]]:
+    """(dims, fuse, overlap) triples worth timing for ``nprocs`` ranks on an L^3 grid
+    (fuse 0 = auto)."""
+    out: List[Tuple[List[int], int, str]] = []
 
-    def add(d, f):
-        if (list(d), f) not in out:
-            out.append((list(d), f))
+    def add(d, f, ov="auto"):
+        if (list(d), f, ov) not in out:
+            out.append((list(d), f, ov))
 
     if nprocs == 1:
-        return [([1, 1, 1], 0)]
+        return [([1, 1, 1], 0, "auto")]
     z = choose_dims(L, nprocs, "z", backend)
     bal = dims_create(nprocs)
     if backend == "hip" and L // nprocs >= 8:
@@ -76,13 +77,15 @@ def candidates(L: int, nprocs: int, backend: str) -> List[Tuple[List[int], int]]
         add(z, 2)
     add(bal, 0)
     if backend == "hip":
+        add(bal, 0, "off")
         add(bal, 3)
     return out
 
 
 def time_data_path(settings, ctx, L: int, dims, fuse: int, steps: int = 30, warmup: int = 6,
                    seed: int = 2024) -> float:
-    """Seconds for ``steps`` steps of the real problem on this data path (max over ranks)."""
+    """(seconds for ``steps`` steps of the real problem on this data path (max over ranks),
+    whether its passes overlap the halo exchange)."""
     import torch
 
     from ..models.grayscott import GrayScott
@@ -107,30 +110,35 @@ def time_data_path(settings, ctx, L: int, dims, fuse: int, steps: int = 30, warm
         sim.iterate(steps)
         sync()
         el = time.perf_counter() - t0
+        ovd = bool(sim.overlapped)
     finally:
         sim.close()
-    return ctx.allreduce(el, "max")
+    return ctx.allreduce(el, "max"), ovd
 
 
 def tune_data_path(settings, ctx, L: int, backend: str,
-                   cands: Optional[Sequence[Tuple[List[int], int]]] = None,
+                   cands: Optional[Sequence[Tuple]] = None,
                    steps: int = 30, warmup: int = 6, log=None) -> Dict:
-    """Self-check and time every candidate; returns ``{"dims", "fuse", "transport",
-    "overlap", "table"}`` for the fastest correct one (identical on every rank)."""
+    """Self-check and time every candidate ``(dims, fuse[, overlap])``; returns ``{"dims",
+    "fuse", "transport", "overlap", "inplace_halos", "table"}`` for the fastest correct one
+    (identical on every rank)."""
     from ..models.grayscott import default_fuse
 
     cands = list(cands) if cands is not None else candidates(L, ctx.world_size, backend)
     table = []
     best = None
-    for dims, fuse in cands:
+    for cand in cands:
+        dims, fuse = cand[0], cand[1]
+        ov0 = cand[2] if len(cand) > 2 else settings.overlap
         dom = init_domain(L, ctx.world_size, ctx.rank, periodic=False, dims=dims)
         f = fuse if fuse > 0 else default_fuse(backend, dom, settings.dtype_name)
         f = max(1, min(f, min(dom.proc_sizes)))
-        if any(r["dims"] == list(dims) and r["fuse"] == f for r in table):
+        if any(r["dims"] == list(dims) and r["fuse"] == f and r["overlap_req"] == ov0
+               for r in table):
             continue  # "auto" resolved to a depth already in the list
-        row = {"dims": list(dims), "fuse": f}
+        row = {"dims": list(dims), "fuse": f, "overlap_req": ov0}
         chosen = None
-        for tr, ov, inplace in ((settings.transport, settings.overlap, None),
+        for tr, ov, inplace in ((settings.transport, ov0, None),
                                 (settings.transport, "off", "0"), ("torch", "off", "0")):
             with _inplace_env(inplace):
                 try:
@@ -148,8 +156,8 @@ def tune_data_path(settings, ctx, L: int, backend: str,
         s = copy.copy(settings)
         s.transport, s.overlap = chosen[0], chosen[1]
         with _inplace_env(chosen[2]):
-            el = time_data_path(s, ctx, L, dims, f, steps=steps, warmup=warmup)
-        row.update(ok=True, transport=chosen[0], overlap=chosen[1],
+            el, ovd = time_data_path(s, ctx, L, dims, f, steps=steps, warmup=warmup)
+        row.update(ok=True, transport=chosen[0], overlap=chosen[1], overlapped=ovd,
                    inplace_halos=chosen[2] is None, ms_per_step=round(1e3 * el / steps, 4))
         table.append(row)
         if log is not None and ctx.rank == 0:

@@ -6,8 +6,11 @@ For a z-slab sub-domain (what one rank of an N-GPU 1x1xN run owns) it times, per
   inner  -- the launch over planes [k, nz-k) (runs while the halos are in flight),
   shell  -- the launch over the two k-plane boundary slabs (runs after they land).
 The overlapped pass costs shell + max(inner, exchange); the plain one full + exchange.
+With --packed the sub-domain is one rank of the balanced grid (neighbours on every side):
+inner = the inner x-y tiles x planes [k, nz-k), shell = the z end slabs + the ring tiles.
 
   python scripts/bench_overlap_split.py --nz 64 128 256 --k 2 3
+  python scripts/bench_overlap_split.py --packed --L 256 --nz 256 --k 2 3
 """
 import argparse
 import json
@@ -24,6 +27,7 @@ def main():
     ap.add_argument("--k", type=int, nargs="+", default=[2, 3])
     ap.add_argument("--reps", type=int, default=40)
     ap.add_argument("--out", default="")
+    ap.add_argument("--packed", action="store_true")
     a = ap.parse_args()
     import torch
     from grayscott_amd.models.grayscott import GrayScott
@@ -40,8 +44,9 @@ def main():
             sim.init_fields()
             lib, h = sim.engine.lib, sim.engine.h
 
-            def run(z0, n0, z1, n1):
-                native.check(lib, lib.gs_fused_runs_raw(h, k, z0, n0, z1, n1), "fused_runs")
+            def run(z0, n0, z1, n1, tiles=0):
+                native.check(lib, lib.gs_fused_runs_raw(h, k, z0, n0, z1, n1, tiles,
+                                                        15 if tiles else 0), "fused_runs")
 
             def timed(*runs):
                 for _ in range(3):
@@ -58,10 +63,16 @@ def main():
                 return e0.elapsed_time(e1) / a.reps * 1e3  # us
 
             full = timed((0, nz, 0, 0))
-            inner = timed((k, nz - 2 * k, 0, 0))
-            shell = timed((0, k, nz - k, k))
-            both = timed((k, nz - 2 * k, 0, 0), (0, k, nz - k, k))
-            row = {"local": [a.L, a.L, nz], "k": k, "full_us": round(full, 1),
+            if a.packed:
+                ins = [(k, nz - 2 * k, 0, 0, 1)]
+                shs = [(0, k, nz - k, k), (k, nz - 2 * k, 0, 0, 2)]
+            else:
+                ins = [(k, nz - 2 * k, 0, 0)]
+                shs = [(0, k, nz - k, k)]
+            inner = timed(*ins)
+            shell = timed(*shs)
+            both = timed(*(ins + shs))
+            row = {"local": [a.L, a.L, nz], "k": k, "packed": a.packed, "full_us": round(full, 1),
                    "inner_us": round(inner, 1), "shell_us": round(shell, 1),
                    "inner_plus_shell_us": round(both, 1),
                    "full_mlups": round(a.L * a.L * nz * k / full, 0),

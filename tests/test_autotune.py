@@ -22,7 +22,7 @@ def _worker(rank, world, port, out):
     ctx = gdist.init_from_env("cpu")
     s = Settings(L=24, precision="Float32", F=0.02, k=0.048, dt=1.0, Du=0.2, Dv=0.1, noise=0.1,
                  backend="CPU", transport="auto")
-    assert candidates(24, 2, "cpu") == [([2, 1, 1], 0)]
+    assert candidates(24, 2, "cpu") == [([2, 1, 1], 0, "auto")]
     r = tune_data_path(s, ctx, 24, "cpu", cands=[([1, 1, 2], 1), ([2, 1, 1], 0)], steps=4,
                        warmup=1)
     with open(os.path.join(out, f"r{rank}.json"), "w") as fh:
@@ -43,6 +43,7 @@ def test_tune_data_path_two_ranks():
 
 def test_candidates_for_mi355x():
     from grayscott_amd.parallel.autotune import candidates
-    assert candidates(512, 8, "hip") == [([1, 1, 8], 0), ([1, 1, 8], 2), ([2, 2, 2], 0),
-                                        ([2, 2, 2], 3)]
-    assert candidates(512, 1, "hip") == [([1, 1, 1], 0)]
+    assert candidates(512, 8, "hip") == [([1, 1, 8], 0, "auto"), ([1, 1, 8], 2, "auto"),
+                                        ([2, 2, 2], 0, "auto"), ([2, 2, 2], 0, "off"),
+                                        ([2, 2, 2], 3, "auto")]
+    assert candidates(512, 1, "hip") == [([1, 1, 1], 0, "auto")]

@@ -63,6 +63,28 @@ def test_gpu_z_slabs_overlap_matches_single_rank(world, L, fuse, prec, overlap):
     np.testing.assert_array_equal(vn, v1)
 
 
+@pytest.mark.parametrize("world,L,fuse,prec,overlap", [
+    (2, 48, 2, "Float32", "on"),
+    (4, 64, 3, "Float32", "on"),
+    (8, 64, 3, "Float32", "on"),
+    (4, 40, 2, "Float64", "on"),
+    (8, 48, 2, "Float32", "off"),
+])
+def test_gpu_balanced_overlap_matches_single_rank(world, L, fuse, prec, overlap):
+    """Balanced (Dims_create) grid with packed halos: the inner tiles x inner planes run while
+    pack / transport / unpack are in flight on the comm stream, then the z end slabs and the
+    ring tiles -- bit-identical to one rank."""
+    steps = 11
+    u1, v1, _ = run_ranks(1, _cfg(L, steps, fuse, False, prec))
+    cfg = _cfg(L, steps, fuse, False, prec)
+    cfg["settings"].update(decomposition="balanced", overlap=overlap)
+    un, vn, meta = run_ranks(world, cfg)
+    assert not any(m["zplanes"] for m in meta)
+    assert all(m["overlapped"] == (overlap == "on") for m in meta)
+    np.testing.assert_array_equal(un, u1)
+    np.testing.assert_array_equal(vn, v1)
+
+
 @pytest.mark.parametrize("world,L,fuse,decomp,overlap", [
     (1, 40, 3, "balanced", "auto"),
     (4, 40, 2, "balanced", "auto"),

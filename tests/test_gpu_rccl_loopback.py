@@ -68,6 +68,8 @@ def test_rccl_loopback_periodic_packed(L, fuse, prec):
     u1, v1, i1 = _run(dom, s, fuse, 11, loopback=True)
     assert i0["transport"] == "none" and i1["transport"] == "rccl"
     assert not i1["zplanes"]
+    # fused passes overlap the packed exchange with the inner tiles (engine.h overlapped)
+    assert i1["overlapped"] == (fuse > 1 and L >= 2 * fuse + 1)
     assert np.isfinite(u1).all() and np.isfinite(v1).all()
     np.testing.assert_array_equal(u1, u0)
     np.testing.assert_array_equal(v1, v0)
