@@ -114,8 +114,26 @@ class HipBackend final : public gs::Backend {
     if (!gsk::fused_supported(g_, n)) return false;
     if (!tuned_[n]) autotune(src, dst, n, t);
     const bool pin = fused_pinned();
+    // the post-exchange parts of an overlapped pass (z end slabs, ring tiles) are short,
+    // latency-bound launches: they get their own tuned tile shape / schedule
+    const int kind = leave_room ? 0 : (tiles == 2 ? 2 : (zlen1 > 0 ? 1 : 0));
+    int c = cfg_[n], sc = sched_[n];
+    if (kind && !pin) {
+      const int slot = n + 4 * kind;
+      if (!part_tuned_[slot]) {
+        part_tuned_[slot] = true;
+        const Part pt{zlo0, zlen0, zlo1, zlen1, tiles, sides};
+        float ms = 0.f;
+        if (!autotune_part(src, dst, n, t, pt, &part_cfg_[slot], &part_sched_[slot], &ms)) {
+          part_cfg_[slot] = cfg_[n];
+          part_sched_[slot] = sched_[n];
+        }
+      }
+      c = part_cfg_[slot];
+      sc = part_sched_[slot];
+    }
     const bool ok = gsk::launch_fused<T>(buf_[src], buf_[dst], g_, p_, n, t, stream_,
-                                         pin ? -1 : cfg_[n], pin ? -1 : sched_[n], zlo0, zlen0,
+                                         pin ? -1 : c, pin ? -1 : sc, zlo0, zlen0,
                                          zlo1, zlen1, leave_room ? reserve_ : 0, tiles, sides);
     if (!ok) throw std::runtime_error("fused_runs: invalid z-runs");
     HIP_CHECK(hipGetLastError());
@@ -164,12 +182,18 @@ class HipBackend final : public gs::Backend {
   // reads `src` and writes `dst`, so every candidate can be timed on the live buffers without
   // changing the simulation state, and all candidates produce bit-identical results.
   // Disabled by GS_AUTOTUNE=0 or by an explicit GS_FUSED_CFG / GS_FUSED_SCHED.
-  void autotune(int src, int dst, int n, int64_t t) {
-    tuned_[n] = true;
+  struct Part {  // the launch being tuned: z-runs and tile subset (whole interior: zlen0 < 0)
+    int zlo0, zlen0, zlo1, zlen1, tiles, sides;
+  };
+  static bool autotune_enabled() {
     const char* e = getenv("GS_AUTOTUNE");
-    if ((e && atoi(e) == 0) || getenv("GS_FUSED_CFG") || getenv("GS_FUSED_SCHED") ||
-        fused_pinned())
-      return;
+    return !((e && atoi(e) == 0) || getenv("GS_FUSED_CFG") || getenv("GS_FUSED_SCHED") ||
+             fused_pinned());
+  }
+  // best {cfg, sched} for one launch shape; false if tuning is disabled / unsupported
+  bool autotune_part(int src, int dst, int n, int64_t t, const Part& pt, int* cfg, int* sched,
+                     float* ms_best) {
+    if (!autotune_enabled()) return false;
     struct Cand { int cfg, sched; };
     std::vector<Cand> cands;
     const bool variants = !g_.periodic && p_.noise != 0.0;  // tile variants instantiated here
@@ -177,24 +201,26 @@ class HipBackend final : public gs::Backend {
     if (!variants) cfgs = {0};
     else if (sizeof(T) == 4) cfgs = {0, 1, 2, 3, 5, 8, 12, 16, 17, 19, 20, 30, 31, 33};
     else cfgs = {0, 1, 13, 15, 19, 32, 33};
+    const int nsched = pt.zlen1 > 0 ? 1 : 3;  // two z-runs always use schedule 0
     for (int c : cfgs)
-      for (int sc = 0; sc <= 2; ++sc) cands.push_back({c, sc});
+      for (int sc = 0; sc < nsched; ++sc) cands.push_back({c, sc});
+    auto launch = [&](const Cand& c) {
+      return gsk::launch_fused<T>(buf_[src], buf_[dst], g_, p_, n, t, stream_, c.cfg, c.sched,
+                                  pt.zlo0, pt.zlen0, pt.zlo1, pt.zlen1, 0, pt.tiles, pt.sides);
+    };
     // interleaved rounds (box-to-box and launch-to-launch jitter is several %): first launch
     // of each candidate is a warm-up, then the best of kRounds timed launches decides
     constexpr int kRounds = 3;
     std::vector<float> tbest(cands.size(), 1e30f);
     for (size_t i = 0; i < cands.size(); ++i)
-      if (!gsk::launch_fused<T>(buf_[src], buf_[dst], g_, p_, n, t, stream_, cands[i].cfg,
-                                cands[i].sched))
-        return;
+      if (!launch(cands[i])) return false;
     hipEvent_t e0, e1;
     HIP_CHECK(hipEventCreate(&e0));
     HIP_CHECK(hipEventCreate(&e1));
     for (int r = 0; r < kRounds; ++r)
       for (size_t i = 0; i < cands.size(); ++i) {
         HIP_CHECK(hipEventRecord(e0, stream_));
-        gsk::launch_fused<T>(buf_[src], buf_[dst], g_, p_, n, t, stream_, cands[i].cfg,
-                             cands[i].sched);
+        launch(cands[i]);
         HIP_CHECK(hipEventRecord(e1, stream_));
         HIP_CHECK(hipEventSynchronize(e1));
         HIP_CHECK(hipGetLastError());
@@ -206,12 +232,20 @@ class HipBackend final : public gs::Backend {
     for (size_t i = 0; i < cands.size(); ++i)
       if (tbest[i] < best) {
         best = tbest[i];
-        cfg_[n] = cands[i].cfg;
-        sched_[n] = cands[i].sched;
+        *cfg = cands[i].cfg;
+        *sched = cands[i].sched;
       }
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
-    tuned_ms_[n] = best;
+    *ms_best = best;
+    return true;
+  }
+
+  void autotune(int src, int dst, int n, int64_t t) {
+    tuned_[n] = true;
+    const Part whole{0, -1, 0, 0, 0, 0};
+    float ms = 0.f;
+    if (autotune_part(src, dst, n, t, whole, &cfg_[n], &sched_[n], &ms)) tuned_ms_[n] = ms;
   }
 
   void fused_choice(int n, int* cfg, int* sched, float* ms) const {
@@ -346,6 +380,11 @@ class HipBackend final : public gs::Backend {
   int cfg_[4] = {-1, -1, -1, -1};
   int sched_[4] = {-1, -1, -1, -1};
   float tuned_ms_[4] = {0.f, 0.f, 0.f, 0.f};
+  // tuned shapes of the overlapped passes' post-exchange parts: slot n + 4 * kind
+  // (kind 1: the two z end slabs, kind 2: the ring tiles)
+  bool part_tuned_[12] = {};
+  int part_cfg_[12] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+  int part_sched_[12] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
 };
 
 }  // namespace

@@ -43,7 +43,20 @@ def initialization(args: Sequence[str]):
 def initialize_from_settings(settings: Settings):
     backend, _ = load_backend_and_lang(settings)
     ctx = init_from_env(backend)
-    dims = choose_dims(settings.L, ctx.world_size, settings.decomposition, backend)
+    if str(settings.decomposition).lower() == "tune":
+        # time the candidate data paths on this node first (parallel/autotune.py)
+        from .parallel.autotune import tune_data_path
+        if ctx.world_size > 1 and not settings.periodic and isinstance(settings.L, int):
+            t = tune_data_path(settings, ctx, settings.L, backend)
+            settings.fuse_steps = t["fuse"]
+            settings.transport, settings.overlap = t["transport"], t["overlap"]
+            if not t["inplace_halos"]:
+                os.environ["GS_INPLACE_HALO"] = "0"
+            dims = t["dims"]
+        else:
+            dims = choose_dims(settings.L, ctx.world_size, "auto", backend)
+    else:
+        dims = choose_dims(settings.L, ctx.world_size, settings.decomposition, backend)
     domain = init_domain(settings.L, ctx.world_size, ctx.rank, periodic=settings.periodic,
                          dims=dims)
     sim = GrayScott(settings, domain, ctx)

@@ -14,7 +14,8 @@ Extension keys (not in the reference, all optional, documented in README):
   ``periodic`` (bool), ``seed`` (int, noise stream key), ``fuse_steps`` (int, steps fused per
   halo exchange / temporal blocking depth, 0 = auto), ``transport`` ("auto"|"rccl"|"torch"),
   ``output_engine`` ("bp4"), ``perf_log`` (path of a JSON-lines perf log), ``diagnostics`` (bool),
-  ``decomposition`` ("auto"|"balanced"|"z": process grid, see parallel/decomp.choose_dims),
+  ``decomposition`` ("auto"|"balanced"|"z": process grid, see parallel/decomp.choose_dims;
+  "tune": self-check and time the candidate grids / fuse depths, parallel/autotune.py),
   ``overlap`` ("auto"|"on"|"off": overlap the halo exchange with the inner-plane update),
   ``async_output`` (bool, default true: output steps are written behind the simulation).
 """

@@ -61,6 +61,21 @@ def test_decomposition_invariant_output(tmp_path):
     np.testing.assert_array_equal(out[1][1], out[3][1])
 
 
+def test_tuned_decomposition_run(tmp_path):
+    """decomposition = "tune": the data path is self-checked and timed before the run, and the
+    output equals a one-rank run."""
+    out = {}
+    for n, dec in ((1, "auto"), (2, "tune")):
+        d = tmp_path / f"r{n}"
+        d.mkdir()
+        r = launch(_cfg(d, "c.toml", steps=12, plotgap=12, L=24, output="o.bp",
+                        decomposition=dec), n, str(d))
+        assert r.returncode == 0, r.stderr[-3000:]
+        with BP4Reader(str(d / "o.bp")) as rd:
+            out[n] = rd.read("U", -1)
+    np.testing.assert_array_equal(out[1], out[2])
+
+
 def test_checkpoint_restart_bitwise(tmp_path):
     """Run 40 steps straight vs 20 steps + restart (with a different rank count) to 40."""
     full = tmp_path / "full"
