@@ -79,14 +79,34 @@ class DistContext:
 _CTX: Optional[DistContext] = None
 
 
+# Launcher environments: torchrun, then the MPI / batch launchers the reference is run with
+# (`mpirun -n N`, test/functional/functional-GrayScott.jl:9; srun / jsrun in scripts/job_*.sh).
+_LAUNCHERS = (
+    ("RANK", "WORLD_SIZE", "LOCAL_RANK"),                                  # torchrun
+    ("PMI_RANK", "PMI_SIZE", "MPI_LOCALRANKID"),                           # MPICH / hydra
+    ("OMPI_COMM_WORLD_RANK", "OMPI_COMM_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_RANK"),  # Open MPI
+    ("SLURM_PROCID", "SLURM_NTASKS", "SLURM_LOCALID"),                     # srun
+)
+
+
+def launcher_env(env=None):
+    """(rank, world_size, local_rank) from the first launcher whose variables are set."""
+    env = os.environ if env is None else env
+    for rk, sz, lc in _LAUNCHERS:
+        if rk in env and sz in env:
+            rank = int(env[rk])
+            return rank, int(env[sz]), int(env.get(lc, rank))
+    return 0, 1, 0
+
+
 def init_from_env(device: str = "cpu") -> DistContext:
-    """Initialise (once) from torchrun-style environment variables."""
+    """Initialise (once) from the launcher's environment (torchrun, mpiexec, srun).  Without
+    torchrun, the gloo rendezvous uses MASTER_ADDR (default 127.0.0.1: one node) and
+    MASTER_PORT (default 29531)."""
     global _CTX
     if _CTX is not None:
         return _CTX
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    rank, world, local = launcher_env()
     ctx = DistContext(rank=rank, world_size=world, local_rank=local)
     if device == "hip":
         torch.cuda.set_device(local % max(1, torch.cuda.device_count()))

@@ -61,6 +61,48 @@ def test_decomposition_invariant_output(tmp_path):
     np.testing.assert_array_equal(out[1][1], out[3][1])
 
 
+def _mpiexec():
+    import shutil
+    for c in (shutil.which("mpiexec"), "/opt/conda/bin/mpiexec"):
+        if c and os.path.exists(c):
+            return c
+    return None
+
+
+@pytest.mark.skipif(_mpiexec() is None, reason="no mpiexec on this machine")
+def test_mpiexec_launch_4_ranks(tmp_path):
+    """The reference's own launch form (`mpirun -n 4 ...`, functional-GrayScott.jl:9): ranks
+    come from the MPI launcher's environment (PMI_RANK / OMPI_COMM_WORLD_RANK), same output as
+    one rank."""
+    out = {}
+    for n in (1, 4):
+        d = tmp_path / f"r{n}"
+        d.mkdir()
+        cfg = _cfg(d, "c.toml", steps=12, plotgap=6, L=24, output="o.bp")
+        e = dict(os.environ, OMP_NUM_THREADS="1", MASTER_ADDR="127.0.0.1",
+                 MASTER_PORT=str(free_port()))
+        for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+            e.pop(k, None)
+        r = subprocess.run([_mpiexec(), "-n", str(n), sys.executable,
+                            os.path.join(ROOT, "gray-scott.py"), cfg], cwd=str(d), env=e,
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-3000:]
+        with BP4Reader(str(d / "o.bp")) as rd:
+            assert rd.steps == 2
+            assert len(rd.variables(0)["U"].blocks) == n
+            out[n] = rd.read("U", -1)
+    np.testing.assert_array_equal(out[1], out[4])
+
+
+def test_launcher_env_mapping():
+    from grayscott_amd.parallel.dist import launcher_env
+    assert launcher_env({}) == (0, 1, 0)
+    assert launcher_env({"PMI_RANK": "3", "PMI_SIZE": "4", "MPI_LOCALRANKID": "1"}) == (3, 4, 1)
+    assert launcher_env({"OMPI_COMM_WORLD_RANK": "2", "OMPI_COMM_WORLD_SIZE": "8"}) == (2, 8, 2)
+    assert launcher_env({"SLURM_PROCID": "5", "SLURM_NTASKS": "8", "SLURM_LOCALID": "5",
+                         "RANK": "1", "WORLD_SIZE": "2"}) == (1, 2, 1)
+
+
 def test_tuned_decomposition_run(tmp_path):
     """decomposition = "tune": the data path is self-checked and timed before the run, and the
     output equals a one-rank run."""
