@@ -534,7 +534,11 @@ struct FusedLaunch {
       const int64_t M = std::max<int64_t>(1, slots / 8);
       int best = 1;
       int64_t bcost = INT64_MAX;
-      const int maxch = std::max(1, a.nzv / (2 * C::TL + 2));
+      // chunks of >= 2 planes: small sub-domains (one round) trade pipeline fill for
+      // parallelism -- L=64 at T=2: 10.4 -> 6.8 us/step; large ones are set by the rounds
+      // (profiles/r1_tune_chunking.txt).  GS_FUSED_CHDIV overrides the divisor.
+      static const int chdiv = getenv("GS_FUSED_CHDIV") ? atoi(getenv("GS_FUSED_CHDIV")) : 2;
+      const int maxch = std::max(1, a.nzv / std::max(1, chdiv));
       for (int nch = 1; nch <= maxch; ++nch) {
         const int64_t per = ((int64_t)a.ntiles * nch + 7) / 8;
         const int64_t rounds = (per + M - 1) / M;
