@@ -102,3 +102,28 @@ def test_gpu_halo_poisoning(world, L, fuse, decomp, overlap):
     assert np.isfinite(un).all() and np.isfinite(vn).all()
     np.testing.assert_array_equal(un, u1)
     np.testing.assert_array_equal(vn, v1)
+
+
+def test_gpu_bench_two_ranks_tunes_data_path():
+    """bench.py under torchrun with 2 ranks on the one GPU (host transport: RCCL refuses two
+    ranks on one device): every candidate data path is self-checked and timed, the JSON line
+    reports the table, and the timed run uses the winner."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    from .mp_utils import ROOT, free_port
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "bench.py",
+           "--gpus", "2", "--L", "96", "--steps", "24", "--warmup", "6", "--transport", "host"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    tab = d["data_path_tuning"]
+    assert len(tab) >= 3 and all(row["ok"] for row in tab)
+    best = min(tab, key=lambda row: row["ms_per_step"])
+    assert d["config"]["dims"] == best["dims"] and d["config"]["fuse_steps"] == best["fuse"]
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["check"]["finite"]
