@@ -2,6 +2,7 @@
 #   make            -> grayscott_amd/_lib/libgs_core.so (CPU/OpenMP backend, BP4 I/O)
 #                      grayscott_amd/_lib/libgs_hip.so  (gfx950 kernels + RCCL transport)
 #   make selftest   -> build/bin/core_selftest (threads-as-ranks runtime self-test)
+#   make tools      -> build/bin/ubench_valu (gfx950 VALU issue-rate micro-benchmark)
 #   make asan/tsan  -> the same self-test under AddressSanitizer+UBSan / ThreadSanitizer (host
 #                      code only: GPU sanitizers are not available on the MI355X pool)
 ROCM     ?= /opt/rocm
@@ -45,6 +46,13 @@ build/tsan/core_selftest: $(SELFTEST_SRC) $(HDRS)
 	@mkdir -p build/tsan
 	$(CXX) -O1 -g -std=c++17 -Wno-unknown-pragmas -fsanitize=thread $(INC) -o $@ $(SELFTEST_SRC) -lpthread
 
+# VALU issue-rate micro-benchmark (profiles/r1_ubench_valu.txt)
+build/bin/ubench_valu: csrc/tools/ubench_valu.hip
+	@mkdir -p build/bin
+	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -o $@ $<
+
+tools: build/bin/ubench_valu
+
 selftest: build/bin/core_selftest
 	build/bin/core_selftest $(SELFTEST_TMP)
 asan: build/asan/core_selftest
@@ -56,4 +64,4 @@ clean:
 	rm -f $(OUT)/*.so
 	rm -rf build
 
-.PHONY: all clean selftest asan tsan
+.PHONY: all clean selftest asan tsan tools
