@@ -164,7 +164,8 @@ struct FCfg {
   // ablation (timing experiments only, results are WRONG): bit0 = no workgroup barriers,
   // bit1 = every level-0 load reads plane 0 (L2-resident); bit2 (results exact) = hoistable
   // Philox key schedule (the pre-noise_block_dev code generation); bit3 (results exact) =
-  // hoistable step words in the Philox counter (before the opaque-step change)
+  // hoistable step words in the Philox counter (before the opaque-step change); bit4 (exact) =
+  // float2 LDS reads split by the compiler into two ds_read_b32 (before lds_load2)
   static constexpr int ABL = ABL_;
   static constexpr int R = PF + 2;                    // level-0 ring slots
   static constexpr int NS = SKEW ? 3 : 2;             // level-l output ring / xch buffers
@@ -195,6 +196,14 @@ __device__ __forceinline__ int64_t gwrap(int64_t v, int64_t L) {
   if constexpr (C::PERIODIC) return wrap(v, L);
   else return v;
 }
+
+// One (u, v) pair from LDS as a single 8-byte ds_read_b64 (the compiler otherwise splits a
+// float2 into two ds_read_b32 at an 8-byte lane stride: 2-way bank conflicts).
+__device__ __forceinline__ float2 lds_load2(const float2* p) {
+  const uint64_t b = *reinterpret_cast<const uint64_t*>(__builtin_assume_aligned(p, 8));
+  return make_float2(__uint_as_float((uint32_t)b), __uint_as_float((uint32_t)(b >> 32)));
+}
+__device__ __forceinline__ double2 lds_load2(const double2* p) { return *p; }
 
 // One pipeline iteration p (i = p - pstart).  IR = i % R, IS = i % NS.
 // Non-skewed: level l+1 is computed from level l of the SAME iteration (one barrier per level).
@@ -243,8 +252,14 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
       xch[l][IS][sg.wave][1][sg.lane] = in[ROWS - 1];
       if constexpr (!(C::ABL & 1)) __syncthreads();
     }
-    const V2 up = sg.wave > 0 ? xch[l][IS][sg.wave - 1][1][sg.lane] : in[0];
-    const V2 dn = sg.wave < WAVES - 1 ? xch[l][IS][sg.wave + 1][0][sg.lane] : in[ROWS - 1];
+    V2 up, dn;
+    if constexpr (C::ABL & 16) {  // ablation: the compiler's split float2 LDS reads
+      up = sg.wave > 0 ? xch[l][IS][sg.wave - 1][1][sg.lane] : in[0];
+      dn = sg.wave < WAVES - 1 ? xch[l][IS][sg.wave + 1][0][sg.lane] : in[ROWS - 1];
+    } else {
+      up = sg.wave > 0 ? lds_load2(&xch[l][IS][sg.wave - 1][1][sg.lane]) : in[0];
+      dn = sg.wave < WAVES - 1 ? lds_load2(&xch[l][IS][sg.wave + 1][0][sg.lane]) : in[ROWS - 1];
+    }
     const int q = C::SKEW ? p - (2 * l + 1) : p - l - 1;  // plane produced by level l+1
     const int64_t gz = gwrap<C>(g.oz + q, g.Lz);
     const uint64_t tstep = (uint64_t)(a.t + l);
@@ -572,7 +587,8 @@ inline const char* const* fused_cfg_names(int* n) {
                                 "8x4:4s", "4x8:1s", "4x8:4s", "abl1",   "abl2",    "abl3",
                                 "4x8:1w4", "4x16:1", "4x16:2w4", "4x8:2w3", "abl4", "4x8:1abl4",
                                 "4x12:2s", "4x12:1s", "4x6:2s", "4x12:1", "4x12:1s-abl1",
-                                "4x12:1s-abl2", "4x12:1s-abl8", "4x12:2s-abl8"};
+                                "4x12:1s-abl2", "4x12:1s-abl8", "4x12:2s-abl8", "4x12:1s-abl16",
+                                "4x12:2s-abl16"};
   *n = (int)(sizeof(names) / sizeof(names[0]));
   return names;
 }
@@ -653,6 +669,8 @@ void run_fused_cfg(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, c
       case 35: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, 1, true, 2>, T>::run(s, d, a, p, st); return;
       case 36: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, 1, true, 8>, T>::run(s, d, a, p, st); return;
       case 37: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, 1, true, 8>, T>::run(s, d, a, p, st); return;
+      case 38: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, 1, true, 16>, T>::run(s, d, a, p, st); return;
+      case 39: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, 1, true, 16>, T>::run(s, d, a, p, st); return;
       default: break;
     }
   }

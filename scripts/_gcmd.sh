@@ -1,8 +1,6 @@
 set -e
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest -x -v --timeout 500 --timeout-method thread tests/test_gpu_multirank.py -k bench_two_ranks > gpurun_out/t_bench2.log 2>&1 || { tail -30 gpurun_out/t_bench2.log; exit 1; }
-tail -2 gpurun_out/t_bench2.log
-timeout -k 10 300 python bench.py --L 1024 --steps 60 --warmup 6 > gpurun_out/b1024f32.json 2>/dev/null
-timeout -k 10 300 python bench.py --L 1024 --precision Float64 --steps 40 --warmup 4 > gpurun_out/b1024f64.json 2>/dev/null
-timeout -k 10 300 python bench.py --L 512 --precision Float64 --steps 100 --warmup 10 > gpurun_out/b512f64.json 2>/dev/null
-for f in b1024f32 b1024f64 b512f64; do python -c "import json; d=json.load(open('gpurun_out/$f.json')); print('$f', d['value'], d['ms_per_step'], d['config']['fuse_steps'], d['config']['fused_kernel'])"; done
+timeout -k 10 400 python scripts/tune_inproc.py --L 512 --fuse 3 --cfg 4x12:1s 4x12:1s-abl16 --sched 2 --rounds 6 > gpurun_out/ab_lds64.txt 2>&1
+timeout -k 10 300 python scripts/tune_inproc.py --L 256 --fuse 2 --cfg 4x12:2s 4x12:2s-abl16 4x8:1 --sched 1 --rounds 6 >> gpurun_out/ab_lds64.txt 2>&1
+timeout -k 10 300 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_kernels.py -k "fused_tuning_configs_agree or fused_passes" >> gpurun_out/ab_lds64.txt 2>&1
+grep -E "median|passed|failed" gpurun_out/ab_lds64.txt
