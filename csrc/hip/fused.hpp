@@ -78,6 +78,19 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const void* base, i
                                            0x00020000);
 }
 
+// Descriptor for storage plane `plane` (0-based, ghosts included) of a buffer of `nplanes`
+// planes of `pzb` bytes, covering that plane only.  All the checks are 32-bit and wave-uniform
+// (SALU); the 64-bit form above needs VALU compares.  Accesses past the plane's end -- tile
+// rows beyond the ghost layer -- read 0 instead of the next plane's data: neither ever reaches
+// a stored output (an output depends on rows within T <= H of it).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc_p(const void* base, int plane,
+                                                               int nplanes, int64_t pzb, bool on) {
+  const bool inside = on && (unsigned)plane < (unsigned)nplanes;
+  const int nrec = inside ? (int)(pzb > 0x7ffffff0LL ? 0x7ffffff0LL : pzb) : 0;
+  return __builtin_amdgcn_make_buffer_rsrc(
+      (void*)((const char*)base + (int64_t)(inside ? plane : 0) * pzb), 0, nrec, 0x00020000);
+}
+
 __device__ __forceinline__ float2 bload(__amdgpu_buffer_rsrc_t r, int voff, int soff, float2*) {
   const gs_u2 v = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
   return make_float2(__uint_as_float(v.x), __uint_as_float(v.y));
@@ -165,7 +178,8 @@ struct FCfg {
   // bit1 = every level-0 load reads plane 0 (L2-resident); bit2 (results exact) = hoistable
   // Philox key schedule (the pre-noise_block_dev code generation); bit3 (results exact) =
   // hoistable step words in the Philox counter (before the opaque-step change); bit4 (exact) =
-  // float2 LDS reads split by the compiler into two ds_read_b32 (before lds_load2)
+  // float2 LDS reads split by the compiler into two ds_read_b32 (before lds_load2); bit5
+  // (exact) = 64-bit buffer-range descriptors (before plane_rsrc_p)
   static constexpr int ABL = ABL_;
   static constexpr int R = PF + 2;                    // level-0 ring slots
   static constexpr int NS = SKEW ? 3 : 2;             // level-l output ring / xch buffers
@@ -226,7 +240,9 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
   {
     const bool pf_ok = p + C::PF < sg.ldend;
     const __amdgpu_buffer_rsrc_t r =
-        plane_rsrc(src, (C::ABL & 2) ? 0 : (int64_t)(p + C::PF + g.H) * PZB, pf_ok ? a.buf_bytes : 0);
+        (C::ABL & 32) ? plane_rsrc(src, (C::ABL & 2) ? 0 : (int64_t)(p + C::PF + g.H) * PZB,
+                                   pf_ok ? a.buf_bytes : 0)
+                      : plane_rsrc_p(src, (C::ABL & 2) ? 0 : p + C::PF + g.H, g.pz, PZB, pf_ok);
 #pragma unroll
     for (int j = 0; j < ROWS; ++j)
       S.LD[(IR + C::PF) % C::R][j] = bload(r, sg.voff + j * sg.pitchb, 0, (V2*)nullptr);
@@ -316,7 +332,8 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
       {  // unconditional stores: planes before the segment go to an empty descriptor
         const bool st_ok = q >= sg.z0;
         const __amdgpu_buffer_rsrc_t w =
-            plane_rsrc(dst, (int64_t)(q + g.H) * PZB, st_ok ? a.buf_bytes : 0);
+            (C::ABL & 32) ? plane_rsrc(dst, (int64_t)(q + g.H) * PZB, st_ok ? a.buf_bytes : 0)
+                          : plane_rsrc_p(dst, q + g.H, g.pz, PZB, st_ok);
 #pragma unroll
         for (int j = 0; j < ROWS; ++j) {
           const int off = (j >= sg.srow0 && j < sg.srow1) ? sg.svoff + j * sg.pitchb : (int)0x80000000;
@@ -466,8 +483,8 @@ __global__ __launch_bounds__(64 * C::WAVES, C::MINW) void k_fused(const typename
   #pragma unroll
       for (int k = 0; k < C::PF; ++k) {
         {
-          const __amdgpu_buffer_rsrc_t r = plane_rsrc(
-              s, (int64_t)(sg.p + k + g.H) * PZB, sg.p + k < sg.ldend ? a.buf_bytes : 0);
+          const __amdgpu_buffer_rsrc_t r = plane_rsrc_p(s, sg.p + k + g.H, g.pz, PZB,
+                                                        sg.p + k < sg.ldend);
   #pragma unroll
           for (int j = 0; j < ROWS; ++j) S.LD[k][j] = bload(r, sg.voff + j * sg.pitchb, 0, (V2*)nullptr);
         }
@@ -588,7 +605,7 @@ inline const char* const* fused_cfg_names(int* n) {
                                 "4x8:1w4", "4x16:1", "4x16:2w4", "4x8:2w3", "abl4", "4x8:1abl4",
                                 "4x12:2s", "4x12:1s", "4x6:2s", "4x12:1", "4x12:1s-abl1",
                                 "4x12:1s-abl2", "4x12:1s-abl8", "4x12:2s-abl8", "4x12:1s-abl16",
-                                "4x12:2s-abl16"};
+                                "4x12:2s-abl16", "4x12:1s-abl32"};
   *n = (int)(sizeof(names) / sizeof(names[0]));
   return names;
 }
@@ -671,6 +688,7 @@ void run_fused_cfg(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, c
       case 37: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, 1, true, 8>, T>::run(s, d, a, p, st); return;
       case 38: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, 1, true, 16>, T>::run(s, d, a, p, st); return;
       case 39: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, 1, true, 16>, T>::run(s, d, a, p, st); return;
+      case 40: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, 1, true, 32>, T>::run(s, d, a, p, st); return;
       default: break;
     }
   }
