@@ -1,5 +1,8 @@
 set -e
 mkdir -p gpurun_out
-timeout -k 10 400 python scripts/tune_inproc.py --L 512 --fuse 3 --cfg 4x12:1s 4x12:1s-abl32 4x12:1s-abl16 --sched 2 --rounds 6 > gpurun_out/ab_rsrc.txt 2>&1
-timeout -k 10 400 python scripts/tune_inproc.py --L 256 --fuse 2 --cfg 4x12:2s 4x12:2s-abl16 --sched 1 --rounds 6 >> gpurun_out/ab_rsrc.txt 2>&1
-grep -E "median|passed|failed" gpurun_out/ab_rsrc.txt
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { tail -40 gpurun_out/gpu_tests.log; exit 1; }
+tail -2 gpurun_out/gpu_tests.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+tail -1 gpurun_out/smoke.log
+for i in 1 2; do timeout -k 10 300 python bench.py 2>/dev/null | cut -c1-200; done
+timeout -k 10 300 python bench.py --L 256 --steps 1000 --warmup 50 2>/dev/null | cut -c1-200
