@@ -61,21 +61,46 @@ def parse_arguments(args: Sequence[str]) -> Dict[str, object]:
             "output_inputdata": ns.output_inputdata, "follow": ns.follow, "timeout": ns.timeout}
 
 
-def compute_pdf(data: np.ndarray, nbins: int, vmin: float, vmax: float) -> Tuple[np.ndarray, np.ndarray]:
-    """Per-slice histograms of ``data`` (count, ny, nx) -> (pdf[count, nbins], bins[nbins])."""
-    count = data.shape[0]
+def compute_pdf(data, nbins: int, vmin: float, vmax: float,
+                device: Optional[str] = None) -> Tuple[np.ndarray, np.ndarray]:
+    """Per-slice histograms of ``data`` (count, ny, nx) -> (pdf[count, nbins], bins[nbins]).
+
+    Bin index = floor((x - vmin) / width) in float64, clamped to [0, nbins) (a value equal to
+    max lands in the last bin).  ``device="cuda"`` (default when a GPU is visible) bins on the
+    MI355X: one float64 index pass + one ``bincount`` over (slice, bin) -- an L=512 step is a
+    few ms instead of seconds; the counts are identical to the host path."""
+    count = int(data.shape[0])
     slice_size = int(np.prod(data.shape[1:]))
     bin_width = (vmax - vmin) / nbins
     bins = vmin + bin_width * np.arange(nbins, dtype=np.float64)
     if nbins == 1 or _epsilon(vmax - vmin) or _epsilon(abs(bin_width)):
         return np.full((count, nbins), float(slice_size)), bins
-    flat = data.reshape(count, slice_size).astype(np.float64)
+    if device is None:
+        device = _default_device()
+    if device != "cpu":
+        import torch
+        t = torch.as_tensor(np.ascontiguousarray(data)).to(device)
+        flat = t.reshape(count, slice_size).to(torch.float64)
+        idx = torch.floor((flat - vmin) / bin_width).to(torch.int64).clamp_(0, nbins - 1)
+        idx += torch.arange(count, device=device, dtype=torch.int64).unsqueeze(1) * nbins
+        pdf = torch.bincount(idx.reshape(-1), minlength=count * nbins)
+        return pdf.reshape(count, nbins).to(torch.float64).cpu().numpy(), bins
+    flat = np.asarray(data).reshape(count, slice_size).astype(np.float64)
     idx = np.floor((flat - vmin) / bin_width).astype(np.int64)
-    np.clip(idx, 0, nbins - 1, out=idx)  # value == max -> last bin; outliers clamp
-    pdf = np.zeros((count, nbins), dtype=np.float64)
-    rows = np.repeat(np.arange(count), slice_size)
-    np.add.at(pdf, (rows, idx.ravel()), 1.0)
-    return pdf, bins
+    np.clip(idx, 0, nbins - 1, out=idx)
+    idx += (np.arange(count, dtype=np.int64) * nbins)[:, None]
+    pdf = np.bincount(idx.ravel(), minlength=count * nbins).astype(np.float64)
+    return pdf.reshape(count, nbins), bins
+
+
+def _default_device() -> str:
+    if os.environ.get("GS_PDF_DEVICE"):
+        return os.environ["GS_PDF_DEVICE"]
+    try:
+        import torch
+        return "cuda" if torch.cuda.is_available() else "cpu"
+    except Exception:  # pragma: no cover
+        return "cpu"
 
 
 def _split_z(nz: int, rank: int, size: int) -> Tuple[int, int]:

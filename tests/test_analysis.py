@@ -91,3 +91,35 @@ def test_plot_and_listing_tools(sim_file, tmp_path):
     fb, shape = pdecomp.blocks_from_file(sim_file)
     assert shape == (16, 16, 16) and fb[0]["count_xyz"] == (16, 16, 16)
     assert pdecomp.main(["12", "4", "--png", str(tmp_path / "d.png")]) == 0
+
+
+def _pdf_add_at(data, nbins, vmin, vmax):
+    """The original scatter formulation (np.add.at) as an independent reference."""
+    count = data.shape[0]
+    w = (vmax - vmin) / nbins
+    flat = data.reshape(count, -1).astype(np.float64)
+    idx = np.clip(np.floor((flat - vmin) / w).astype(np.int64), 0, nbins - 1)
+    pdf = np.zeros((count, nbins))
+    np.add.at(pdf, (np.repeat(np.arange(count), flat.shape[1]), idx.ravel()), 1.0)
+    return pdf
+
+
+def test_compute_pdf_bincount_matches_scatter():
+    rng = np.random.default_rng(3)
+    data = rng.random((5, 9, 7)).astype(np.float32)
+    data[0, 0, 0] = 1.0  # the max lands in the last bin
+    pdf, _ = compute_pdf(data, 13, 0.0, 1.0, device="cpu")
+    np.testing.assert_array_equal(pdf, _pdf_add_at(data, 13, 0.0, 1.0))
+
+
+@pytest.mark.gpu
+def test_compute_pdf_on_gpu_matches_host():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    rng = np.random.default_rng(4)
+    data = rng.random((16, 64, 64)).astype(np.float32)
+    a, ba = compute_pdf(data, 100, float(data.min()), float(data.max()), device="cuda")
+    b, bb = compute_pdf(data, 100, float(data.min()), float(data.max()), device="cpu")
+    np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(ba, bb)
