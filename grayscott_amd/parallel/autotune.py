@@ -118,7 +118,7 @@ def time_data_path(settings, ctx, L: int, dims, fuse: int, steps: int = 30, warm
 
 def tune_data_path(settings, ctx, L: int, backend: str,
                    cands: Optional[Sequence[Tuple]] = None,
-                   steps: int = 30, warmup: int = 6, log=None) -> Dict:
+                   steps: int = 120, warmup: int = 12, log=None) -> Dict:
     """Self-check and time every candidate ``(dims, fuse[, overlap])``; returns ``{"dims",
     "fuse", "transport", "overlap", "inplace_halos", "table"}`` for the fastest correct one
     (identical on every rank)."""
