@@ -113,7 +113,7 @@ class Engine {
   int64_t step() const { return t_; }
   void set_step(int64_t t) { t_ = t; bc_parity_[0] = bc_parity_[1] = -1; }
   void set_transport(TransportFn fn, void* user) { tfn_ = fn; tuser_ = user; }
-  // comm/compute overlap: -1 auto (on when the plan is zplanes and a comm stream exists),
+  // comm/compute overlap: -1 auto (on with a device transport and a comm stream),
   // 0 off, 1 on where possible
   void set_overlap(int mode) { overlap_ = mode; }
   // Loopback (tests): periodic wraps onto this rank travel through the device transport
@@ -128,8 +128,10 @@ class Engine {
   }
   // whether a pass of k steps runs with the halo exchange overlapped with the inner update:
   // z-slab plans (in-place planes) split z only; packed plans split z and the x-y tile grid
+  // ("auto" only with a device transport: a host callback transport serialises anyway)
   bool overlapped(int k) const {
-    return overlap_ != 0 && cfg_.use_fused && k > 1 && has_remote_ && be_->has_comm_stream() &&
+    return (overlap_ == 1 || (overlap_ == -1 && tfn_ == nullptr)) && cfg_.use_fused && k > 1 &&
+           has_remote_ && be_->has_comm_stream() &&
            be_->fused_supported(k) && cfg_.g.nz >= 2 * k + 1;
   }
   double comm_calls() const { return (double)ncomm_; }
