@@ -114,23 +114,28 @@ class HipBackend final : public gs::Backend {
     if (!gsk::fused_supported(g_, n)) return false;
     if (!tuned_[n]) autotune(src, dst, n, t);
     const bool pin = fused_pinned();
-    // the post-exchange parts of an overlapped pass (z end slabs, ring tiles) are short,
-    // latency-bound launches: they get their own tuned tile shape / schedule
-    const int kind = leave_room ? 0 : (tiles == 2 ? 2 : (zlen1 > 0 ? 1 : 0));
+    // the post-exchange parts of an overlapped pass (z end slabs: kind 1, ring tiles: kind 2)
+    // are short, latency-bound launches: they get their own tuned tile shape / schedule
+    const int kind = leave_room ? 0 : (tiles == 2 ? 2 : 1);
     int c = cfg_[n], sc = sched_[n];
     if (kind && !pin) {
-      const int slot = n + 4 * kind;
-      if (!part_tuned_[slot]) {
-        part_tuned_[slot] = true;
-        const Part pt{zlo0, zlen0, zlo1, zlen1, tiles, sides};
+      const Part pt{zlo0, zlen0, zlo1, zlen1, tiles, sides};
+      PartChoice* pc = nullptr;
+      for (PartChoice& q : parts_)
+        if (q.n == n && q.pt.zlo0 == pt.zlo0 && q.pt.zlen0 == pt.zlen0 && q.pt.zlo1 == pt.zlo1 &&
+            q.pt.zlen1 == pt.zlen1 && q.pt.tiles == pt.tiles && q.pt.sides == pt.sides)
+          pc = &q;
+      if (!pc) {
+        parts_.push_back(PartChoice{n, pt, cfg_[n], sched_[n]});
+        pc = &parts_.back();
         float ms = 0.f;
-        if (!autotune_part(src, dst, n, t, pt, &part_cfg_[slot], &part_sched_[slot], &ms)) {
-          part_cfg_[slot] = cfg_[n];
-          part_sched_[slot] = sched_[n];
+        if (!autotune_part(src, dst, n, t, pt, &pc->cfg, &pc->sched, &ms)) {
+          pc->cfg = cfg_[n];
+          pc->sched = sched_[n];
         }
       }
-      c = part_cfg_[slot];
-      sc = part_sched_[slot];
+      c = pc->cfg;
+      sc = pc->sched;
     }
     const bool ok = gsk::launch_fused<T>(buf_[src], buf_[dst], g_, p_, n, t, stream_,
                                          pin ? -1 : c, pin ? -1 : sc, zlo0, zlen0,
@@ -380,11 +385,13 @@ class HipBackend final : public gs::Backend {
   int cfg_[4] = {-1, -1, -1, -1};
   int sched_[4] = {-1, -1, -1, -1};
   float tuned_ms_[4] = {0.f, 0.f, 0.f, 0.f};
-  // tuned shapes of the overlapped passes' post-exchange parts: slot n + 4 * kind
-  // (kind 1: the two z end slabs, kind 2: the ring tiles)
-  bool part_tuned_[12] = {};
-  int part_cfg_[12] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
-  int part_sched_[12] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+  // tuned shapes of the overlapped passes' post-exchange parts (one entry per launch shape)
+  struct PartChoice {
+    int n;
+    Part pt;
+    int cfg, sched;
+  };
+  std::vector<PartChoice> parts_;
 };
 
 }  // namespace

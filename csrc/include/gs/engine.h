@@ -253,11 +253,12 @@ class Engine {
         be_->comm_select(true);
         exchange_start();
         be_->comm_select(false);
-        // packed plans: the inner box is clear of every face with a neighbour (z by planes,
-        // x / y by whole tiles); z-slab plans keep all tiles and split z only
+        // the inner box is clear of every face with a neighbour (z by planes, x / y by whole
+        // tiles; z-slab plans split z only); a face without one (global boundary) needs no
+        // halo, so its end slab joins the inner part
         const int* nb = cfg_.nbr;
-        const bool zm = plan_.zplanes || nb[dir_index(0, 0, -1)] >= 0;
-        const bool zp = plan_.zplanes || nb[dir_index(0, 0, 1)] >= 0;
+        const bool zm = nb[dir_index(0, 0, -1)] >= 0;
+        const bool zp = nb[dir_index(0, 0, 1)] >= 0;
         const int z0 = zm ? k : 0, z1 = zp ? nz - k : nz;
         const int sides = plan_.zplanes ? 0
             : (nb[dir_index(-1, 0, 0)] >= 0 ? 1 : 0) | (nb[dir_index(1, 0, 0)] >= 0 ? 2 : 0) |
