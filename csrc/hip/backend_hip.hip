@@ -114,9 +114,12 @@ class HipBackend final : public gs::Backend {
     if (!gsk::fused_supported(g_, n)) return false;
     if (!tuned_[n]) autotune(src, dst, n, t);
     const bool pin = fused_pinned();
+    // launched on the selected stream (comm_select): the ring tiles of a packed pass run on the
+    // comm stream next to the z end slabs on the compute stream.
     // the post-exchange parts of an overlapped pass (z end slabs: kind 1, ring tiles: kind 2)
     // are short, latency-bound launches: they get their own tuned tile shape / schedule
-    const int kind = leave_room ? 0 : (tiles == 2 ? 2 : 1);
+    // (an inner-tiles launch always keeps the whole-domain shape its ring complements)
+    const int kind = (leave_room || tiles == 1) ? 0 : (tiles == 2 ? 2 : 1);
     int c = cfg_[n], sc = sched_[n];
     if (kind && !pin) {
       const Part pt{zlo0, zlen0, zlo1, zlen1, tiles, sides};
@@ -129,7 +132,10 @@ class HipBackend final : public gs::Backend {
         parts_.push_back(PartChoice{n, pt, cfg_[n], sched_[n]});
         pc = &parts_.back();
         float ms = 0.f;
-        if (!autotune_part(src, dst, n, t, pt, &pc->cfg, &pc->sched, &ms)) {
+        // the ring tiles are the complement of the inner launch's tile rectangle, which
+        // depends on the tile shape: keep the inner (whole-domain) shape, tune the schedule
+        const int fixed = kind == 2 ? std::max(cfg_[n], 0) : -1;
+        if (!autotune_part(src, dst, n, t, pt, &pc->cfg, &pc->sched, &ms, fixed)) {
           pc->cfg = cfg_[n];
           pc->sched = sched_[n];
         }
@@ -137,7 +143,7 @@ class HipBackend final : public gs::Backend {
       c = pc->cfg;
       sc = pc->sched;
     }
-    const bool ok = gsk::launch_fused<T>(buf_[src], buf_[dst], g_, p_, n, t, stream_,
+    const bool ok = gsk::launch_fused<T>(buf_[src], buf_[dst], g_, p_, n, t, xs_,
                                          pin ? -1 : c, pin ? -1 : sc, zlo0, zlen0,
                                          zlo1, zlen1, leave_room ? reserve_ : 0, tiles, sides);
     if (!ok) throw std::runtime_error("fused_runs: invalid z-runs");
@@ -196,14 +202,17 @@ class HipBackend final : public gs::Backend {
              fused_pinned());
   }
   // best {cfg, sched} for one launch shape; false if tuning is disabled / unsupported
+  // fixed_cfg >= 0 keeps the tile shape and tunes the schedule only (a ring launch must use
+  // the tile grid of the inner launch it complements)
   bool autotune_part(int src, int dst, int n, int64_t t, const Part& pt, int* cfg, int* sched,
-                     float* ms_best) {
+                     float* ms_best, int fixed_cfg = -1) {
     if (!autotune_enabled()) return false;
     struct Cand { int cfg, sched; };
     std::vector<Cand> cands;
     const bool variants = !g_.periodic && p_.noise != 0.0;  // tile variants instantiated here
     std::vector<int> cfgs;
-    if (!variants) cfgs = {0};
+    if (fixed_cfg >= 0) cfgs = {fixed_cfg};
+    else if (!variants) cfgs = {0};
     else if (sizeof(T) == 4) cfgs = {0, 1, 2, 3, 5, 8, 12, 16, 17, 19, 20, 30, 31, 33};
     else cfgs = {0, 1, 13, 15, 19, 32, 33};
     const int nsched = pt.zlen1 > 0 ? 1 : 3;  // two z-runs always use schedule 0

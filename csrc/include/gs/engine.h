@@ -153,7 +153,12 @@ class Engine {
   // Tune every fused depth this engine can use, without changing the state.
   void prepare() {
     if (!cfg_.use_fused) return;
-    for (int n = 2; n <= cfg_.fuse; ++n) be_->prepare_fused(cur_, 1 - cur_, n, t_);
+    for (int n = 2; n <= cfg_.fuse; ++n) {
+      be_->prepare_fused(cur_, 1 - cur_, n, t_);
+      // tune the overlapped passes' post-exchange launches now too (their first call times
+      // the candidates), so no tuning lands inside a timed region; all on the compute stream
+      if (overlapped(n)) shell_runs(cur_, 1 - cur_, n, t_, overlap_split(n), false);
+    }
     // the timing runs scribbled over the other buffer: restore the reference's zeroed
     // u_temp/v_temp (ghosts included) so the ghost-parity bookkeeping stays exact
     const Geom& g = cfg_.g;
@@ -247,37 +252,24 @@ class Engine {
       if (overlapped(k)) {
         // Inner planes [k, nz-k) need no halo: run them while the exchange is in flight on
         // the comm stream, then the two k-plane boundary slabs once it has landed.
-        const int nz = cfg_.g.nz;
         ensure_bc(cur_, t_);  // before the fork: the exchanged planes carry these ghosts
         be_->comm_fork();
         be_->comm_select(true);
         exchange_start();
         be_->comm_select(false);
-        // the inner box is clear of every face with a neighbour (z by planes, x / y by whole
-        // tiles; z-slab plans split z only); a face without one (global boundary) needs no
-        // halo, so its end slab joins the inner part
-        const int* nb = cfg_.nbr;
-        const bool zm = nb[dir_index(0, 0, -1)] >= 0;
-        const bool zp = nb[dir_index(0, 0, 1)] >= 0;
-        const int z0 = zm ? k : 0, z1 = zp ? nz - k : nz;
-        const int sides = plan_.zplanes ? 0
-            : (nb[dir_index(-1, 0, 0)] >= 0 ? 1 : 0) | (nb[dir_index(1, 0, 0)] >= 0 ? 2 : 0) |
-              (nb[dir_index(0, -1, 0)] >= 0 ? 4 : 0) | (nb[dir_index(0, 1, 0)] >= 0 ? 8 : 0);
-        if (z1 > z0) {
+        const Split sp = overlap_split(k);
+        if (sp.z1 > sp.z0) {
           TraceRange tr("gs.fused_inner");
-          be_->fused_runs(cur_, oth, k, t_, z0, z1 - z0, 0, 0, true, sides ? 1 : 0, sides);
+          be_->fused_runs(cur_, oth, k, t_, sp.z0, sp.z1 - sp.z0, 0, 0, true,
+                          sp.sides ? 1 : 0, sp.sides);
         }
         be_->comm_select(true);
         exchange_finish(true);
         be_->comm_select(false);
-        be_->comm_join();
+        be_->comm_join();  // the compute stream sees the landed halos
         {
           TraceRange tr("gs.fused_shell");
-          // z end slabs over all tiles, then (packed plans) the ring tiles of the inner planes
-          const int la = z0, lb = nz - (z1 > z0 ? z1 : z0);
-          if (la > 0) be_->fused_runs(cur_, oth, k, t_, 0, la, nz - lb, lb);
-          else if (lb > 0) be_->fused_runs(cur_, oth, k, t_, nz - lb, lb, 0, 0);
-          if (sides && z1 > z0) be_->fused_runs(cur_, oth, k, t_, z0, z1 - z0, 0, 0, false, 2, sides);
+          shell_runs(cur_, oth, k, t_, sp, true);
         }
         cur_ = oth;
         t_ += k;
@@ -308,6 +300,42 @@ class Engine {
   }
 
  private:
+  // Split of an overlapped k-step pass.  The inner box [z0, z1) x (inner tiles) is clear of
+  // every face with a neighbour -- z by planes, x / y by whole tiles (z-slab plans split z
+  // only); a face without a neighbour (global boundary) needs no halo, so its end slab joins
+  // the inner part.
+  struct Split {
+    int z0, z1, sides;
+  };
+  Split overlap_split(int k) const {
+    const int nz = cfg_.g.nz;
+    const int32_t* nb = cfg_.nbr;
+    Split sp;
+    sp.z0 = nb[dir_index(0, 0, -1)] >= 0 ? k : 0;
+    sp.z1 = nb[dir_index(0, 0, 1)] >= 0 ? nz - k : nz;
+    sp.sides = plan_.zplanes ? 0
+        : (nb[dir_index(-1, 0, 0)] >= 0 ? 1 : 0) | (nb[dir_index(1, 0, 0)] >= 0 ? 2 : 0) |
+          (nb[dir_index(0, -1, 0)] >= 0 ? 4 : 0) | (nb[dir_index(0, 1, 0)] >= 0 ? 8 : 0);
+    return sp;
+  }
+  // The post-exchange launches of an overlapped pass: the z end slabs over all tiles and
+  // (packed plans) the ring tiles of the inner planes.  ring_on_comm: the ring runs on the comm
+  // stream in parallel with the end slabs on the compute stream -- two short, latency-bound
+  // launches side by side instead of back to back -- and the compute stream joins it.
+  void shell_runs(int src, int dst, int k, int64_t t, const Split& sp, bool ring_on_comm) {
+    const int nz = cfg_.g.nz;
+    const bool ring = sp.sides && sp.z1 > sp.z0;
+    if (ring) {
+      if (ring_on_comm) be_->comm_select(true);
+      be_->fused_runs(src, dst, k, t, sp.z0, sp.z1 - sp.z0, 0, 0, false, 2, sp.sides);
+      if (ring_on_comm) be_->comm_select(false);
+    }
+    const int la = sp.z0, lb = nz - (sp.z1 > sp.z0 ? sp.z1 : sp.z0);
+    if (la > 0) be_->fused_runs(src, dst, k, t, 0, la, nz - lb, lb);
+    else if (lb > 0) be_->fused_runs(src, dst, k, t, nz - lb, lb, 0, 0);
+    if (ring && ring_on_comm) be_->comm_join();
+  }
+
   EngineConfig cfg_;
   Backend* be_;
   HaloPlan plan_;

@@ -10,6 +10,7 @@ one-GPU box:
   over just two links;
 * the balanced ``MPI_Dims_create`` grid (2x2x2 on 8 GPUs): 4x less halo per link, spread over
   up to six links, but packed (pack / RCCL / unpack) and not overlapped;
+* ``1 x 2 x N/2``: z slabs split once along y -- half the plane bytes per link, one tile ring;
 * the fuse depth T (steps per exchange): the same bytes per step, fewer messages at larger T.
 
 ``tune_data_path`` first checks every candidate's exact data path against the golden model on
@@ -79,6 +80,10 @@ def candidates(L: int, nprocs: int, backend: str) -> List[Tuple[List[int], int, 
     if backend == "hip":
         add(bal, 0, "off")
         add(bal, 3)
+        # z slabs split once along y: half the z-plane bytes per link of the plain slabs, full
+        # 64-lane x tiles, and only one tile ring (the y face) outside the overlap
+        if nprocs >= 4 and nprocs % 2 == 0 and L // (nprocs // 2) >= 8:
+            add([1, 2, nprocs // 2], 0)
     return out
 
 

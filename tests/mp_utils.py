@@ -37,7 +37,7 @@ def _worker(rank, world, port, outdir, cfg):
         settings = Settings(**cfg["settings"])
         backend = "hip" if settings.backend.lower() in ("amdgpu", "hip", "gpu") else "cpu"
         ctx = gdist.init_from_env(backend)
-        dims = choose_dims(settings.L, world, settings.decomposition, backend)
+        dims = cfg.get("dims") or choose_dims(settings.L, world, settings.decomposition, backend)
         dom = init_domain(settings.L, world, rank, periodic=settings.periodic, dims=dims)
         sim = GrayScott(settings, dom, ctx, fuse=cfg.get("fuse"), transport=cfg.get("transport"),
                         use_fused=cfg.get("use_fused", True))

@@ -85,6 +85,21 @@ def test_gpu_balanced_overlap_matches_single_rank(world, L, fuse, prec, overlap)
     np.testing.assert_array_equal(vn, v1)
 
 
+@pytest.mark.parametrize("world,dims,L,fuse", [(4, [1, 2, 2], 64, 3), (8, [1, 2, 4], 64, 2)])
+def test_gpu_hybrid_slabs_overlap_matches_single_rank(world, dims, L, fuse):
+    """z slabs split along y (packed halos, one tile ring): overlapped passes with the ring
+    tiles on the comm stream next to the z end slabs -- bit-identical to one rank."""
+    steps = 11
+    u1, v1, _ = run_ranks(1, _cfg(L, steps, fuse))
+    cfg = _cfg(L, steps, fuse)
+    cfg["settings"].update(overlap="on")
+    cfg["dims"] = dims
+    un, vn, meta = run_ranks(world, cfg)
+    assert all(m["overlapped"] for m in meta)
+    np.testing.assert_array_equal(un, u1)
+    np.testing.assert_array_equal(vn, v1)
+
+
 @pytest.mark.parametrize("world,L,fuse,decomp,overlap", [
     (1, 40, 3, "balanced", "auto"),
     (4, 40, 2, "balanced", "auto"),
