@@ -161,7 +161,16 @@ def tune_data_path(settings, ctx, L: int, backend: str,
         s = copy.copy(settings)
         s.transport, s.overlap = chosen[0], chosen[1]
         with _inplace_env(chosen[2]):
-            el, ovd = time_data_path(s, ctx, L, dims, f, steps=steps, warmup=warmup)
+            try:
+                el, ovd = time_data_path(s, ctx, L, dims, f, steps=steps, warmup=warmup)
+                ran = 1.0
+            except Exception as ex:  # e.g. out of memory at the real size: skip this path
+                el, ovd, ran = float("inf"), False, 0.0
+                row["error"] = str(ex)[:200]
+        if ctx.allreduce(ran, "min") <= 0:
+            row.update(ok=False)
+            table.append(row)
+            continue
         row.update(ok=True, transport=chosen[0], overlap=chosen[1], overlapped=ovd,
                    inplace_halos=chosen[2] is None, ms_per_step=round(1e3 * el / steps, 4))
         table.append(row)
