@@ -64,6 +64,7 @@ class HipBackend final : public gs::Backend {
     HIP_CHECK(hipEventCreateWithFlags(&ev_, hipEventDisableTiming));
     HIP_CHECK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
     HIP_CHECK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
+    for (hipEvent_t& e : marks_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     // halo traffic on its own high-priority stream so it overlaps the inner-plane kernel
     int lo = 0, hi = 0;
     HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -76,6 +77,8 @@ class HipBackend final : public gs::Backend {
     if (ev_) (void)hipEventDestroy(ev_);
     if (ev_fork_) (void)hipEventDestroy(ev_fork_);
     if (ev_join_) (void)hipEventDestroy(ev_join_);
+    for (hipEvent_t e : marks_)
+      if (e) (void)hipEventDestroy(e);
     if (comm_stream_) (void)hipStreamDestroy(comm_stream_);
   }
 
@@ -161,6 +164,19 @@ class HipBackend final : public gs::Backend {
     HIP_CHECK(hipStreamWaitEvent(stream_, ev_join_, 0));
   }
   void comm_select(bool on) override { xs_ = on ? comm_stream_ : stream_; }
+  void mark(int which, bool on_comm) override {
+    HIP_CHECK(hipEventRecord(marks_[which & 3], on_comm ? comm_stream_ : stream_));
+  }
+  void wait_mark(int which, bool on_comm) override {
+    HIP_CHECK(hipStreamWaitEvent(on_comm ? comm_stream_ : stream_, marks_[which & 3], 0));
+  }
+  bool can_exchange_inplace(const gs::HaloPlan& p) const override {
+    if (!comm_ || !p.zplanes || inplace_off_) return false;
+    if (!loopback_)
+      for (int i = 0; i < p.nrecv; ++i)
+        if (p.recv[i].peer == rank_) return false;
+    return true;
+  }
 
   // zplanes plan: every message is a contiguous run of storage planes of buffer b, so RCCL
   // sends and receives them in place.  Same message order as the packed path (sends ascend
@@ -381,6 +397,7 @@ class HipBackend final : public gs::Backend {
   void* ws_ = nullptr;
   hipEvent_t ev_ = nullptr;
   hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
+  hipEvent_t marks_[4] = {nullptr, nullptr, nullptr, nullptr};
   hipStream_t comm_stream_ = nullptr;
   hipStream_t xs_ = nullptr;  // stream for halo traffic (compute or comm stream)
   // workgroup slots left free for RCCL while the inner-plane kernel runs (GS_OVERLAP_RESERVE)

@@ -11,6 +11,7 @@
 #pragma once
 
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 #include <stdexcept>
 #include <string>
@@ -62,6 +63,13 @@ class Backend {
   virtual void comm_fork() {}
   virtual void comm_join() {}
   virtual void comm_select(bool on) { (void)on; }
+  // event slots (0..3) for finer cross-stream ordering: mark records slot `which` on the comm
+  // (on_comm) or compute stream at this point; wait_mark makes that stream wait for the slot's
+  // last record
+  virtual void mark(int which, bool on_comm) { (void)which; (void)on_comm; }
+  virtual void wait_mark(int which, bool on_comm) { (void)which; (void)on_comm; }
+  // whether native_exchange_inplace would carry this plan (device transport, no self copies)
+  virtual bool can_exchange_inplace(const HaloPlan& p) const { (void)p; return false; }
   virtual void pack(int b, const HaloPlan& p) = 0;
   virtual void unpack(int b, const HaloPlan& p) = 0;
   // copy send-buffer cells [src_off, +n) to recv-buffer cells [dst_off, +n)
@@ -245,10 +253,21 @@ class Engine {
     bc_parity_[b] = par;
   }
 
+  // whether full-depth passes run as a chain on two streams (advance_chained)
+  bool chained(int k) const {
+    return chain_ && overlapped(k) && plan_.zplanes && be_->can_exchange_inplace(plan_);
+  }
+
   void advance(int64_t nsteps) {
     while (nsteps > 0) {
       const int k = (int)(nsteps < cfg_.fuse ? nsteps : cfg_.fuse);
       const int oth = 1 - cur_;
+      if (nsteps >= 2 * (int64_t)k && chained(k)) {
+        const int64_t npass = nsteps / k;
+        advance_chained(k, npass);
+        nsteps -= npass * k;
+        continue;
+      }
       if (overlapped(k)) {
         // Inner planes [k, nz-k) need no halo: run them while the exchange is in flight on
         // the comm stream, then the two k-plane boundary slabs once it has landed.
@@ -300,6 +319,48 @@ class Engine {
   }
 
  private:
+  // Chained overlapped passes for in-place plane halos (z slabs over RCCL).  The critical
+  // chain -- halo exchange of pass p, then its z end slabs, then the exchange of pass p+1 --
+  // stays on the comm stream with no cross-stream hop; the inner planes run on the compute
+  // stream.  Ordering (S = source, D = destination buffer of pass p):
+  //   comm:    exchange(S_p) -> [wait inner_{p-1}] -> end slabs S_p -> D_p -> mark 2
+  //   compute: [wait mark 2 = end slabs_{p-1}] -> inner S_p -> D_p -> mark p&1
+  // End slabs read S_p planes [-k, 2k): the halos (same stream), their own previous output
+  // (same stream) and inner_{p-1}'s planes (waited); they overwrite planes inner_{p-1} read.
+  // The inner part reads S_p = end slabs_{p-1} + inner_{p-1} and overwrites planes that
+  // end slabs_{p-1} read (waited).  The exchange writes only ghost planes and sends planes
+  // written by the previous end slabs.  Both buffers' outer ghosts are set before the chain
+  // (their time parities stay fixed through it), so no fill runs inside.
+  void advance_chained(int k, int64_t npass) {
+    const Split sp = overlap_split(k);
+    ensure_bc(cur_, t_);
+    ensure_bc(1 - cur_, t_ + k);
+    be_->comm_fork();
+    for (int64_t p = 0; p < npass; ++p) {
+      const int oth = 1 - cur_;
+      be_->comm_select(true);
+      exchange_start();  // in-place RCCL group on the comm stream
+      be_->comm_select(false);
+      if (p > 0) be_->wait_mark(2, false);
+      if (sp.z1 > sp.z0) {
+        TraceRange tr("gs.fused_inner");
+        be_->fused_runs(cur_, oth, k, t_, sp.z0, sp.z1 - sp.z0, 0, 0, true, 0, 0);
+      }
+      be_->mark((int)(p & 1), false);
+      if (p > 0) be_->wait_mark((int)((p - 1) & 1), true);
+      {
+        TraceRange tr("gs.fused_shell");
+        be_->comm_select(true);
+        shell_runs(cur_, oth, k, t_, sp, false);
+        be_->comm_select(false);
+      }
+      be_->mark(2, true);
+      cur_ = oth;
+      t_ += k;
+    }
+    be_->comm_join();
+  }
+
   // Split of an overlapped k-step pass.  The inner box [z0, z1) x (inner tiles) is clear of
   // every face with a neighbour -- z by planes, x / y by whole tiles (z-slab plans split z
   // only); a face without a neighbour (global boundary) needs no halo, so its end slab joins
@@ -343,6 +404,8 @@ class Engine {
   bool has_remote_ = false;
   int overlap_ = -1;
   bool loopback_ = false;
+  // GS_OVERLAP_CHAIN=0: run in-place overlapped passes one by one (A/B of advance_chained)
+  bool chain_ = !(getenv("GS_OVERLAP_CHAIN") && atoi(getenv("GS_OVERLAP_CHAIN")) == 0);
   enum { kNone, kUnpack, kCallback };
   int xpending_ = kNone;
   int cur_ = 0;
