@@ -1,11 +1,7 @@
 set -e
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_rccl_loopback.py > gpurun_out/lb.log 2>&1 || { tail -30 gpurun_out/lb.log; exit 1; }
-tail -1 gpurun_out/lb.log
-cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-rm -rf gpurun_out/ovl_z gpurun_out/ovl_z0
-timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/ovl_z -o run -- python3 scripts/trace_overlap.py --mode zplanes --L 512 --nz 64 > gpurun_out/ovl_z.log 2>&1
-GS_OVERLAP_CHAIN=0 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/ovl_z0 -o run -- python3 scripts/trace_overlap.py --mode zplanes --L 512 --nz 64 > gpurun_out/ovl_z0.log 2>&1
-python3 scripts/trace_overlap.py --summarise gpurun_out/ovl_z > gpurun_out/ovl_z.txt
-python3 scripts/trace_overlap.py --summarise gpurun_out/ovl_z0 > gpurun_out/ovl_z0.txt
-tail -8 gpurun_out/ovl_z.txt; tail -8 gpurun_out/ovl_z0.txt
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 500 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { tail -40 gpurun_out/gpu_tests.log; exit 1; }
+tail -2 gpurun_out/gpu_tests.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+tail -1 gpurun_out/smoke.log
+timeout -k 10 300 python bench.py 2>/dev/null | cut -c1-200
