@@ -170,6 +170,7 @@ class HipBackend final : public gs::Backend {
   void wait_mark(int which, bool on_comm) override {
     HIP_CHECK(hipStreamWaitEvent(on_comm ? comm_stream_ : stream_, marks_[which & 3], 0));
   }
+  bool has_native_transport() const override { return comm_ != nullptr; }
   bool can_exchange_inplace(const gs::HaloPlan& p) const override {
     if (!comm_ || !p.zplanes || inplace_off_) return false;
     if (!loopback_)

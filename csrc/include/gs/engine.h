@@ -70,6 +70,8 @@ class Backend {
   virtual void wait_mark(int which, bool on_comm) { (void)which; (void)on_comm; }
   // whether native_exchange_inplace would carry this plan (device transport, no self copies)
   virtual bool can_exchange_inplace(const HaloPlan& p) const { (void)p; return false; }
+  // whether native_exchange has a device transport (RCCL) configured
+  virtual bool has_native_transport() const { return false; }
   virtual void pack(int b, const HaloPlan& p) = 0;
   virtual void unpack(int b, const HaloPlan& p) = 0;
   // copy send-buffer cells [src_off, +n) to recv-buffer cells [dst_off, +n)
@@ -255,7 +257,8 @@ class Engine {
 
   // whether full-depth passes run as a chain on two streams (advance_chained)
   bool chained(int k) const {
-    return chain_ && overlapped(k) && plan_.zplanes && be_->can_exchange_inplace(plan_);
+    return chain_ && overlapped(k) && tfn_ == nullptr &&
+           (plan_.zplanes ? be_->can_exchange_inplace(plan_) : be_->has_native_transport());
   }
 
   void advance(int64_t nsteps) {
@@ -319,18 +322,20 @@ class Engine {
   }
 
  private:
-  // Chained overlapped passes for in-place plane halos (z slabs over RCCL).  The critical
-  // chain -- halo exchange of pass p, then its z end slabs, then the exchange of pass p+1 --
-  // stays on the comm stream with no cross-stream hop; the inner planes run on the compute
-  // stream.  Ordering (S = source, D = destination buffer of pass p):
-  //   comm:    exchange(S_p) -> [wait inner_{p-1}] -> end slabs S_p -> D_p -> mark 2
-  //   compute: [wait mark 2 = end slabs_{p-1}] -> inner S_p -> D_p -> mark p&1
-  // End slabs read S_p planes [-k, 2k): the halos (same stream), their own previous output
-  // (same stream) and inner_{p-1}'s planes (waited); they overwrite planes inner_{p-1} read.
-  // The inner part reads S_p = end slabs_{p-1} + inner_{p-1} and overwrites planes that
-  // end slabs_{p-1} read (waited).  The exchange writes only ghost planes and sends planes
-  // written by the previous end slabs.  Both buffers' outer ghosts are set before the chain
-  // (their time parities stay fixed through it), so no fill runs inside.
+  // Chained overlapped passes over a device transport (RCCL).  The critical chain -- halo
+  // exchange of pass p, then its post-exchange launches (z end slabs, ring tiles), then the
+  // exchange of pass p+1 -- stays on the comm stream with no cross-stream hop; the inner part
+  // runs on the compute stream.  Ordering (S = source, D = destination buffer of pass p):
+  //   comm:    exchange(S_p) -> [wait inner_{p-1}] -> shell S_p -> D_p -> mark 2
+  //   compute: [wait mark 2 = shell_{p-1}] -> inner S_p -> D_p -> mark p&1
+  // The shell reads S_p within k of the faces with neighbours: the halos (same stream), its
+  // own previous output (same stream) and inner_{p-1}'s cells (waited); it overwrites cells
+  // inner_{p-1} read.  The inner part reads S_p = shell_{p-1} + inner_{p-1} and overwrites
+  // cells that shell_{p-1} read (waited).  The exchange writes only ghost cells and sends
+  // (packs) cells within k of the faces -- all written by the previous shell, since inner
+  // outputs are at least k away from every face with a neighbour.  Both buffers' outer ghosts
+  // are set before the chain (their time parities stay fixed through it), so no fill runs
+  // inside.
   void advance_chained(int k, int64_t npass) {
     const Split sp = overlap_split(k);
     ensure_bc(cur_, t_);
@@ -339,12 +344,14 @@ class Engine {
     for (int64_t p = 0; p < npass; ++p) {
       const int oth = 1 - cur_;
       be_->comm_select(true);
-      exchange_start();  // in-place RCCL group on the comm stream
+      exchange_start();      // in-place RCCL group, or pack + RCCL group, on the comm stream
+      exchange_finish(true);  // (packed plans) unpack
       be_->comm_select(false);
       if (p > 0) be_->wait_mark(2, false);
       if (sp.z1 > sp.z0) {
         TraceRange tr("gs.fused_inner");
-        be_->fused_runs(cur_, oth, k, t_, sp.z0, sp.z1 - sp.z0, 0, 0, true, 0, 0);
+        be_->fused_runs(cur_, oth, k, t_, sp.z0, sp.z1 - sp.z0, 0, 0, true, sp.sides ? 1 : 0,
+                        sp.sides);
       }
       be_->mark((int)(p & 1), false);
       if (p > 0) be_->wait_mark((int)((p - 1) & 1), true);
