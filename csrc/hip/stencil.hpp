@@ -20,7 +20,8 @@
 
 // ------------------------------------------------------------------------------------------
 // DPP lane shifts.  shr: lane i receives lane i-1; shl: lane i receives lane i+1.
-// Lanes without a source receive 0 (they only ever feed tile-halo cells).
+// Lanes without a source receive 0 (they only ever feed tile-halo cells); bound_ctrl gives
+// that 0 without materialising an old-value register (one v_mov per shift otherwise).
 // ------------------------------------------------------------------------------------------
 __device__ __forceinline__ float lane_from_left(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, true));
@@ -30,14 +31,14 @@ __device__ __forceinline__ float lane_from_right(float v) {
 }
 __device__ __forceinline__ double lane_from_left(double v) {
   const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x138, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x138, 0xf, 0xf, false);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x138, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x138, 0xf, 0xf, true);
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 __device__ __forceinline__ double lane_from_right(double v) {
   const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x130, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x130, 0xf, 0xf, false);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x130, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x130, 0xf, 0xf, true);
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
