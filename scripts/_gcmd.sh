@@ -1,5 +1,7 @@
 set -e
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_kernels.py > gpurun_out/kt.log 2>&1 || { tail -30 gpurun_out/kt.log; exit 1; }
-tail -1 gpurun_out/kt.log
-for L in 512 1024; do timeout -k 10 300 python bench.py --L $L --precision Float64 --steps 60 --warmup 6 2>/dev/null | cut -c1-160; done
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+rm -rf gpurun_out/pmc_final
+GS_FUSED_CFG=4x12:1s GS_FUSED_SCHED=2 timeout -k 10 900 bash scripts/profile_kernels.sh gpurun_out/pmc_final --steps 60 --warmup 6 > gpurun_out/pmc_final.log 2>&1
+python scripts/pmc_summary.py gpurun_out/pmc_final > gpurun_out/pmc_final_summary.txt
+grep -A22 "k_fused" gpurun_out/pmc_final_summary.txt | head -24
