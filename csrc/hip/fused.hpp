@@ -167,19 +167,24 @@ __device__ __forceinline__ gs::U4 noise_block_dev(int64_t gx, int64_t gy4, int64
 constexpr int gs_gcd(int a, int b) { return b == 0 ? a : gs_gcd(b, a % b); }
 constexpr int gs_lcm(int a, int b) { return a / gs_gcd(a, b) * b; }
 
-template <typename T, int TL_, int ROWS_, int WAVES_, int PF_, bool PERIODIC_, bool NOISE_,
+template <typename T_, int TL_, int ROWS_, int WAVES_, int PF_, bool PERIODIC_, bool NOISE_,
           int MINW_ = 1, bool SKEW_ = false, int ABL_ = 0>
 struct FCfg {
   static constexpr int MINW = MINW_;  // __launch_bounds__ min waves per SIMD
+  using T = T_;
   using V2 = typename Vec2<T>::type;
   static constexpr int TL = TL_, ROWS = ROWS_, WAVES = WAVES_, PF = PF_;
   static constexpr bool PERIODIC = PERIODIC_, NOISE = NOISE_, SKEW = SKEW_;
+  // fp32: the noise coefficient dt*noise*2^-31 in a VGPR (saves the uniform's v_mul; an SGPR
+  // copy spilled, profiles/r1_ab_noise_fold.txt); ABL bit 6 restores the separate scale
+  static constexpr bool FOLD31 = sizeof(T_) == 4 && !(ABL_ & 64);
   // ablation (timing experiments only, results are WRONG): bit0 = no workgroup barriers,
   // bit1 = every level-0 load reads plane 0 (L2-resident); bit2 (results exact) = hoistable
   // Philox key schedule (the pre-noise_block_dev code generation); bit3 (results exact) =
   // hoistable step words in the Philox counter (before the opaque-step change); bit4 (exact) =
   // float2 LDS reads split by the compiler into two ds_read_b32 (before lds_load2); bit5
-  // (exact) = 64-bit buffer-range descriptors (before plane_rsrc_p)
+  // (exact) = 64-bit buffer-range descriptors (before plane_rsrc_p); bit6 (exact) = separate
+  // 2^-31 noise scale (before FOLD31)
   static constexpr int ABL = ABL_;
   static constexpr int R = PF + 2;                    // level-0 ring slots
   static constexpr int NS = SKEW ? 3 : 2;             // level-l output ring / xch buffers
@@ -190,6 +195,7 @@ struct FCfg {
 template <class C>
 struct FusedState {
   using V2 = typename C::V2;
+  typename C::T ar31;  // dt * noise * 2^-31 held in a VGPR (C::FOLD31)
   V2 LD[C::R][C::ROWS];
   V2 OUT[C::NO][C::NS][C::ROWS];
   V2 A[C::TL][C::ROWS];
@@ -304,7 +310,8 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
           // (folding the 2^-31 of uniform_pm1 into ar saves a v_mul but costs an SGPR; the
           // extra spill reloads made it 2 % slower: profiles/r1_ab_noise_fold.txt)
           const uint32_t w = k == 0 ? blk.x : (k == 1 ? blk.y : (k == 2 ? blk.z : blk.w));
-          ru = fma(f.ar, gs::uniform_pm1<T>(w), ru);
+          if constexpr (C::FOLD31) ru = fma(S.ar31, (T)(int32_t)w, ru);
+          else ru = fma(f.ar, gs::uniform_pm1<T>(w), ru);
         }
         res[j].x = fma(f.au, cu, fma(f.asu, su, fma(-f.dt, uvv, ru)));
         res[j].y = fma(f.bv, cv, fma(f.bsv, sv, f.dt * uvv));
@@ -428,6 +435,12 @@ __global__ __launch_bounds__(64 * C::WAVES, C::MINW) void k_fused(const typename
     if (lu0 >= lu1) return;
   }
   FusedState<C> S;
+  if constexpr (C::FOLD31) {
+    // exact: power-of-two scaling (gs::uniform_pm1 = int * 2^-31); a VGPR copy keeps the
+    // coefficient out of the (full) SGPR budget
+    const T c = f.ar * (T)4.656612873077392578125e-10;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(S.ar31) : "s"(c));
+  }
 
   for (int lu = lu0; lu < lu1; lu += lstep) {
     int64_t u, uend;
@@ -605,7 +618,8 @@ inline const char* const* fused_cfg_names(int* n) {
                                 "4x8:1w4", "4x16:1", "4x16:2w4", "4x8:2w3", "abl4", "4x8:1abl4",
                                 "4x12:2s", "4x12:1s", "4x6:2s", "4x12:1", "4x12:1s-abl1",
                                 "4x12:1s-abl2", "4x12:1s-abl8", "4x12:2s-abl8", "4x12:1s-abl16",
-                                "4x12:2s-abl16", "4x12:1s-abl32"};
+                                "4x12:2s-abl16", "4x12:1s-abl32", "4x12:1s-abl64",
+                                "4x12:2s-abl64"};
   *n = (int)(sizeof(names) / sizeof(names[0]));
   return names;
 }
@@ -689,6 +703,8 @@ void run_fused_cfg(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, c
       case 38: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, 1, true, 16>, T>::run(s, d, a, p, st); return;
       case 39: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, 1, true, 16>, T>::run(s, d, a, p, st); return;
       case 40: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, 1, true, 32>, T>::run(s, d, a, p, st); return;
+      case 41: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, 1, true, 64>, T>::run(s, d, a, p, st); return;
+      case 42: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, 1, true, 64>, T>::run(s, d, a, p, st); return;
       default: break;
     }
   }
