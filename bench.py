@@ -79,8 +79,7 @@ def main(argv=None) -> int:
         dims = tuning["dims"]
         settings.fuse_steps = tuning["fuse"]
         settings.transport, settings.overlap = tuning["transport"], tuning["overlap"]
-        if not tuning["inplace_halos"]:
-            os.environ["GS_INPLACE_HALO"] = "0"
+        os.environ.update(tuning["env"])
     dom = init_domain(args.L, ctx.world_size, ctx.rank, periodic=False, dims=dims)
     sim = GrayScott(settings, dom, ctx, use_fused=not args.no_fused_kernel)
     sim.init_fields()

@@ -50,8 +50,7 @@ def initialize_from_settings(settings: Settings):
             t = tune_data_path(settings, ctx, settings.L, backend)
             settings.fuse_steps = t["fuse"]
             settings.transport, settings.overlap = t["transport"], t["overlap"]
-            if not t["inplace_halos"]:
-                os.environ["GS_INPLACE_HALO"] = "0"
+            os.environ.update(t["env"])
             dims = t["dims"]
         else:
             dims = choose_dims(settings.L, ctx.world_size, "auto", backend)

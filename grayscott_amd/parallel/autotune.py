@@ -60,10 +60,10 @@ def selfcheck(ctx, backend: str, dims, fuse: int, transport: str, overlap: str, 
     return err < 1e-4, err, used
 
 
-def candidates(L: int, nprocs: int, backend: str) -> List[Tuple[List[int], int, str]]:
-    """(dims, fuse, overlap) triples worth timing for ``nprocs`` ranks on an L^3 grid
-    (fuse 0 = auto)."""
-    out: List[Tuple[List[int], int, str]] = []
+def candidates(L: int, nprocs: int, backend: str) -> List[Tuple]:
+    """(dims, fuse, overlap[, env]) candidates worth timing for ``nprocs`` ranks on an L^3 grid
+    (fuse 0 = auto; env: engine knobs set for that candidate)."""
+    out: List[Tuple] = []
 
     def add(d, f, ov="auto"):
         if (list(d), f, ov) not in out:
@@ -84,6 +84,10 @@ def candidates(L: int, nprocs: int, backend: str) -> List[Tuple[List[int], int, 
         # 64-lane x tiles, and only one tile ring (the y face) outside the overlap
         if nprocs >= 4 and nprocs % 2 == 0 and L // (nprocs // 2) >= 8:
             add([1, 2, nprocs // 2], 0)
+        # z slabs with more workgroup slots left free for RCCL's kernel next to the inner
+        # update (16 by default): trades inner-kernel throughput for halo bandwidth
+        if L // nprocs >= 8:
+            out.append((list(z), 0, "auto", {"GS_OVERLAP_RESERVE": "64"}))
     return out
 
 
@@ -124,9 +128,9 @@ def time_data_path(settings, ctx, L: int, dims, fuse: int, steps: int = 30, warm
 def tune_data_path(settings, ctx, L: int, backend: str,
                    cands: Optional[Sequence[Tuple]] = None,
                    steps: int = 120, warmup: int = 12, log=None) -> Dict:
-    """Self-check and time every candidate ``(dims, fuse[, overlap])``; returns ``{"dims",
-    "fuse", "transport", "overlap", "inplace_halos", "table"}`` for the fastest correct one
-    (identical on every rank)."""
+    """Self-check and time every candidate ``(dims, fuse[, overlap[, env]])``; returns
+    ``{"dims", "fuse", "transport", "overlap", "inplace_halos", "env", "table"}`` for the fastest
+    correct one (identical on every rank; ``env`` must be set for the run that uses it)."""
     from ..models.grayscott import default_fuse
 
     cands = list(cands) if cands is not None else candidates(L, ctx.world_size, backend)
@@ -135,24 +139,29 @@ def tune_data_path(settings, ctx, L: int, backend: str,
     for cand in cands:
         dims, fuse = cand[0], cand[1]
         ov0 = cand[2] if len(cand) > 2 else settings.overlap
+        env0 = dict(cand[3]) if len(cand) > 3 else {}
         dom = init_domain(L, ctx.world_size, ctx.rank, periodic=False, dims=dims)
         f = fuse if fuse > 0 else default_fuse(backend, dom, settings.dtype_name)
         f = max(1, min(f, min(dom.proc_sizes)))
         if any(r["dims"] == list(dims) and r["fuse"] == f and r["overlap_req"] == ov0
-               for r in table):
+               and r.get("env", {}) == env0 for r in table):
             continue  # "auto" resolved to a depth already in the list
         row = {"dims": list(dims), "fuse": f, "overlap_req": ov0}
+        if env0:
+            row["env"] = env0
         chosen = None
-        for tr, ov, inplace in ((settings.transport, ov0, None),
-                                (settings.transport, "off", "0"), ("torch", "off", "0")):
-            with _inplace_env(inplace):
+        for tr, ov, extra in ((settings.transport, ov0, {}),
+                              (settings.transport, "off", {"GS_INPLACE_HALO": "0"}),
+                              ("torch", "off", {"GS_INPLACE_HALO": "0"})):
+            env = {**env0, **extra}
+            with _env(env):
                 try:
                     ok, err, used = selfcheck(ctx, backend, dims, f, tr, ov)
                 except Exception:  # a path that cannot even be set up is skipped
                     ok, used = False, None
             ok = ctx.allreduce(1.0 if ok else 0.0, "min") > 0
             if ok:
-                chosen = (used, ov, inplace)
+                chosen = (used, ov, env)
                 break
         if chosen is None:
             row.update(ok=False)
@@ -160,7 +169,7 @@ def tune_data_path(settings, ctx, L: int, backend: str,
             continue
         s = copy.copy(settings)
         s.transport, s.overlap = chosen[0], chosen[1]
-        with _inplace_env(chosen[2]):
+        with _env(chosen[2]):
             try:
                 el, ovd = time_data_path(s, ctx, L, dims, f, steps=steps, warmup=warmup)
                 ran = 1.0
@@ -172,7 +181,8 @@ def tune_data_path(settings, ctx, L: int, backend: str,
             table.append(row)
             continue
         row.update(ok=True, transport=chosen[0], overlap=chosen[1], overlapped=ovd,
-                   inplace_halos=chosen[2] is None, ms_per_step=round(1e3 * el / steps, 4))
+                   inplace_halos=chosen[2].get("GS_INPLACE_HALO") != "0",
+                   ms_per_step=round(1e3 * el / steps, 4))
         table.append(row)
         if log is not None and ctx.rank == 0:
             log(f"data path {row}")
@@ -180,21 +190,22 @@ def tune_data_path(settings, ctx, L: int, backend: str,
             best = (el, list(dims), f, chosen)
     if best is None:
         raise RuntimeError(f"no multi-rank data path passed its self-check: {table}")
+    env = best[3][2]
     return {"dims": best[1], "fuse": best[2], "transport": best[3][0], "overlap": best[3][1],
-            "inplace_halos": best[3][2] is None, "table": table}
+            "inplace_halos": env.get("GS_INPLACE_HALO") != "0", "env": env, "table": table}
 
 
 @contextlib.contextmanager
-def _inplace_env(inplace: Optional[str]):
-    """GS_INPLACE_HALO=0 turns the in-place RCCL plane halos off (read at engine creation)."""
-    old = os.environ.get("GS_INPLACE_HALO")
-    if inplace is not None:
-        os.environ["GS_INPLACE_HALO"] = inplace
+def _env(overrides: Dict[str, str]):
+    """Environment knobs read at engine creation (GS_INPLACE_HALO, GS_OVERLAP_RESERVE, ...)
+    set for one candidate and restored afterwards."""
+    old = {k: os.environ.get(k) for k in overrides}
+    os.environ.update(overrides)
     try:
         yield
     finally:
-        if inplace is not None:
-            if old is None:
-                os.environ.pop("GS_INPLACE_HALO", None)
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
             else:
-                os.environ["GS_INPLACE_HALO"] = old
+                os.environ[k] = v
