@@ -40,6 +40,18 @@ namespace {
 using gs::Box;
 using gs::Geom;
 
+// One RCCL communicator per process, reused by every engine over the same (nranks, rank):
+// data-path tuning builds a dozen engines in sequence, and each communicator set-up costs
+// seconds at 8 ranks.  Every rank makes the same sequence of engines, so all reuse together.
+struct SharedComm {
+  ncclComm_t comm = nullptr;
+  int nranks = -1, rank = -1;
+};
+SharedComm& shared_comm() {
+  static SharedComm c;
+  return c;
+}
+
 // set once a configuration is chosen explicitly through gs_fused_select / gs_fused_sched
 bool& fused_pinned() {
   static bool v = false;
@@ -72,7 +84,7 @@ class HipBackend final : public gs::Backend {
     xs_ = stream_;
   }
   ~HipBackend() override {
-    if (comm_) ncclCommDestroy(comm_);
+    if (comm_ && comm_ != shared_comm().comm) ncclCommDestroy(comm_);
     if (ws_) (void)hipFree(ws_);
     if (ev_) (void)hipEventDestroy(ev_);
     if (ev_fork_) (void)hipEventDestroy(ev_fork_);
@@ -342,14 +354,12 @@ class HipBackend final : public gs::Backend {
       ncclResult_t async = ncclSuccess;
       NCCL_CHECK(ncclCommGetAsyncError(comm_, &async));
       if (async != ncclSuccess) {
-        ncclCommAbort(comm_);
-        comm_ = nullptr;
+        abort_comm();
         throw std::runtime_error(std::string("RCCL asynchronous error: ") + ncclGetErrorString(async));
       }
       const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
       if (timeout_s > 0 && el > timeout_s) {
-        ncclCommAbort(comm_);
-        comm_ = nullptr;
+        abort_comm();
         throw std::runtime_error("halo exchange watchdog: device work not finished after " +
                                  std::to_string(timeout_s) + " s (GS_COMM_TIMEOUT)");
       }
@@ -382,9 +392,24 @@ class HipBackend final : public gs::Backend {
     out[0] = su; out[1] = mnu; out[2] = mxu; out[3] = sv; out[4] = mnv; out[5] = mxv;
   }
 
+  // a failed communicator is aborted and never reused
+  void abort_comm() {
+    if (comm_ == shared_comm().comm) shared_comm() = SharedComm{};
+    ncclCommAbort(comm_);
+    comm_ = nullptr;
+  }
+
   void init_comm(const ncclUniqueId& id, int nranks, int rank) {
+    SharedComm& sc = shared_comm();
+    if (sc.comm && sc.nranks == nranks && sc.rank == rank &&
+        !(getenv("GS_RCCL_REUSE") && atoi(getenv("GS_RCCL_REUSE")) == 0)) {
+      rank_ = rank;
+      comm_ = sc.comm;
+      return;
+    }
     rank_ = rank;
     NCCL_CHECK(ncclCommInitRank(&comm_, nranks, id, rank));
+    if (!sc.comm) sc = SharedComm{comm_, nranks, rank};  // kept for the process lifetime
   }
 
  private:
