@@ -178,13 +178,18 @@ struct FCfg {
   // fp32: the noise coefficient dt*noise*2^-31 in a VGPR (saves the uniform's v_mul; an SGPR
   // copy spilled, profiles/r1_ab_noise_fold.txt); ABL bit 6 restores the separate scale
   static constexpr bool FOLD31 = sizeof(T_) == 4 && !(ABL_ & 64);
+  // fp32 T=3: x-neighbour pair sum as one DPP move + one DPP add (lane_pair_sum): -36 VALU
+  // and -16 VGPRs per unrolled period, +1.8 % at L=512 (profiles/r1_ab_xsum_dpp.txt); neutral
+  // at T=2, which keeps the compiler's form.  ABL bit 7 restores it at T=3.
+  static constexpr bool XSUM_DPP = sizeof(T_) == 4 && TL_ == 3 && !(ABL_ & 128);
   // ablation (timing experiments only, results are WRONG): bit0 = no workgroup barriers,
   // bit1 = every level-0 load reads plane 0 (L2-resident); bit2 (results exact) = hoistable
   // Philox key schedule (the pre-noise_block_dev code generation); bit3 (results exact) =
   // hoistable step words in the Philox counter (before the opaque-step change); bit4 (exact) =
   // float2 LDS reads split by the compiler into two ds_read_b32 (before lds_load2); bit5
   // (exact) = 64-bit buffer-range descriptors (before plane_rsrc_p); bit6 (exact) = separate
-  // 2^-31 noise scale (before FOLD31)
+  // 2^-31 noise scale (before FOLD31); bit7 (exact) = compiler-formed x-neighbour sums at T=3
+  // (before XSUM_DPP)
   static constexpr int ABL = ABL_;
   static constexpr int R = PF + 2;                    // level-0 ring slots
   static constexpr int NS = SKEW ? 3 : 2;             // level-l output ring / xch buffers
@@ -215,6 +220,21 @@ template <class C>
 __device__ __forceinline__ int64_t gwrap(int64_t v, int64_t L) {
   if constexpr (C::PERIODIC) return wrap(v, L);
   else return v;
+}
+
+// left + right x-neighbours in two instructions: one DPP move and one DPP add (the compiler
+// pairs the u and v halves into v_pk_add_f32 instead and keeps both moves).  Same rounding
+// as lane_from_left(v) + lane_from_right(v).  The leading s_nop covers the VALU-write ->
+// DPP-read hazard the compiler cannot see through inline asm.
+__device__ __forceinline__ float lane_pair_sum(float v) {
+  float t, r;
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_mov_b32_dpp %1, %2 wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %0, %2, %1 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+      : "=v"(r), "=&v"(t)
+      : "v"(v));
+  return r;
 }
 
 // One (u, v) pair from LDS as a single 8-byte ds_read_b64 (the compiler otherwise splits a
@@ -299,8 +319,14 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
         const int j = 4 * m + k;
         const V2 ym = j == 0 ? up : in[j - 1];
         const V2 yp = j == ROWS - 1 ? dn : in[j + 1];
-        const T xyu = (lane_from_left(in[j].x) + lane_from_right(in[j].x)) + (ym.x + yp.x);
-        const T xyv = (lane_from_left(in[j].y) + lane_from_right(in[j].y)) + (ym.y + yp.y);
+        T xyu, xyv;
+        if constexpr (C::XSUM_DPP) {
+          xyu = lane_pair_sum(in[j].x) + (ym.x + yp.x);
+          xyv = lane_pair_sum(in[j].y) + (ym.y + yp.y);
+        } else {
+          xyu = (lane_from_left(in[j].x) + lane_from_right(in[j].x)) + (ym.x + yp.x);
+          xyv = (lane_from_left(in[j].y) + lane_from_right(in[j].y)) + (ym.y + yp.y);
+        }
         const T su = S.A[l][j].x + in[j].x;
         const T sv = S.A[l][j].y + in[j].y;
         const T cu = Cc[j].x, cv = Cc[j].y;
@@ -619,7 +645,7 @@ inline const char* const* fused_cfg_names(int* n) {
                                 "4x12:2s", "4x12:1s", "4x6:2s", "4x12:1", "4x12:1s-abl1",
                                 "4x12:1s-abl2", "4x12:1s-abl8", "4x12:2s-abl8", "4x12:1s-abl16",
                                 "4x12:2s-abl16", "4x12:1s-abl32", "4x12:1s-abl64",
-                                "4x12:2s-abl64"};
+                                "4x12:2s-abl64", "4x12:1s-abl128", "4x12:2s-abl128"};
   *n = (int)(sizeof(names) / sizeof(names[0]));
   return names;
 }
@@ -705,6 +731,8 @@ void run_fused_cfg(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, c
       case 40: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, 1, true, 32>, T>::run(s, d, a, p, st); return;
       case 41: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, 1, true, 64>, T>::run(s, d, a, p, st); return;
       case 42: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, 1, true, 64>, T>::run(s, d, a, p, st); return;
+      case 43: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, 1, true, 128>, T>::run(s, d, a, p, st); return;
+      case 44: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, 1, true, 128>, T>::run(s, d, a, p, st); return;
       default: break;
     }
   }
