@@ -86,14 +86,16 @@ __global__ __launch_bounds__(256) void k_pack(typename Vec2<T>::type* __restrict
                                               PackArgs a) {
   const Box b = a.box[blockIdx.y];
   typename Vec2<T>::type* p = buf + a.off[blockIdx.y];
-  const int64_t n = gs::box_cells(b);
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int x = (int)(i % b.nx);
-    const int64_t r = i / b.nx;
-    const int y = (int)(r % b.ny);
-    const int z = (int)(r / b.ny);
-    const int64_t j = gs::lin(g, b.x0 + x, b.y0 + y, b.z0 + z);
+  // a message box holds < 2^31 cells (halo slabs of one sub-domain): 32-bit index math
+  // (the 64-bit divisions dominated this kernel)
+  const uint32_t n = (uint32_t)gs::box_cells(b);
+  const uint32_t bnx = (uint32_t)b.nx, bny = (uint32_t)b.ny;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t r = i / bnx;
+    const int x = (int)(i - r * bnx);
+    const uint32_t z = r / bny;
+    const int y = (int)(r - z * bny);
+    const int64_t j = gs::lin(g, b.x0 + x, b.y0 + y, b.z0 + (int)z);
     if (PACK) p[i] = f[j];
     else f[j] = p[i];
   }
