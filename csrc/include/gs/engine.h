@@ -272,8 +272,9 @@ class Engine {
         continue;
       }
       if (overlapped(k)) {
-        // Inner planes [k, nz-k) need no halo: run them while the exchange is in flight on
-        // the comm stream, then the two k-plane boundary slabs once it has landed.
+        // One overlapped pass: the inner part (overlap_split) needs no halo, so it runs on
+        // the compute stream while the exchange is in flight on the comm stream; the end
+        // slabs (and, packed plans, the ring tiles) follow once the halos have landed.
         ensure_bc(cur_, t_);  // before the fork: the exchanged planes carry these ghosts
         be_->comm_fork();
         be_->comm_select(true);
