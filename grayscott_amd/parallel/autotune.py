@@ -79,7 +79,7 @@ def candidates(L: int, nprocs: int, backend: str) -> List[Tuple]:
     add(bal, 0)
     if backend == "hip":
         add(bal, 0, "off")
-        add(bal, 3)
+        add(bal, 2)
         # z slabs split once along y: half the z-plane bytes per link of the plain slabs, full
         # 64-lane x tiles, and only one tile ring (the y face) outside the overlap
         if nprocs >= 4 and nprocs % 2 == 0 and L // (nprocs // 2) >= 8:

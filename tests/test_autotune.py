@@ -45,6 +45,6 @@ def test_candidates_for_mi355x():
     from grayscott_amd.parallel.autotune import candidates
     assert candidates(512, 8, "hip") == [([1, 1, 8], 0, "auto"), ([1, 1, 8], 2, "auto"),
                                         ([2, 2, 2], 0, "auto"), ([2, 2, 2], 0, "off"),
-                                        ([2, 2, 2], 3, "auto"), ([1, 2, 4], 0, "auto"),
+                                        ([2, 2, 2], 2, "auto"), ([1, 2, 4], 0, "auto"),
                                         ([1, 1, 8], 0, "auto", {"GS_OVERLAP_RESERVE": "64"})]
     assert candidates(512, 1, "hip") == [([1, 1, 1], 0, "auto")]
