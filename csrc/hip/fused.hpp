@@ -175,9 +175,9 @@ struct FCfg {
   using V2 = typename Vec2<T>::type;
   static constexpr int TL = TL_, ROWS = ROWS_, WAVES = WAVES_, PF = PF_;
   static constexpr bool PERIODIC = PERIODIC_, NOISE = NOISE_, SKEW = SKEW_;
-  // fp32: the noise coefficient dt*noise*2^-31 in a VGPR (saves the uniform's v_mul; an SGPR
+  // the noise coefficient dt*noise*2^-31 in a VGPR (saves the uniform's v_mul; an SGPR
   // copy spilled, profiles/r1_ab_noise_fold.txt); ABL bit 6 restores the separate scale
-  static constexpr bool FOLD31 = sizeof(T_) == 4 && !(ABL_ & 64);
+  static constexpr bool FOLD31 = !(ABL_ & 64);
   // fp32 T=3: x-neighbour pair sum as one DPP move + one DPP add (lane_pair_sum): -36 VALU
   // and -16 VGPRs per unrolled period, +1.8 % at L=512 (profiles/r1_ab_xsum_dpp.txt); neutral
   // at T=2, which keeps the compiler's form.  ABL bit 7 restores it at T=3.
@@ -465,7 +465,8 @@ __global__ __launch_bounds__(64 * C::WAVES, C::MINW) void k_fused(const typename
     // exact: power-of-two scaling (gs::uniform_pm1 = int * 2^-31); a VGPR copy keeps the
     // coefficient out of the (full) SGPR budget
     const T c = f.ar * (T)4.656612873077392578125e-10;
-    asm volatile("v_mov_b32 %0, %1" : "=v"(S.ar31) : "s"(c));
+    if constexpr (sizeof(T) == 4) asm volatile("v_mov_b32 %0, %1" : "=v"(S.ar31) : "s"(c));
+    else asm volatile("v_mov_b64 %0, %1" : "=v"(S.ar31) : "s"(c));
   }
 
   for (int lu = lu0; lu < lu1; lu += lstep) {
@@ -645,7 +646,8 @@ inline const char* const* fused_cfg_names(int* n) {
                                 "4x12:2s", "4x12:1s", "4x6:2s", "4x12:1", "4x12:1s-abl1",
                                 "4x12:1s-abl2", "4x12:1s-abl8", "4x12:2s-abl8", "4x12:1s-abl16",
                                 "4x12:2s-abl16", "4x12:1s-abl32", "4x12:1s-abl64",
-                                "4x12:2s-abl64", "4x12:1s-abl128", "4x12:2s-abl128"};
+                                "4x12:2s-abl64", "4x12:1s-abl128", "4x12:2s-abl128", "(unused)",
+                                "4x8:1s-abl64"};
   *n = (int)(sizeof(names) / sizeof(names[0]));
   return names;
 }
@@ -684,6 +686,7 @@ void run_fused_cfg(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, c
       case 19: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, 1, true>, T>::run(s, d, a, p, st); return;
       case 32: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, 1, true>, T>::run(s, d, a, p, st); return;
       case 33: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ>, T>::run(s, d, a, p, st); return;
+      case 46: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, 1, true, 64>, T>::run(s, d, a, p, st); return;
       default: break;
     }
   }
