@@ -102,3 +102,21 @@ def test_rccl_loopback_zplanes_not_inplace(monkeypatch):
     assert i1["transport"] == "rccl"
     np.testing.assert_array_equal(u1, u0)
     np.testing.assert_array_equal(v1, v0)
+
+
+@pytest.mark.parametrize("mode", ["zplanes", "packed"])
+def test_rccl_loopback_chained_long_run(mode):
+    """Many chained passes (advance_chained: exchange -> end slabs -> next exchange on the comm
+    stream, inner part on the compute stream) stay bit-identical to self copies, also with a
+    trailing partial pass that leaves the chain."""
+    L = 48
+    dom = init_domain(L, 1, 0, periodic=True)
+    if mode == "zplanes":
+        dom = _z_only(dom)
+    s = _settings(overlap="on")
+    s.L = L
+    u0, v0, _ = _run(dom, s, 3, 3 * 20 + 2, loopback=False)
+    u1, v1, i1 = _run(dom, s, 3, 3 * 20 + 2, loopback=True)
+    assert i1["overlapped"] and i1["transport"] == "rccl"
+    np.testing.assert_array_equal(u1, u0)
+    np.testing.assert_array_equal(v1, v0)
