@@ -22,7 +22,7 @@ import os
 import sys
 import time
 import traceback
-from typing import List, Optional, Sequence
+from typing import Optional, Sequence
 
 from .io.checkpoint import restart as do_restart
 from .io.checkpoint import write_checkpoint

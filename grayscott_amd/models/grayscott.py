@@ -12,9 +12,6 @@ memory on MI355X, host memory for the CPU backend) and updated in place by the n
 """
 from __future__ import annotations
 
-import math
-import os
-from dataclasses import dataclass
 from typing import Optional, Tuple
 
 import numpy as np

@@ -9,7 +9,6 @@ environment (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR / MASTER_PORT); the *d
 from __future__ import annotations
 
 import os
-import pickle
 from dataclasses import dataclass
 from typing import Any, List, Optional
 
