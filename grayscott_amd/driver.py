@@ -86,6 +86,7 @@ def run(settings: Settings, out=sys.stdout) -> dict:
             step = do_restart(sim, settings, ctx)
         if rank == 0 and settings.verbose:
             print(f"Restarting from step {step} ({settings.restart_input})", file=out, flush=True)
+    first_step = step
     t_loop = time.perf_counter()
     compute_s = 0.0
     cells = float(domain.L[0]) * domain.L[1] * domain.L[2]
@@ -126,7 +127,7 @@ def run(settings: Settings, out=sys.stdout) -> dict:
     with timer.phase("io_close"):
         stream.close()
     result = {"steps": step, "loop_s": loop_s, "compute_s": compute_s,
-              "mlups_compute": cells * settings.steps / max(compute_s, 1e-12) / 1e6,
+              "mlups_compute": cells * (step - first_step) / max(compute_s, 1e-12) / 1e6,
               "timers": timer.summary(), "ranks": ctx.world_size, "fuse": sim.fuse,
               "transport": sim.transport}
     perf.write(summary=result)
