@@ -11,7 +11,10 @@ Parity:
 Additions: checkpoint every ``checkpoint_freq`` steps and restart from ``restart_input`` (the
 reference parses these keys but ignores them, D6), a JSON-lines perf log, optional global
 diagnostics, and fault injection for restart testing (``GS_FAIL_AT_STEP=<n>`` makes every
-rank exit with status 3 right after step n has been computed and checkpointed).
+rank exit with status 3 right after step n has been computed and checkpointed).  Checkpoints
+are written behind the simulation by default (``async_checkpoint``, io/checkpoint.py
+``CheckpointWriter``): the data write runs on a host thread from the same snapshot as the output
+step, and is committed before the next snapshot, at the end, or before a fault-injected exit.
 
 The loop advances in chunks up to the next output/checkpoint event, so steps between events
 run back to back in the native engine (temporal blocking, no per-step Python).
@@ -25,7 +28,7 @@ import traceback
 from typing import Optional, Sequence
 
 from .io.checkpoint import restart as do_restart
-from .io.checkpoint import write_checkpoint
+from .io.checkpoint import CheckpointWriter, write_checkpoint
 from .io.output import SimulationOutput
 from .models.grayscott import GrayScott
 from .parallel.decomp import choose_dims, init_domain
@@ -87,6 +90,9 @@ def run(settings: Settings, out=sys.stdout) -> dict:
         if rank == 0 and settings.verbose:
             print(f"Restarting from step {step} ({settings.restart_input})", file=out, flush=True)
     first_step = step
+    ckpt_on = settings.checkpoint and settings.checkpoint_freq > 0
+    ckpt = (CheckpointWriter(settings, domain, ctx)
+            if ckpt_on and getattr(settings, "async_checkpoint", True) else None)
     t_loop = time.perf_counter()
     compute_s = 0.0
     cells = float(domain.L[0]) * domain.L[1] * domain.L[2]
@@ -100,29 +106,47 @@ def run(settings: Settings, out=sys.stdout) -> dict:
         nsteps = nxt - step
         step = nxt
         io_s = 0.0
-        if settings.plotgap > 0 and step % settings.plotgap == 0:
+        do_out = settings.plotgap > 0 and step % settings.plotgap == 0
+        do_ckpt = ckpt_on and step % settings.checkpoint_freq == 0
+        if ckpt is not None and ckpt.pending and (do_out or do_ckpt):
+            # the previous checkpoint's data thread reads the snapshot buffers: commit it
+            # before they are reused
+            t1 = time.perf_counter()
+            with timer.phase("checkpoint"):
+                ckpt.finish()
+            io_s += time.perf_counter() - t1
+        snap = None
+        if do_out:
             if rank == 0 and settings.verbose:
                 print(f"Simulation at step {step} writing output step "
                       f"{step / settings.plotgap}", file=out, flush=True)
             t1 = time.perf_counter()
             with timer.phase("output"):
-                stream.write_step(step, sim)
+                snap = stream.write_step(step, sim)
             io_s += time.perf_counter() - t1
             if settings.diagnostics:
                 d = sim.global_stats()
                 if rank == 0:
                     print(f"  step {step}: " + " ".join(f"{k}={v:.6g}" for k, v in d.items()),
                           file=out, flush=True)
-        if settings.checkpoint and settings.checkpoint_freq > 0 and step % settings.checkpoint_freq == 0:
+        if do_ckpt:
             t1 = time.perf_counter()
             with timer.phase("checkpoint"):
-                write_checkpoint(settings.checkpoint_output, step, sim, settings, ctx)
+                if ckpt is not None:
+                    ckpt.start(step, sim, snap)
+                else:
+                    write_checkpoint(settings.checkpoint_output, step, sim, settings, ctx)
             io_s += time.perf_counter() - t1
         perf.write(step=step, steps=nsteps, compute_s=dt_c, io_s=io_s,
                    mlups=cells * nsteps / max(dt_c, 1e-12) / 1e6, ranks=ctx.world_size)
         if fail_at >= 0 and step >= fail_at:
+            if ckpt is not None:
+                ckpt.finish()
             sys.stdout.flush()
             os._exit(3)  # simulated node failure (no clean shutdown)
+    if ckpt is not None and ckpt.pending:
+        with timer.phase("checkpoint"):
+            ckpt.finish()
     loop_s = time.perf_counter() - t_loop
     with timer.phase("io_close"):
         stream.close()

@@ -25,13 +25,10 @@ from .bp4 import BP4Reader, BP4Writer
 _NP = {"float32": np.float32, "float64": np.float64}
 
 
-def write_checkpoint(path: str, step: int, sim, settings, ctx: Optional[DistContext] = None) -> None:
-    ctx = ctx or DistContext()
-    tmp = path.rstrip("/") + ".tmp"
+def _open_writer(tmp: str, settings, dom, ctx: DistContext) -> BP4Writer:
     if ctx.rank == 0 and os.path.isdir(tmp):
         shutil.rmtree(tmp)
     ctx.barrier()
-    dom = sim.domain
     w = BP4Writer(tmp, "SimulationCheckpoint", ctx.rank, ctx.world_size)
     if ctx.rank == 0:
         w.define_attribute("seed", np.uint64(settings.seed))
@@ -46,12 +43,20 @@ def write_checkpoint(path: str, step: int, sim, settings, ctx: Optional[DistCont
     w.define_variable("step", np.int32)
     w.define_variable("U", dt, (Lz, Ly, Lx), (oz, oy, ox), (nz, ny, nx))
     w.define_variable("V", dt, (Lz, Ly, Lx), (oz, oy, ox), (nz, ny, nx))
-    u, v = sim.get_fields()
+    return w
+
+
+def _write_data(w: BP4Writer, step: int, u, v) -> bytes:
     w.begin_step()
     w.put("step", np.int32(step))
     w.put("U", u)
     w.put("V", v)
-    blobs = ctx.gather_object(w.end_step(), dst=0)
+    return w.end_step()
+
+
+def _commit(w: BP4Writer, blob: bytes, path: str, tmp: str, ctx: DistContext) -> None:
+    """Collective: metadata of all ranks into rank 0's index, then the atomic rename."""
+    blobs = ctx.gather_object(blob, dst=0)
     if ctx.rank == 0:
         w.write_metadata(blobs)
     w.close()
@@ -66,6 +71,59 @@ def write_checkpoint(path: str, step: int, sim, settings, ctx: Optional[DistCont
         if os.path.isdir(old):
             shutil.rmtree(old)
     ctx.barrier()
+
+
+def write_checkpoint(path: str, step: int, sim, settings, ctx: Optional[DistContext] = None) -> None:
+    """Synchronous checkpoint of the current state (collective)."""
+    ctx = ctx or DistContext()
+    tmp = path.rstrip("/") + ".tmp"
+    w = _open_writer(tmp, settings, sim.domain, ctx)
+    u, v = sim.get_fields()
+    _commit(w, _write_data(w, step, u, v), path, tmp, ctx)
+
+
+class CheckpointWriter:
+    """Checkpoints written behind the simulation (``async_checkpoint``, the default).
+
+    ``start`` snapshots the state (device compaction + D2H on the I/O stream, or a snapshot the
+    output stream already took at the same step) and writes the data file on a host thread;
+    ``finish`` -- called by the driver before the next snapshot and at the end of the run --
+    joins it, gathers the per-rank metadata and renames ``<path>.tmp`` over the previous
+    checkpoint.  Until then the previous checkpoint stays the committed one, so a failure
+    while the data is in flight loses at most that one checkpoint, as with the synchronous
+    writer.  Collectives only run on the main thread."""
+
+    def __init__(self, settings, domain, ctx: Optional[DistContext] = None):
+        self.settings, self.domain = settings, domain
+        self.ctx = ctx or DistContext()
+        self.path = settings.checkpoint_output
+        self.tmp = self.path.rstrip("/") + ".tmp"
+        self._pending = None
+
+    @property
+    def pending(self) -> bool:
+        return self._pending is not None
+
+    def start(self, step: int, sim, snap=None) -> None:
+        """Begin the checkpoint of ``step``.  ``snap`` = ``(u, v, wait)`` from
+        ``sim.snapshot_fields()`` when the caller already took one for this step."""
+        from .output import _Job
+        self.finish()
+        w = _open_writer(self.tmp, self.settings, self.domain, self.ctx)
+        u, v, wait = snap if snap is not None else sim.snapshot_fields()
+
+        def job():
+            wait()
+            return _write_data(w, step, u, v)
+
+        self._pending = (w, _Job(job))
+
+    def finish(self) -> None:
+        job, self._pending = self._pending, None
+        if job is None:
+            return
+        w, j = job
+        _commit(w, j.result(), self.path, self.tmp, self.ctx)
 
 
 def read_checkpoint(path: str, domain, dtype: str) -> Tuple[int, np.ndarray, np.ndarray, dict]:

@@ -113,17 +113,21 @@ class SimulationOutput:
             self.w.write_metadata(blobs)
         self.steps_written += 1
 
-    def write_step(self, step: int, sim) -> None:
+    def write_step(self, step: int, sim):
         """IO.jl:82-96.  With ``async_output`` (default) the step is written behind the
         simulation: device snapshot + D2H on an I/O stream, data write on a host thread; the
         collective metadata gather of step n happens on the main thread at step n+1 (or at
-        close), so no collective ever runs off the main thread."""
+        close), so no collective ever runs off the main thread.  Returns the snapshot
+        ``(u, v, wait)`` it writes from (None when synchronous), so an asynchronous checkpoint
+        of the same step can share it; the caller must have finished every other reader of
+        the previous snapshot (the host buffers are reused)."""
         if not self.async_io:
             u, v = sim.get_fields()
             self.write_fields(step, u, v)
-            return
+            return None
         self.flush()
-        u, v, wait = sim.snapshot_fields()
+        snap = sim.snapshot_fields()
+        u, v, wait = snap
 
         def job():
             wait()
@@ -134,6 +138,7 @@ class SimulationOutput:
             return self.w.end_step()
 
         self._pending = _Job(job)
+        return snap
 
     def flush(self) -> None:
         """Finish the in-flight asynchronous step: wait for its data write, gather the

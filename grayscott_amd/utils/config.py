@@ -17,7 +17,9 @@ Extension keys (not in the reference, all optional, documented in README):
   ``decomposition`` ("auto"|"balanced"|"z": process grid, see parallel/decomp.choose_dims;
   "tune": self-check and time the candidate grids / fuse depths, parallel/autotune.py),
   ``overlap`` ("auto"|"on"|"off": overlap the halo exchange with the inner-plane update),
-  ``async_output`` (bool, default true: output steps are written behind the simulation).
+  ``async_output`` (bool, default true: output steps are written behind the simulation),
+  ``async_checkpoint`` (bool, default true: checkpoint data is written behind the simulation and
+  committed -- metadata, atomic rename -- at the next output/checkpoint event or at the end).
 """
 from __future__ import annotations
 
@@ -79,6 +81,7 @@ class Settings:
     decomposition: str = "auto"
     overlap: str = "auto"
     async_output: bool = True
+    async_checkpoint: bool = True
 
     # -------------------------------------------------------------------------------------
     @property
@@ -124,6 +127,7 @@ EXTENSION_KEYS: Dict[str, str] = {
     "decomposition": _STRING,
     "overlap": _STRING,
     "async_output": _BOOL,
+    "async_checkpoint": _BOOL,
 }
 
 # Keys present in reference configs but commented out of the struct (Structs.jl:20-22):

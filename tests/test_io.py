@@ -190,3 +190,26 @@ def test_async_output_matches_sync(tmp_path):
         assert sa == sb
         np.testing.assert_array_equal(ua, ub)
         np.testing.assert_array_equal(va, vb)
+
+
+def test_async_checkpoint_matches_sync(tmp_path):
+    """async_checkpoint (data written on a host thread, committed at the next event / end)
+    leaves the same checkpoint as the synchronous writer, including when it shares the
+    output step's snapshot (plotgap 3, checkpoint_freq 6) and when it does not (freq 4)."""
+    from grayscott_amd import driver
+
+    for freq in (6, 4):
+        res = {}
+        for mode in (False, True):
+            s = Settings(L=20, steps=14, plotgap=3, noise=0.1, F=0.02, k=0.048, dt=1.0, Du=0.2,
+                         Dv=0.1, precision="Float32", backend="CPU", async_checkpoint=mode,
+                         checkpoint=True, checkpoint_freq=freq,
+                         checkpoint_output=str(tmp_path / f"ck_{freq}_{mode}.bp"),
+                         output=str(tmp_path / f"gs_{freq}_{mode}.bp"))
+            driver.run(s, out=open(os.devnull, "w"))
+            assert not os.path.exists(s.checkpoint_output + ".tmp")
+            with BP4Reader(s.checkpoint_output) as r:
+                res[mode] = (int(r.read("step")), r.read("U", -1), r.read("V", -1))
+        assert res[True][0] == res[False][0] == (14 // freq) * freq
+        np.testing.assert_array_equal(res[True][1], res[False][1])
+        np.testing.assert_array_equal(res[True][2], res[False][2])
