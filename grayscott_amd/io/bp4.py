@@ -409,6 +409,15 @@ class BP4Reader:
             raise BP4Error("truncated data file")
         return np.frombuffer(raw, dtype=dtype).reshape(b.count if b.count else ())
 
+    def _block_view(self, b: Block, dtype: np.dtype) -> np.ndarray:
+        """Array block as a read-only memory map: a (sub-box) selection copies only the pages
+        it touches, once (checkpoint restarts read 512 MB blocks)."""
+        n = int(np.prod(b.count))
+        fh = self._file(b.file_index)
+        if os.fstat(fh.fileno()).st_size < b.payload_offset + n * dtype.itemsize:
+            raise BP4Error("truncated data file")
+        return np.memmap(fh, dtype=dtype, mode="r", offset=b.payload_offset, shape=tuple(b.count))
+
     def read(self, name: str, step: int = -1, start: Optional[Sequence[int]] = None,
              count: Optional[Sequence[int]] = None):
         """Read a variable at ``step`` (negative = from the end), optionally a sub-box."""
@@ -433,7 +442,7 @@ class BP4Reader:
             hi = [min(s + c, bs + bc) for s, c, bs, bc in zip(start, count, b.start, b.count)]
             if any(h <= l for l, h in zip(lo, hi)):
                 continue
-            data = self._block_data(b, dt)
+            data = self._block_view(b, dt)
             src = tuple(slice(l - bs, h - bs) for l, h, bs in zip(lo, hi, b.start))
             dst = tuple(slice(l - s, h - s) for l, h, s in zip(lo, hi, start))
             out[dst] = data[src]
