@@ -3,6 +3,9 @@
 #                      grayscott_amd/_lib/libgs_hip.so  (gfx950 kernels + RCCL transport)
 #   make selftest   -> build/bin/core_selftest (threads-as-ranks runtime self-test)
 #   make tools      -> build/bin/ubench_valu (gfx950 VALU issue-rate micro-benchmark)
+#   make ablation   -> grayscott_amd/_lib/libgs_hip_abl.so: the HIP library plus the fused
+#                      kernel's ablation variants (results WRONG by design; timing experiments
+#                      only, loaded with GS_HIP_VARIANT=abl by scripts/power_probe.py etc.)
 #   make asan/tsan  -> the same self-test under AddressSanitizer+UBSan / ThreadSanitizer (host
 #                      code only: GPU sanitizers are not available on the MI355X pool)
 ROCM     ?= /opt/rocm
@@ -28,6 +31,12 @@ $(OUT)/libgs_core.so: $(CORE_SRC) $(HDRS)
 $(OUT)/libgs_hip.so: $(HIP_SRC) $(HDRS)
 	@mkdir -p $(OUT)
 	$(HIPCC) $(HIPFLAGS) $(INC) -shared -o $@ $(HIP_SRC) -L$(ROCM)/lib -lrccl -Wl,-rpath,$(ROCM)/lib
+
+$(OUT)/libgs_hip_abl.so: $(HIP_SRC) $(HDRS)
+	@mkdir -p $(OUT)
+	$(HIPCC) $(HIPFLAGS) -DGS_ABLATION $(INC) -shared -o $@ $(HIP_SRC) -L$(ROCM)/lib -lrccl -Wl,-rpath,$(ROCM)/lib
+
+ablation: $(OUT)/libgs_hip_abl.so
 
 SELFTEST_TMP ?= /tmp
 SELFTEST_SRC := csrc/tools/core_selftest.cpp $(CORE_SRC)
@@ -64,4 +73,4 @@ clean:
 	rm -f $(OUT)/*.so
 	rm -rf build
 
-.PHONY: all clean selftest asan tsan tools
+.PHONY: all clean selftest asan tsan tools ablation

@@ -3,17 +3,25 @@
 
 BASELINE.json metric: "MLUPS (cell-updates/sec, whole node) at L=512 fp32, 1/2/4/8 MI355X".
 Config: the reference example physics (examples/settings-files.toml: F=0.02, k=0.048, dt=1,
-Du=0.2, Dv=0.1, noise=0.1) on an L^3 = 512^3 fp32 grid, decomposed over the N GPUs (z slabs
-1x1xN or the reference's Dims_create grid 2x2x2, whichever runs faster here).  The global grid
-is fixed as N grows (strong scaling).  Every timed step is a full update of all L^3 cells
-including the Philox noise and the RCCL halo exchange.  With N > 1 the multi-rank data path
-(z slabs or the balanced grid, fuse depth, transport) is verified against the golden model and
-then picked by a short timed run of each candidate before the timed region.
+Du=0.2, Dv=0.1, noise=0.1) on an L^3 = 512^3 fp32 grid with random-init u, v, decomposed over
+the N GPUs.  The global grid is fixed as N grows (strong scaling).  Every timed step is a full
+update of all L^3 cells including the Philox noise and the RCCL halo exchange.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--L 512] [--precision Float32]
-  torchrun --nproc-per-node N bench.py --gpus N ...
+  torchrun --nproc-per-node N bench.py --gpus N ...       (or mpiexec / srun)
 
-Rank 0 prints ONE JSON line.
+``--gpus N`` without a launcher starts the N ranks itself (parallel/launch.py: one worker
+process per GPU over a 127.0.0.1 rendezvous; this parent never touches the GPU) and exits with
+the job's status.  Rank 0 prints ONE JSON line.
+
+Before the timed region:
+  * N = 1: the tuned kernel's first steps on the benchmark state are checked against the native
+    OpenMP golden model (same Philox stream): ``check.max_abs_err``;
+  * N > 1: every candidate data path (z slabs / the reference's Dims_create grid, fuse depth,
+    overlap) is checked against the golden model on a small grid and timed on the real problem
+    (parallel/autotune.py); the fastest one is used, and the reference grid's own timing is
+    reported (``reference_grid``; ``config3_2x2x2`` at N = 8, BASELINE config 3).
+The JSON also records what RCCL saw: communicator size and each rank's device and PCI bus id.
 """
 from __future__ import annotations
 
@@ -23,12 +31,14 @@ import os
 import sys
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+T_START = time.perf_counter()
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
 
 
-def main(argv=None) -> int:
+def parse_args(argv):
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
-    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--gpus", type=int, default=None)
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=40)
     ap.add_argument("--L", type=int, default=512)
@@ -42,21 +52,83 @@ def main(argv=None) -> int:
     ap.add_argument("--overlap", default="auto", help="auto | on | off")
     ap.add_argument("--init", default="random", choices=["random", "seed"],
                     help="random: u, v ~ U[0,1) (BASELINE.json); seed: the reference's seed cube")
-    args = ap.parse_args(argv)
+    ap.add_argument("--check", default="auto", choices=["auto", "golden", "none"],
+                    help="golden-model check of the tuned path before timing (auto: 1 rank)")
+    ap.add_argument("--check-steps", type=int, default=6)
+    ap.add_argument("--tune-budget", type=float, default=float(os.environ.get("GS_TUNE_BUDGET_S",
+                                                                                "180")),
+                    help="seconds for the multi-rank data-path tuning (checks + timing)")
+    ap.add_argument("--timeout", type=float, default=0.0,
+                    help="self-launched jobs: kill all ranks after this many seconds (0 = off)")
+    return ap.parse_args(argv)
 
+
+def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse_args(argv)
+    from grayscott_amd.parallel.launch import launcher_env, spawn_local
+
+    _, world, _ = launcher_env()
+    ngpus = args.gpus if args.gpus is not None else world
+    if ngpus > 1 and world == 1:
+        # self-launch: one worker per GPU, before anything initialises HIP in this process
+        return spawn_local(ngpus, [sys.executable, os.path.abspath(__file__)] + argv,
+                           timeout=args.timeout or None, cwd=ROOT)
+    if ngpus != world:
+        print(f"bench.py: --gpus {ngpus} but the launcher started {world} ranks", file=sys.stderr)
+        return 2
+    try:
+        return run(args)
+    except BaseException:
+        if world > 1:
+            # one failed rank ends the job now instead of leaving its peers blocked
+            import traceback
+            traceback.print_exc()
+            from grayscott_amd.driver import abort_job
+            abort_job(1)
+        raise
+
+
+def golden_check(sim, settings, dom, nsteps: int):
+    """Advance the benchmark state ``nsteps`` steps on the tuned path and on the native OpenMP
+    golden model (CPU backend, single-step kernel, same Philox stream), compare, then restore
+    the state and step counter.  Returns the max |difference| over u and v."""
+    import copy
+
+    import numpy as np
+
+    from grayscott_amd.models.grayscott import GrayScott
+    from grayscott_amd.parallel.dist import DistContext
+
+    t0 = sim.step
+    u0, v0 = sim.get_fields()
+    sim.iterate(nsteps)
+    ug, vg = sim.get_fields()
+    cs = copy.copy(settings)
+    cs.backend, cs.fuse_steps = "CPU", 1
+    cpu = GrayScott(cs, dom, DistContext())
+    try:
+        cpu.init_fields()
+        cpu.set_fields(u0, v0)
+        cpu.set_step(t0)
+        cpu.iterate(nsteps)
+        uc, vc = cpu.get_fields()
+    finally:
+        cpu.close()
+    err = float(max(np.abs(ug - uc).max(), np.abs(vg - vc).max()))
+    sim.set_fields(u0, v0)
+    sim.set_step(t0)
+    return err
+
+
+def run(args) -> int:
     import torch
 
     from grayscott_amd.models.grayscott import GrayScott
-    from grayscott_amd.parallel.decomp import choose_dims, init_domain
+    from grayscott_amd.parallel.decomp import choose_dims, dims_create, init_domain
     from grayscott_amd.parallel.dist import init_from_env
     from grayscott_amd.utils.config import Settings, load_backend_and_lang
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            print(f"bench.py: --gpus {args.gpus} needs a torchrun launch with "
-                  f"--nproc-per-node {args.gpus}", file=sys.stderr)
-            return 2
     settings = Settings(L=args.L, steps=args.steps, plotgap=args.steps + args.warmup + 1,
                         F=0.02, k=0.048, dt=1.0, Du=0.2, Dv=0.1, noise=args.noise,
                         precision=args.precision, backend=args.backend, fuse_steps=args.fuse,
@@ -66,6 +138,7 @@ def main(argv=None) -> int:
     ctx = init_from_env("hip" if backend == "hip" else "cpu")
     dims = choose_dims(args.L, ctx.world_size, args.decomposition, backend)
     tuning = None
+    t_tune = time.perf_counter()
     if ctx.world_size > 1:
         # Verify every candidate multi-rank data path against the golden model, then time a
         # short run of each on this problem and keep the fastest (parallel/autotune.py): the
@@ -75,16 +148,32 @@ def main(argv=None) -> int:
         if args.decomposition != "auto" or args.fuse > 0:
             cands = [(dims, args.fuse)]
         log = (lambda m: print(f"bench.py: {m}", file=sys.stderr, flush=True))
-        tuning = tune_data_path(settings, ctx, args.L, backend, cands=cands, log=log)
+        tuning = tune_data_path(settings, ctx, args.L, backend, cands=cands, log=log,
+                                budget_s=args.tune_budget)
         dims = tuning["dims"]
         settings.fuse_steps = tuning["fuse"]
         settings.transport, settings.overlap = tuning["transport"], tuning["overlap"]
         os.environ.update(tuning["env"])
+    tuning_s = time.perf_counter() - t_tune
     dom = init_domain(args.L, ctx.world_size, ctx.rank, periodic=False, dims=dims)
     sim = GrayScott(settings, dom, ctx, use_fused=not args.no_fused_kernel)
     sim.init_fields()
     if args.init == "random":
         sim.randomize_fields(seed=2024)
+
+    check = {}
+    do_golden = (args.check == "golden" or
+                 (args.check == "auto" and ctx.world_size == 1 and backend == "hip"))
+    if do_golden and args.check_steps > 0:
+        t_chk = time.perf_counter()
+        err = golden_check(sim, settings, dom, args.check_steps)
+        err = ctx.allreduce(err, "max")
+        tol = 2e-5 if settings.dtype_name == "float32" else 1e-12
+        check.update(golden_steps=args.check_steps, max_abs_err=err, golden_tol=tol,
+                     golden_ok=bool(err < tol), golden_s=round(time.perf_counter() - t_chk, 2))
+        if not err < tol:
+            print(f"bench.py: golden check FAILED: max |gpu - golden| = {err:.3e} after "
+                  f"{args.check_steps} steps (tolerance {tol:g})", file=sys.stderr, flush=True)
 
     def sync():
         sim.synchronize()
@@ -93,6 +182,9 @@ def main(argv=None) -> int:
 
     sim.iterate(args.warmup)
     sync()
+    if (os.environ.get("GS_RAISE_AT_STEP") is not None and
+            int(os.environ.get("GS_FAIL_RANK", "-1")) in (-1, ctx.rank)):
+        raise RuntimeError(f"injected failure on rank {ctx.rank} (GS_RAISE_AT_STEP)")
     ctx.barrier()
     sync()
     t0 = time.perf_counter()
@@ -103,10 +195,21 @@ def main(argv=None) -> int:
     local = t1 - t0
     elapsed = ctx.allreduce(local, "max")
     stats = sim.global_stats()
+    world_info = ctx.gather_object(sim.device_info())
     cells = float(args.L) ** 3
     mlups = cells * args.steps / elapsed / 1e6
     if ctx.rank == 0:
-        dims = "x".join(str(d) for d in dom.dims)
+        dstr = "x".join(str(d) for d in dom.dims)
+        ref_grid = None
+        if tuning:
+            bal = dims_create(ctx.world_size)
+            rows = [r for r in tuning["table"] if r["dims"] == bal and r.get("ok")]
+            if rows:
+                r = min(rows, key=lambda r: r["ms_per_step"])
+                ref_grid = {"dims": bal, "fuse": r["fuse"], "overlapped": r.get("overlapped"),
+                            "ms_per_step": r["ms_per_step"],
+                            "mlups": round(cells / (r["ms_per_step"] * 1e-3) / 1e6, 1),
+                            "steps_timed": r.get("steps")}
         rec = {
             "metric": f"MLUPS (cell-updates/sec, whole node) at L={args.L} "
                       f"{'fp32' if settings.dtype_name == 'float32' else 'fp64'}",
@@ -128,8 +231,8 @@ def main(argv=None) -> int:
                 "L": args.L,
                 "global_batch": 1,
                 "seq_len": args.L,
-                "parallelism": (f"spatial-z-slabs {dims} ({sim.transport} plane halos, overlapped)"
-                                if sim.overlapped else f"spatial-3d {dims}"),
+                "parallelism": (f"spatial-z-slabs {dstr} ({sim.transport} plane halos, overlapped)"
+                                if sim.overlapped else f"spatial-3d {dstr}"),
                 "dims": dom.dims,
                 "local_extent": dom.proc_sizes,
                 "fuse_steps": sim.fuse,
@@ -140,14 +243,25 @@ def main(argv=None) -> int:
                 "noise": args.noise,
                 "backend": backend,
             },
+            "world": {
+                "ranks": ctx.world_size,
+                "rccl_nranks": world_info[0].get("rccl_nranks"),
+                "distinct_devices": len({w.get("pci") or w.get("device") for w in world_info}),
+                "per_rank": world_info,
+            },
+            "tuning_s": round(tuning_s, 2),
+            "wall_s": round(time.perf_counter() - T_START, 2),
             "data_path_tuning": tuning and tuning["table"],
+            "reference_grid": ref_grid,
             "check": {"mean_u": stats["mean_u"], "mean_v": stats["mean_v"],
-                      "finite": all(map(lambda x: x == x, stats.values()))},
+                      "finite": all(map(lambda x: x == x, stats.values())), **check},
         }
+        if ref_grid is not None and ctx.world_size == 8 and ref_grid["dims"] == [2, 2, 2]:
+            rec["config3_2x2x2"] = ref_grid
         print(json.dumps(rec), flush=True)
     sim.close()
     ctx.finalize()
-    return 0
+    return 0 if check.get("golden_ok", True) else 1
 
 
 if __name__ == "__main__":

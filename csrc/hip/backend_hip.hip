@@ -233,17 +233,64 @@ class HipBackend final : public gs::Backend {
   // best {cfg, sched} for one launch shape; false if tuning is disabled / unsupported
   // fixed_cfg >= 0 keeps the tile shape and tunes the schedule only (a ring launch must use
   // the tile grid of the inner launch it complements)
+  // Process-wide cache of tuning results per launch shape: data-path tuning (and the golden
+  // checks) build many engines over the same sub-domain shape; each would re-time the same
+  // candidates.  GS_AUTOTUNE_CACHE=0 disables it.
+  struct TuneKey {
+    int tsize, nx, ny, nz, H, periodic, noise, n, fixed;
+    Part pt;
+    bool operator==(const TuneKey& o) const {
+      return tsize == o.tsize && nx == o.nx && ny == o.ny && nz == o.nz && H == o.H &&
+             periodic == o.periodic && noise == o.noise && n == o.n && fixed == o.fixed &&
+             pt.zlo0 == o.pt.zlo0 && pt.zlen0 == o.pt.zlen0 && pt.zlo1 == o.pt.zlo1 &&
+             pt.zlen1 == o.pt.zlen1 && pt.tiles == o.pt.tiles && pt.sides == o.pt.sides;
+    }
+  };
+  struct TuneVal {
+    int cfg, sched;
+    float ms;
+  };
+  static std::vector<std::pair<TuneKey, TuneVal>>& tune_cache() {
+    static std::vector<std::pair<TuneKey, TuneVal>> c;
+    return c;
+  }
   bool autotune_part(int src, int dst, int n, int64_t t, const Part& pt, int* cfg, int* sched,
                      float* ms_best, int fixed_cfg = -1) {
     if (!autotune_enabled()) return false;
+    static const bool use_cache = !(getenv("GS_AUTOTUNE_CACHE") && atoi(getenv("GS_AUTOTUNE_CACHE")) == 0);
+    const TuneKey key{(int)sizeof(T), g_.nx, g_.ny, g_.nz, g_.H, g_.periodic,
+                      p_.noise != 0.0 ? 1 : 0, n, fixed_cfg, pt};
+    if (use_cache)
+      for (const auto& kv : tune_cache())
+        if (kv.first == key) {
+          *cfg = kv.second.cfg;
+          *sched = kv.second.sched;
+          *ms_best = kv.second.ms;
+          return true;
+        }
+    if (!autotune_run(src, dst, n, t, pt, cfg, sched, ms_best, fixed_cfg)) return false;
+    if (use_cache) tune_cache().push_back({key, TuneVal{*cfg, *sched, *ms_best}});
+    return true;
+  }
+  bool autotune_run(int src, int dst, int n, int64_t t, const Part& pt, int* cfg, int* sched,
+                    float* ms_best, int fixed_cfg) {
     struct Cand { int cfg, sched; };
     std::vector<Cand> cands;
-    const bool variants = !g_.periodic && p_.noise != 0.0;  // tile variants instantiated here
+    // tile variants are instantiated for the production path only (fused.hpp run_fused_cfg)
+    const bool variants = !g_.periodic && p_.noise != 0.0 && gsk::philox_q32(g_);
     std::vector<int> cfgs;
-    if (fixed_cfg >= 0) cfgs = {fixed_cfg};
-    else if (!variants) cfgs = {0};
-    else if (sizeof(T) == 4) cfgs = {0, 1, 2, 3, 5, 8, 12, 16, 17, 19, 20, 30, 31, 33};
-    else cfgs = {0, 1, 13, 15, 19, 32, 33};
+    if (fixed_cfg >= 0) {
+      cfgs = {fixed_cfg};
+    } else if (!variants) {
+      cfgs = {0};
+    } else {
+      int nt = 0;
+      const gsk::FusedCfgEntry* tab = gsk::fused_cfg_table(&nt);
+      const int dflt = sizeof(T) == 4 ? gsk::fused_cfg_lookup("4x12:2s") : gsk::fused_cfg_lookup("4x8:1s");
+      for (int i = 0; i < nt; ++i)
+        if ((sizeof(T) == 4 ? tab[i].f32 : tab[i].f64) && i != dflt && !strstr(tab[i].name, "-abl"))
+          cfgs.push_back(i);
+    }
     const int nsched = pt.zlen1 > 0 ? 1 : 3;  // two z-runs always use schedule 0
     for (int c : cfgs)
       for (int sc = 0; sc < nsched; ++sc) cands.push_back({c, sc});
@@ -399,6 +446,17 @@ class HipBackend final : public gs::Backend {
     comm_ = nullptr;
   }
 
+  // what RCCL sees: communicator size, this rank in it, the device it drives
+  void comm_info(int32_t* out3) const {
+    out3[0] = out3[1] = out3[2] = -1;
+    if (!comm_) return;
+    int n = -1, r = -1, d = -1;
+    NCCL_CHECK(ncclCommCount(comm_, &n));
+    NCCL_CHECK(ncclCommUserRank(comm_, &r));
+    NCCL_CHECK(ncclCommCuDevice(comm_, &d));
+    out3[0] = n; out3[1] = r; out3[2] = d;
+  }
+
   void init_comm(const ncclUniqueId& id, int nranks, int rank) {
     SharedComm& sc = shared_comm();
     if (sc.comm && sc.nranks == nranks && sc.rank == rank &&
@@ -470,6 +528,38 @@ int gs_rccl_unique_id(char* out, int32_t cap) {
   }
 }
 
+// {communicator size, rank in it, HIP device} of the engine's RCCL communicator (-1: none)
+int gs_rccl_info(gs_engine* e, int32_t dtype, int32_t* out3) {
+  try {
+    gs::Backend* b = e->eng->backend();
+    if (dtype == gs::kF32) static_cast<HipBackend<float>*>(b)->comm_info(out3);
+    else static_cast<HipBackend<double>*>(b)->comm_info(out3);
+    return 0;
+  } catch (const std::exception& ex) {
+    g_gs_err = ex.what();
+    return -1;
+  }
+}
+
+// Abort the process-wide RCCL communicator (job-wide failure handling: a rank that is about to
+// exit on an error aborts its communicator first, so peers blocked in a halo exchange see an
+// error instead of waiting for a message that never comes).  Engines must not be used after.
+int gs_rccl_abort(void) {
+  SharedComm& sc = shared_comm();
+  if (!sc.comm) return 0;
+  const ncclResult_t r = ncclCommAbort(sc.comm);
+  sc = SharedComm{};
+  return r == ncclSuccess ? 0 : -1;
+}
+
+// PCI bus id of the current HIP device ("0000:05:00.0"); returns its length or -1
+int gs_device_pci(char* out, int32_t cap) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return -1;
+  if (hipDeviceGetPCIBusId(out, cap, dev) != hipSuccess) return -1;
+  return (int)strlen(out);
+}
+
 int gs_rccl_init(gs_engine* e, const char* uid, int32_t nranks, int32_t rank, int32_t dtype) {
   try {
     ncclUniqueId id;
@@ -532,6 +622,10 @@ int gs_fused_choice(gs_engine* e, int32_t n, int32_t dtype, int32_t* out2, float
 
 extern "C" const char* gs_fused_cfg_name(int32_t index) {
   int n = 0;
-  const char* const* names = gsk::fused_cfg_names(&n);
-  return (index >= 0 && index < n) ? names[index] : nullptr;
+  const gsk::FusedCfgEntry* t = gsk::fused_cfg_table(&n);
+  return (index >= 0 && index < n) ? t[index].name : nullptr;
 }
+
+// index of a fused-kernel configuration name in this build (-1: unknown, e.g. an ablation
+// variant in the production library)
+extern "C" int gs_fused_cfg_lookup(const char* name) { return gsk::fused_cfg_lookup(name); }

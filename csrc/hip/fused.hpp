@@ -2,20 +2,34 @@
 // k_fused: T time levels per HBM pass over the interior (temporal blocking) for gfx950.
 // Included inside namespace gsk by kernels.hpp, after stencil.hpp.
 //
-// Work unit = one (tile, z-plane) pair; the units are split evenly over a persistent grid
-// of `occupancy x CUs` workgroups, each walking one or two contiguous z-segments.
-// Tile = 64 columns (one lane each) x WAVES*ROWS rows of level-0 data (ghosts included);
-// it yields (64-2T) x ystep interior outputs.  A segment [z0,z1) streams level-0 planes
-// z0-T .. z1+T-1; at iteration p level l produces plane p-l; level T is stored.
+// The update being computed is the reference's calculate! (Simulation_CPU.jl:92-112), T steps
+// per pass: HBM is read once and written once per T steps.
 //
-// Register plan (no rotation copies): level-0 planes live in a 3-deep ring LD[3] (plane p,
-// p-1 and the prefetch of p+1); level-l outputs in a 2-deep ring OUT[l][2]; per consumer
-// level a running partial sum A (xy-neighbours of plane q-1 plus plane q-2).  The loop is
-// unrolled by the ring period (6) so every ring index is a compile-time constant.
-// Memory goes through buffer descriptors built per plane: 32-bit lane offsets, no address
-// VGPRs, out-of-range loads return 0 and masked stores use an out-of-range offset.
-// Intermediate levels outside the global domain (non-periodic) are reset to the boundary
-// value of their time level -- what the single-step path reads from its ghost shell.
+// Work unit = one (tile, z-plane) pair; the units are split over a grid of workgroups, each
+// walking one or more contiguous z-segments.  Tile = 64 columns (one lane each) x WAVES*ROWS
+// rows of level-0 data (ghosts included); it yields (64-2T) x ystep interior outputs.  A segment
+// [z0,z1) streams level-0 planes z0-T .. z1+T-1.
+//
+// Register plan (no rotation copies): level-0 planes live in a ring LD[PF+2] (plane p, p-1 and
+// the prefetches); level-l outputs in a ring OUT[l][NS]; per consumer level a running partial
+// sum A (xy-neighbours of plane q-1 plus plane q-2).  The loop is unrolled by the ring period
+// so every ring index is a compile-time constant.  Memory goes through buffer descriptors of
+// one storage plane each, walked by a running 64-bit plane pointer: 32-bit lane offsets, no
+// address VGPRs, out-of-range loads return 0 and masked stores use an out-of-range offset.
+// Intermediate levels outside the global domain (non-periodic) are reset to the boundary value
+// of their time level -- what the single-step path reads from its ghost shell.
+//
+// Energy per cell update is what limits this kernel on random data (profiles/
+// r2_power_probe.txt: the same dispatch runs at the full clock on smooth data and ~20 % slower
+// on rough data, with identical cycle counts), so every VALU instruction counts:
+//  * fp32 arithmetic on the interleaved (u, v) pairs is packed (v_pk_add/v_pk_mul/v_pk_fma_f32);
+//  * the x-neighbour pair sum is one DPP move + one DPP add;
+//  * the LDS row exchange wraps around (wave 0 reads the last wave's row: a tile-halo row whose
+//    value never reaches an output), so the exchange has no branches or register copies;
+//  * waves whose rows are all outside a level's dependency cone skip that level (the row slack
+//    of the 4-row noise quads: at T=3 the last wave of a 48-row tile skips levels 2 and 3);
+//  * Philox rounds 1-3 keep their wave-uniform words on the SALU when the global counter fits
+//    32 bits (Q32: Lx * ceil(Ly/4) * Lz < 2^32, every grid up to L = 2580).
 #pragma once
 
 struct FusedArgs {
@@ -25,93 +39,85 @@ struct FusedArgs {
   int32_t ybase;
   int32_t bcfix;
   int64_t units;
-  int32_t sched;   // 0: units split evenly; 1: XCD-grouped z-chunks walked in lockstep
-  int32_t nchunk;  // sched 1: z-chunks per tile
+  int32_t sched;   // 0: units split evenly; 1: XCD-grouped z-chunks; 2: persistent XCD rounds
+  int32_t nchunk;  // sched 1/2: z-chunks per tile
   int32_t ntiles;  // tiles enumerated (ntx * nty, or the inner / ring subset)
   // tile subset (comm/compute overlap of packed halos): 0 all tiles, 1 the inner rectangle
   // [itx0, itx1) x [ity0, ity1) (no input cell within reach of a fresh halo), 2 its ring
   int32_t tmode;
   int32_t sides;  // bit0/1/2/3: neighbour at -x/+x/-y/+y (whose halo is in flight)
   int32_t itx0, itx1, ity0, ity1;
-  int32_t grpM;    // sched 1: workgroups per XCD group (grid = 8 * grpM)
+  int32_t grpM;    // sched 1/2: workgroups per XCD group (grid = 8 * grpM)
   int32_t cfg;     // tile/prefetch configuration index (fused_cfg_names)
   int64_t t;
-  int64_t buf_bytes;  // bytes of one state buffer (descriptor range)
   int32_t reserve;    // workgroup slots to leave free (comm kernels running alongside)
+  int32_t q32;        // Philox counter fits 32 bits (host check)
   // output z-runs [zlo[r], zlo[r] + zlen[r]) (zlen[1] may be 0); a tile's units enumerate the
   // planes of run 0 then run 1 (nzv = zlen[0] + zlen[1] units per tile)
   int32_t zlo[2], zlen[2];
   int32_t nzv;
 };
 
-// Folded update coefficients: u' = au*u + asu*su + ac - dt*uvv + ar*r ; v' = bv*v + bsv*sv + dt*uvv
+template <typename T> struct PairT;
+template <> struct PairT<float> { typedef float type __attribute__((ext_vector_type(2))); };
+template <> struct PairT<double> { typedef double type __attribute__((ext_vector_type(2))); };
+
+// Folded update coefficients:
+//   u' = au*u + asu*su + ac - dt*uvv + ar*r ;  v' = bv*v + bsv*sv + dt*uvv
+// held as (u, v) pairs for the packed fp32 form: P = kd*uvv + kc ; P += ks*s ; P += kc2*c.
 template <typename T>
 struct FoldCoef {
-  T au, asu, ac, ar, dt, bv, bsv;
+  using P2 = typename PairT<T>::type;
+  P2 kd, kc, ks, kcc;  // (-dt, dt), (ac, 0), (asu, bsv), (au, bv)
+  T ar;                // dt * noise
 };
 
 template <typename T>
 inline FoldCoef<T> make_fold(const gs::Params& p) {
   FoldCoef<T> f;
-  f.au = (T)(1.0 - p.dt * (p.Du + p.F));
-  f.asu = (T)(p.dt * p.Du / 6.0);
-  f.ac = (T)(p.dt * p.F);
+  f.kd = typename PairT<T>::type{(T)(-p.dt), (T)p.dt};
+  f.kc = typename PairT<T>::type{(T)(p.dt * p.F), (T)0};
+  f.ks = typename PairT<T>::type{(T)(p.dt * p.Du / 6.0), (T)(p.dt * p.Dv / 6.0)};
+  f.kcc = typename PairT<T>::type{(T)(1.0 - p.dt * (p.Du + p.F)),
+                                  (T)(1.0 - p.dt * (p.Dv + p.F + p.k))};
   f.ar = (T)(p.dt * p.noise);
-  f.dt = (T)p.dt;
-  f.bv = (T)(1.0 - p.dt * (p.Dv + p.F + p.k));
-  f.bsv = (T)(p.dt * p.Dv / 6.0);
   return f;
 }
 
 typedef unsigned int gs_u2 __attribute__((ext_vector_type(2)));
 typedef unsigned int gs_u4 __attribute__((ext_vector_type(4)));
 
-// Descriptor for the plane starting `off_bytes` into a buffer of `total_bytes`.  The range is
-// empty when the plane is disabled (total_bytes == 0) or starts outside the buffer, so every
-// access through it is dropped (loads return 0) -- never a wild address.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const void* base, int64_t off_bytes,
-                                                             int64_t total_bytes) {
-  const int64_t rem = total_bytes - off_bytes;
-  const bool inside = total_bytes > 0 && off_bytes >= 0 && rem > 0;
-  const int nrec = inside ? (int)(rem > 0x7ffffff0LL ? 0x7ffffff0LL : rem) : 0;
-  return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)base + off_bytes), 0, nrec,
-                                           0x00020000);
+// Descriptor for one storage plane starting at `base` (bytes `nbytes`; 0 = disabled: every
+// access through it is dropped, loads return 0).  Accesses past the plane's end -- tile rows
+// beyond the ghost layer -- read 0 instead of the next plane's data: neither ever reaches a
+// stored output (an output depends on rows within T <= H of it).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const char* base, int nbytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, nbytes, 0x00020000);
 }
 
-// Descriptor for storage plane `plane` (0-based, ghosts included) of a buffer of `nplanes`
-// planes of `pzb` bytes, covering that plane only.  All the checks are 32-bit and wave-uniform
-// (SALU); the 64-bit form above needs VALU compares.  Accesses past the plane's end -- tile
-// rows beyond the ghost layer -- read 0 instead of the next plane's data: neither ever reaches
-// a stored output (an output depends on rows within T <= H of it).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc_p(const void* base, int plane,
-                                                               int nplanes, int64_t pzb, bool on) {
-  const bool inside = on && (unsigned)plane < (unsigned)nplanes;
-  const int nrec = inside ? (int)(pzb > 0x7ffffff0LL ? 0x7ffffff0LL : pzb) : 0;
-  return __builtin_amdgcn_make_buffer_rsrc(
-      (void*)((const char*)base + (int64_t)(inside ? plane : 0) * pzb), 0, nrec, 0x00020000);
+__device__ __forceinline__ PairT<float>::type bload(__amdgpu_buffer_rsrc_t r, int voff,
+                                                    PairT<float>::type*) {
+  const gs_u2 v = __builtin_amdgcn_raw_buffer_load_b64(r, voff, 0, 0);
+  return PairT<float>::type{__uint_as_float(v.x), __uint_as_float(v.y)};
 }
-
-__device__ __forceinline__ float2 bload(__amdgpu_buffer_rsrc_t r, int voff, int soff, float2*) {
-  const gs_u2 v = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
-  return make_float2(__uint_as_float(v.x), __uint_as_float(v.y));
+__device__ __forceinline__ PairT<double>::type bload(__amdgpu_buffer_rsrc_t r, int voff,
+                                                     PairT<double>::type*) {
+  const gs_u4 v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0);
+  return PairT<double>::type{__longlong_as_double(((long long)v.y << 32) | v.x),
+                             __longlong_as_double(((long long)v.w << 32) | v.z)};
 }
-__device__ __forceinline__ double2 bload(__amdgpu_buffer_rsrc_t r, int voff, int soff, double2*) {
-  const gs_u4 v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
-  return make_double2(__longlong_as_double(((long long)v.y << 32) | v.x),
-                      __longlong_as_double(((long long)v.w << 32) | v.z));
-}
-__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, int voff, int soff, float2 c) {
+__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, int voff, PairT<float>::type c) {
   gs_u2 v;
   v.x = __float_as_uint(c.x);
   v.y = __float_as_uint(c.y);
-  __builtin_amdgcn_raw_buffer_store_b64(v, r, voff, soff, 0);
+  __builtin_amdgcn_raw_buffer_store_b64(v, r, voff, 0, 0);
 }
-__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, int voff, int soff, double2 c) {
+__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, int voff, PairT<double>::type c) {
   const unsigned long long a = (unsigned long long)__double_as_longlong(c.x);
   const unsigned long long b = (unsigned long long)__double_as_longlong(c.y);
   gs_u4 v;
   v.x = (unsigned)a; v.y = (unsigned)(a >> 32); v.z = (unsigned)b; v.w = (unsigned)(b >> 32);
-  __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, soff, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, 0, 0);
 }
 
 // a ^ b ^ c in one gfx950 instruction (the compiler does not form v_bitop3 from xor chains)
@@ -121,40 +127,67 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return r;
 }
 
-// Device form of gs::noise_block (same stream, bit for bit).
-//  * The 10-round key schedule is rebuilt from an opaque copy of the seed at every call:
-//    otherwise the compiler hoists the 20 loop-invariant key words out of the plane loop, runs
-//    out of SGPRs and spills them to VGPR lanes (one v_readlane per use in the hot loop).
-//    Rebuilt, they are 20 SALU adds.
-//  * Rounds 1-2 still see wave-uniform counter words (step, and its products), which the
-//    compiler folds on the SALU; from round 3 on every word varies per lane and each output
-//    word's two xors become one v_bitop3.
-template <bool kOpaqueStep = true>
-__device__ __forceinline__ gs::U4 noise_block_dev(int64_t gx, int64_t gy4, int64_t gz, int64_t Lx,
-                                                  int64_t Ly, uint64_t step, uint64_t seed) {
+constexpr uint32_t kPhM0 = 0xD2511F53u, kPhM1 = 0xCD9E8D57u;
+constexpr uint32_t kPhW0 = 0x9E3779B9u, kPhW1 = 0xBB67AE85u;
+
+// Device Philox4x32-10 of counter (c0, c1, step_lo, step_hi): gs::noise_block's stream, bit
+// for bit.  The key schedule and the step words are rebuilt from opaque copies at every call:
+// otherwise the compiler hoists their loop-invariant products out of the plane loop, runs out
+// of SGPRs and spills them to VGPR lanes (a v_readlane per use).  Rebuilt, they are a few
+// SALU ops.
+//   Q32 (c1 = 0): round 1's second product and the round-2 first product see only
+//   wave-uniform words, so rounds 1-3 cost 1 + 3 + 4 VALU instead of 4 + 4 + 4.
+template <bool Q32>
+__device__ __forceinline__ gs::U4 philox_dev(uint32_t c0, uint32_t c1, uint64_t step,
+                                             uint64_t seed) {
   uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-  asm volatile("" : "+s"(k0), "+s"(k1));
-  const uint64_t Ly4 = ((uint64_t)Ly + 3) >> 2;
-  const uint64_t q = (uint64_t)gx + (uint64_t)Lx * ((uint64_t)gy4 + Ly4 * (uint64_t)gz);
-  uint32_t c0 = (uint32_t)q, c1 = (uint32_t)(q >> 32), c2 = (uint32_t)step,
-           c3 = (uint32_t)(step >> 32);
-  // the step words are wave-uniform and loop-invariant per time level: without this the
-  // compiler hoists their round-1/2 products out of the plane loop and spills them to VGPR
-  // lanes (a v_readlane per use); recomputed they are a few SALU ops
-  if constexpr (kOpaqueStep) asm volatile("" : "+s"(c2), "+s"(c3));
+  uint32_t s0 = (uint32_t)step, s1 = (uint32_t)(step >> 32);
+  asm volatile("" : "+s"(k0), "+s"(k1), "+s"(s0), "+s"(s1));
+  uint32_t c2, c3;
+  if constexpr (Q32) {
+    // round 1: (c0 lane, 0, s0, s1)
+    const uint64_t m0 = (uint64_t)kPhM0 * c0;  // lane
+    const uint64_t m1 = (uint64_t)kPhM1 * s0;  // uniform
+    const uint32_t u0 = (uint32_t)(m1 >> 32) ^ k0;            // uniform (c1 = 0)
+    const uint32_t l2 = (uint32_t)(m0 >> 32) ^ (s1 ^ k1);     // lane
+    const uint32_t u1 = (uint32_t)m1;                          // uniform
+    const uint32_t l3 = (uint32_t)m0;                          // lane
+    k0 += kPhW0; k1 += kPhW1;
+    // round 2: (u0, u1, l2, l3)
+    const uint64_t n0 = (uint64_t)kPhM0 * u0;  // uniform
+    const uint64_t n1 = (uint64_t)kPhM1 * l2;  // lane
+    c0 = (uint32_t)(n1 >> 32) ^ (u1 ^ k0);                      // lane
+    c2 = l3 ^ ((uint32_t)(n0 >> 32) ^ k1);                      // lane
+    c1 = (uint32_t)n1;                                           // lane
+    const uint32_t u3 = (uint32_t)n0;                            // uniform
+    k0 += kPhW0; k1 += kPhW1;
+    // round 3: (c0, c1, c2 lane; u3 uniform)
+    const uint64_t p0 = (uint64_t)kPhM0 * c0;
+    const uint64_t p1 = (uint64_t)kPhM1 * c2;
+    c0 = xor3((uint32_t)(p1 >> 32), c1, k0);
+    c2 = (uint32_t)(p0 >> 32) ^ (u3 ^ k1);
+    c1 = (uint32_t)p1;
+    c3 = (uint32_t)p0;
+    k0 += kPhW0; k1 += kPhW1;
+  } else {
+    c2 = s0;
+    c3 = s1;
 #pragma unroll
-  for (int r = 0; r < 10; ++r) {
-    if (r < 2) {
+    for (int r = 0; r < 3; ++r) {
       gs::philox_round(c0, c1, c2, c3, k0, k1);
-    } else {
-      const uint64_t m0 = (uint64_t)0xD2511F53u * c0;
-      const uint64_t m1 = (uint64_t)0xCD9E8D57u * c2;
-      const uint32_t n0 = xor3((uint32_t)(m1 >> 32), c1, k0);
-      const uint32_t n2 = xor3((uint32_t)(m0 >> 32), c3, k1);
-      c0 = n0; c1 = (uint32_t)m1; c2 = n2; c3 = (uint32_t)m0;
+      k0 += kPhW0;
+      k1 += kPhW1;
     }
-    k0 += 0x9E3779B9u;
-    k1 += 0xBB67AE85u;
+  }
+#pragma unroll
+  for (int r = 3; r < 10; ++r) {
+    const uint64_t m0 = (uint64_t)kPhM0 * c0;
+    const uint64_t m1 = (uint64_t)kPhM1 * c2;
+    const uint32_t n0 = xor3((uint32_t)(m1 >> 32), c1, k0);
+    const uint32_t n2 = xor3((uint32_t)(m0 >> 32), c3, k1);
+    c0 = n0; c1 = (uint32_t)m1; c2 = n2; c3 = (uint32_t)m0;
+    k0 += kPhW0;
+    k1 += kPhW1;
   }
   return gs::U4{c0, c1, c2, c3};
 }
@@ -164,43 +197,36 @@ __device__ __forceinline__ gs::U4 noise_block_dev(int64_t gx, int64_t gy4, int64
 //   PF           : level-0 prefetch distance in planes (register ring of PF+2 planes)
 //   SKEW         : level l consumes level l-1's output of the previous iteration, so all
 //                  levels share ONE workgroup barrier per plane (output ring of 3)
+//   Q32          : the Philox counter fits 32 bits (rounds 1-3 partly on the SALU)
+//   ABL          : ablations for timing experiments, GS_ABLATION builds only (results are
+//                  WRONG by design): bit0 no workgroup barriers, bit1 every level-0 load reads
+//                  plane 0 (L2-resident)
 constexpr int gs_gcd(int a, int b) { return b == 0 ? a : gs_gcd(b, a % b); }
 constexpr int gs_lcm(int a, int b) { return a / gs_gcd(a, b) * b; }
 
 template <typename T_, int TL_, int ROWS_, int WAVES_, int PF_, bool PERIODIC_, bool NOISE_,
-          int MINW_ = 1, bool SKEW_ = false, int ABL_ = 0>
+          bool SKEW_ = false, bool Q32_ = true, int ABL_ = 0>
 struct FCfg {
-  static constexpr int MINW = MINW_;  // __launch_bounds__ min waves per SIMD
   using T = T_;
-  using V2 = typename Vec2<T>::type;
+  using V2 = typename PairT<T>::type;
   static constexpr int TL = TL_, ROWS = ROWS_, WAVES = WAVES_, PF = PF_;
-  static constexpr bool PERIODIC = PERIODIC_, NOISE = NOISE_, SKEW = SKEW_;
-  // the noise coefficient dt*noise*2^-31 in a VGPR (saves the uniform's v_mul; an SGPR
-  // copy spilled, profiles/r1_ab_noise_fold.txt); ABL bit 6 restores the separate scale
-  static constexpr bool FOLD31 = !(ABL_ & 64);
-  // fp32 T=3: x-neighbour pair sum as one DPP move + one DPP add (lane_pair_sum): -36 VALU
-  // and -16 VGPRs per unrolled period, +1.8 % at L=512 (profiles/r1_ab_xsum_dpp.txt); neutral
-  // at T=2, which keeps the compiler's form.  ABL bit 7 restores it at T=3.
-  static constexpr bool XSUM_DPP = sizeof(T_) == 4 && TL_ == 3 && !(ABL_ & 128);
-  // ablation (timing experiments only, results are WRONG): bit0 = no workgroup barriers,
-  // bit1 = every level-0 load reads plane 0 (L2-resident); bit2 (results exact) = hoistable
-  // Philox key schedule (the pre-noise_block_dev code generation); bit3 (results exact) =
-  // hoistable step words in the Philox counter (before the opaque-step change); bit4 (exact) =
-  // float2 LDS reads split by the compiler into two ds_read_b32 (before lds_load2); bit5
-  // (exact) = 64-bit buffer-range descriptors (before plane_rsrc_p); bit6 (exact) = separate
-  // 2^-31 noise scale (before FOLD31); bit7 (exact) = compiler-formed x-neighbour sums at T=3
-  // (before XSUM_DPP)
+  static constexpr bool PERIODIC = PERIODIC_, NOISE = NOISE_, SKEW = SKEW_, Q32 = Q32_;
   static constexpr int ABL = ABL_;
   static constexpr int R = PF + 2;                    // level-0 ring slots
   static constexpr int NS = SKEW ? 3 : 2;             // level-l output ring / xch buffers
   static constexpr int PERIOD = gs_lcm(R, NS);
   static constexpr int NO = TL > 1 ? TL - 1 : 1;
+  static constexpr int RT = ROWS * WAVES;                 // tile rows
+  static constexpr int YSTEP = (RT - 2 * TL) & ~3;        // output rows per tile
+  // rows of output level L = l + 1 that some stored output depends on: [l + 1, hi(l)]
+  static constexpr int need_hi(int l) { return 2 * TL + YSTEP - 2 - l; }
 };
 
 template <class C>
 struct FusedState {
   using V2 = typename C::V2;
-  typename C::T ar31;  // dt * noise * 2^-31 held in a VGPR (C::FOLD31)
+  typename C::T ar31;  // dt * noise * 2^-31 held in a VGPR (an SGPR copy spills)
+  typename C::V2 kc;   // (dt F, 0) held in VGPRs (the first packed FMA's addend)
   V2 LD[C::R][C::ROWS];
   V2 OUT[C::NO][C::NS][C::ROWS];
   V2 A[C::TL][C::ROWS];
@@ -209,10 +235,15 @@ struct FusedState {
 // Per-segment constants (wave-uniform values and the lane's offsets).
 struct FusedSeg {
   int p, pend, ldend, z0;
-  int lane, wave;
+  int lane, wave, wup, wdn;  // LDS exchange partners (wrap around)
+  int skip;                  // bit l: this wave's rows are outside level l+1's cone
   int voff, svoff, pitchb;
   int srow0, srow1;
+  int pzb;                   // bytes per storage plane
+  const char* ldp;           // source plane of the next prefetch (p + PF)
+  char* stp;                 // destination plane of this iteration's last-level output
   int64_t gx, gxu, gy0;
+  uint32_t gx32;             // Q32 noise counter: lane part
   bool edge;
 };
 
@@ -222,10 +253,9 @@ __device__ __forceinline__ int64_t gwrap(int64_t v, int64_t L) {
   else return v;
 }
 
-// left + right x-neighbours in two instructions: one DPP move and one DPP add (the compiler
-// pairs the u and v halves into v_pk_add_f32 instead and keeps both moves).  Same rounding
-// as lane_from_left(v) + lane_from_right(v).  The leading s_nop covers the VALU-write ->
-// DPP-read hazard the compiler cannot see through inline asm.
+// left + right x-neighbours in two instructions: one DPP move and one DPP add.  Same rounding
+// as lane_from_left(v) + lane_from_right(v).  The leading s_nop covers the VALU-write -> DPP
+// read hazard the compiler cannot see through inline asm.
 __device__ __forceinline__ float lane_pair_sum(float v) {
   float t, r;
   asm volatile(
@@ -236,14 +266,58 @@ __device__ __forceinline__ float lane_pair_sum(float v) {
       : "v"(v));
   return r;
 }
-
-// One (u, v) pair from LDS as a single 8-byte ds_read_b64 (the compiler otherwise splits a
-// float2 into two ds_read_b32 at an 8-byte lane stride: 2-way bank conflicts).
-__device__ __forceinline__ float2 lds_load2(const float2* p) {
-  const uint64_t b = *reinterpret_cast<const uint64_t*>(__builtin_assume_aligned(p, 8));
-  return make_float2(__uint_as_float((uint32_t)b), __uint_as_float((uint32_t)(b >> 32)));
+__device__ __forceinline__ double lane_pair_sum(double v) {
+  return lane_from_left(v) + lane_from_right(v);
 }
-__device__ __forceinline__ double2 lds_load2(const double2* p) { return *p; }
+
+// v[lane-1] + v[lane+1] + s in two DPP adds (the right neighbour is added to s first):
+// folds the y/z partial sum into the x-neighbour instructions.
+__device__ __forceinline__ float lane_pair_sum_add(float v, float s) {
+  float t, r;
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_add_f32_dpp %1, %2, %3 wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %0, %2, %1 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+      : "=v"(r), "=&v"(t)
+      : "v"(v), "v"(s));
+  return r;
+}
+__device__ __forceinline__ double lane_pair_sum_add(double v, double s) {
+  return lane_from_left(v) + lane_from_right(v) + s;
+}
+
+// One (u, v) pair from LDS as a single 8-byte ds_read_b64.
+__device__ __forceinline__ PairT<float>::type lds_load2(const PairT<float>::type* p) {
+  const uint64_t b = *reinterpret_cast<const uint64_t*>(__builtin_assume_aligned(p, 8));
+  return PairT<float>::type{__uint_as_float((uint32_t)b), __uint_as_float((uint32_t)(b >> 32))};
+}
+__device__ __forceinline__ PairT<double>::type lds_load2(const PairT<double>::type* p) {
+  return *p;
+}
+
+// The cell update of one level: neighbour sums, reaction, noise, Euler step, and the running
+// partial sum for the next plane.  xs: x-neighbour pair sums, ym/yp: y-neighbours, in: this
+// plane, c: the centre (plane before), w: the Philox word.
+template <class C>
+__device__ __forceinline__ typename C::V2 cell_update(typename C::V2& A, typename C::V2 in,
+                                                      typename C::V2 c, typename C::V2 ym,
+                                                      typename C::V2 yp, const FoldCoef<typename C::T>& f,
+                                                      typename C::T ar31, typename C::V2 kc,
+                                                      uint32_t w) {
+  using T = typename C::T;
+  using V2 = typename C::V2;
+  const V2 s = A + in;
+  const V2 yz = (ym + yp) + c;
+  A = V2{lane_pair_sum_add(in.x, yz.x), lane_pair_sum_add(in.y, yz.y)};
+  // uvv in both halves: (cu cv, cv cv) then (cu cv cv, cu cv cv)
+  const V2 t = c * c.yy;
+  const V2 uvv = t.xx * c.yy;
+  V2 P = __builtin_elementwise_fma(f.kd, uvv, kc);
+  P = __builtin_elementwise_fma(f.ks, s, P);
+  P = __builtin_elementwise_fma(f.kcc, c, P);
+  if constexpr (C::NOISE) P.x = fma(ar31, (T)(int32_t)w, P.x);
+  return P;
+}
 
 // One pipeline iteration p (i = p - pstart).  IR = i % R, IS = i % NS.
 // Non-skewed: level l+1 is computed from level l of the SAME iteration (one barrier per level).
@@ -253,25 +327,23 @@ template <class C, typename T, int IR, int IS>
 __device__ __forceinline__ void fused_iter(FusedState<C>& S,
                                            typename C::V2 (*xch)[C::NS][C::WAVES][2][64],
                                            const FusedArgs& a, const FoldCoef<T>& f,
-                                           uint64_t seed, const typename C::V2* src,
-                                           typename C::V2* dst, const FusedSeg& sg) {
+                                           uint64_t seed, FusedSeg& sg) {
   using V2 = typename C::V2;
-  constexpr int ROWS = C::ROWS, WAVES = C::WAVES, TL = C::TL, NS = C::NS;
+  constexpr int ROWS = C::ROWS, TL = C::TL, NS = C::NS;
   const Geom& g = a.g;
   const int p = sg.p;
-  const int64_t PZB = gs::plane_elems(g) * (int64_t)sizeof(V2);
   // prefetch level-0 plane p+PF into the ring slot of plane p-2.  Issued unconditionally
   // (an empty descriptor past the segment) so every iteration has the same VMEM count and
   // the compiler's s_waitcnt vmcnt(N) can leave the prefetch in flight.
   {
     const bool pf_ok = p + C::PF < sg.ldend;
     const __amdgpu_buffer_rsrc_t r =
-        (C::ABL & 32) ? plane_rsrc(src, (C::ABL & 2) ? 0 : (int64_t)(p + C::PF + g.H) * PZB,
-                                   pf_ok ? a.buf_bytes : 0)
-                      : plane_rsrc_p(src, (C::ABL & 2) ? 0 : p + C::PF + g.H, g.pz, PZB, pf_ok);
+        plane_rsrc((C::ABL & 2) ? sg.ldp - (int64_t)(p + C::PF + g.H) * sg.pzb : sg.ldp,
+                   pf_ok ? sg.pzb : 0);
 #pragma unroll
     for (int j = 0; j < ROWS; ++j)
-      S.LD[(IR + C::PF) % C::R][j] = bload(r, sg.voff + j * sg.pitchb, 0, (V2*)nullptr);
+      S.LD[(IR + C::PF) % C::R][j] = bload(r, sg.voff + j * sg.pitchb, (V2*)nullptr);
+    sg.ldp += sg.pzb;
   }
   if constexpr (C::SKEW) {
 #pragma unroll
@@ -294,87 +366,66 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
       xch[l][IS][sg.wave][1][sg.lane] = in[ROWS - 1];
       if constexpr (!(C::ABL & 1)) __syncthreads();
     }
-    V2 up, dn;
-    if constexpr (C::ABL & 16) {  // ablation: the compiler's split float2 LDS reads
-      up = sg.wave > 0 ? xch[l][IS][sg.wave - 1][1][sg.lane] : in[0];
-      dn = sg.wave < WAVES - 1 ? xch[l][IS][sg.wave + 1][0][sg.lane] : in[ROWS - 1];
-    } else {
-      up = sg.wave > 0 ? lds_load2(&xch[l][IS][sg.wave - 1][1][sg.lane]) : in[0];
-      dn = sg.wave < WAVES - 1 ? lds_load2(&xch[l][IS][sg.wave + 1][0][sg.lane]) : in[ROWS - 1];
-    }
     const int q = C::SKEW ? p - (2 * l + 1) : p - l - 1;  // plane produced by level l+1
-    const int64_t gz = gwrap<C>(g.oz + q, g.Lz);
-    const uint64_t tstep = (uint64_t)(a.t + l);
-    V2 res[ROWS];
+    if (!((sg.skip >> l) & 1)) {  // wave-uniform
+      const V2 up = lds_load2(&xch[l][IS][sg.wup][1][sg.lane]);
+      const V2 dn = lds_load2(&xch[l][IS][sg.wdn][0][sg.lane]);
+      const int64_t gz = gwrap<C>(g.oz + q, g.Lz);
+      const uint64_t tstep = (uint64_t)(a.t + l);
+      V2 res[ROWS];
 #pragma unroll
-    for (int m = 0; m < ROWS / 4; ++m) {
-      gs::U4 blk{0, 0, 0, 0};
-      if constexpr (C::NOISE) {
-        const int64_t gyq = gwrap<C>(sg.gy0 + 4 * m, g.Ly);
-        if constexpr (C::ABL & 4) blk = gs::noise_block(sg.gx, gyq >> 2, gz, g.Lx, g.Ly, tstep, seed);
-        else blk = noise_block_dev<!(C::ABL & 8)>(sg.gx, gyq >> 2, gz, g.Lx, g.Ly, tstep, seed);
-      }
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int j = 4 * m + k;
-        const V2 ym = j == 0 ? up : in[j - 1];
-        const V2 yp = j == ROWS - 1 ? dn : in[j + 1];
-        T xyu, xyv;
-        if constexpr (C::XSUM_DPP) {
-          xyu = lane_pair_sum(in[j].x) + (ym.x + yp.x);
-          xyv = lane_pair_sum(in[j].y) + (ym.y + yp.y);
-        } else {
-          xyu = (lane_from_left(in[j].x) + lane_from_right(in[j].x)) + (ym.x + yp.x);
-          xyv = (lane_from_left(in[j].y) + lane_from_right(in[j].y)) + (ym.y + yp.y);
-        }
-        const T su = S.A[l][j].x + in[j].x;
-        const T sv = S.A[l][j].y + in[j].y;
-        const T cu = Cc[j].x, cv = Cc[j].y;
-        const T uvv = cu * cv * cv;
-        T ru = f.ac;
+      for (int m = 0; m < ROWS / 4; ++m) {
+        gs::U4 blk{0, 0, 0, 0};
         if constexpr (C::NOISE) {
-          // (folding the 2^-31 of uniform_pm1 into ar saves a v_mul but costs an SGPR; the
-          // extra spill reloads made it 2 % slower: profiles/r1_ab_noise_fold.txt)
-          const uint32_t w = k == 0 ? blk.x : (k == 1 ? blk.y : (k == 2 ? blk.z : blk.w));
-          if constexpr (C::FOLD31) ru = fma(S.ar31, (T)(int32_t)w, ru);
-          else ru = fma(f.ar, gs::uniform_pm1<T>(w), ru);
-        }
-        res[j].x = fma(f.au, cu, fma(f.asu, su, fma(-f.dt, uvv, ru)));
-        res[j].y = fma(f.bv, cv, fma(f.bsv, sv, f.dt * uvv));
-        S.A[l][j].x = xyu + cu;
-        S.A[l][j].y = xyv + cv;
-      }
-    }
-    if (l + 1 < TL) {
-      if (sg.edge) {
-        const T bu = (T)gs::bc_u(a.t + l + 1);
-        const bool zout = (g.oz + q < 0) || (g.oz + q >= g.Lz);
-        const bool xout = sg.gxu < 0 || sg.gxu >= g.Lx;
-#pragma unroll
-        for (int j = 0; j < ROWS; ++j) {
-          const int64_t gyj = sg.gy0 + j;
-          if (zout || xout || gyj < 0 || gyj >= g.Ly) {
-            res[j].x = bu;
-            res[j].y = (T)0;
+          if constexpr (C::Q32) {
+            // counter q = gx + Lx * (gy4 + Ly4 * gz) < 2^32: uniform part + lane part (a
+            // quad never straddles the periodic wrap: Ly % 4 == 0 there)
+            const uint32_t Ly4 = (uint32_t)((g.Ly + 3) >> 2);
+            const uint32_t gy4 = (uint32_t)(gwrap<C>(sg.gy0 + 4 * m, g.Ly) >> 2);
+            const uint32_t qu = (uint32_t)g.Lx * (gy4 + Ly4 * (uint32_t)gz);
+            blk = philox_dev<true>(qu + sg.gx32, 0u, tstep, seed);
+          } else {
+            const int64_t gyq = gwrap<C>(sg.gy0 + 4 * m, g.Ly);
+            const uint64_t Ly4 = ((uint64_t)g.Ly + 3) >> 2;
+            const uint64_t qq = (uint64_t)sg.gx + (uint64_t)g.Lx * ((uint64_t)(gyq >> 2) +
+                                                                   Ly4 * (uint64_t)gz);
+            blk = philox_dev<false>((uint32_t)qq, (uint32_t)(qq >> 32), tstep, seed);
           }
         }
-      }
 #pragma unroll
-      for (int j = 0; j < ROWS; ++j) S.OUT[l][IS][j] = res[j];
-    } else {
-      {  // unconditional stores: planes before the segment go to an empty descriptor
-        const bool st_ok = q >= sg.z0;
-        const __amdgpu_buffer_rsrc_t w =
-            (C::ABL & 32) ? plane_rsrc(dst, (int64_t)(q + g.H) * PZB, st_ok ? a.buf_bytes : 0)
-                          : plane_rsrc_p(dst, q + g.H, g.pz, PZB, st_ok);
+        for (int k = 0; k < 4; ++k) {
+          const int j = 4 * m + k;
+          const V2 ym = j == 0 ? up : in[j - 1];
+          const V2 yp = j == ROWS - 1 ? dn : in[j + 1];
+          const uint32_t w = k == 0 ? blk.x : (k == 1 ? blk.y : (k == 2 ? blk.z : blk.w));
+          res[j] = cell_update<C>(S.A[l][j], in[j], Cc[j], ym, yp, f, S.ar31, S.kc, w);
+        }
+      }
+      if (l + 1 < TL) {
+        if (sg.edge) {
+          const T bu = (T)gs::bc_u(a.t + l + 1);
+          const bool zout = (g.oz + q < 0) || (g.oz + q >= g.Lz);
+          const bool xout = sg.gxu < 0 || sg.gxu >= g.Lx;
+#pragma unroll
+          for (int j = 0; j < ROWS; ++j) {
+            const int64_t gyj = sg.gy0 + j;
+            if (zout || xout || gyj < 0 || gyj >= g.Ly) res[j] = V2{bu, (T)0};
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < ROWS; ++j) S.OUT[l][IS][j] = res[j];
+      } else {
+        // unconditional stores: planes before the segment go to an empty descriptor
+        const __amdgpu_buffer_rsrc_t w = plane_rsrc(sg.stp, q >= sg.z0 ? sg.pzb : 0);
 #pragma unroll
         for (int j = 0; j < ROWS; ++j) {
           const int off = (j >= sg.srow0 && j < sg.srow1) ? sg.svoff + j * sg.pitchb : (int)0x80000000;
-          bstore(w, off, 0, res[j]);
+          bstore(w, off, res[j]);
         }
       }
     }
   }
+  sg.stp += sg.pzb;
 }
 
 // Unrolled walk over one ring period; returns false when the segment is done.
@@ -382,14 +433,13 @@ template <class C, typename T, int I>
 __device__ __forceinline__ bool fused_period(FusedState<C>& S,
                                              typename C::V2 (*xch)[C::NS][C::WAVES][2][64],
                                              const FusedArgs& a, const FoldCoef<T>& f,
-                                             uint64_t seed, const typename C::V2* src,
-                                             typename C::V2* dst, FusedSeg& sg) {
+                                             uint64_t seed, FusedSeg& sg) {
   if constexpr (I == C::PERIOD) {
     return true;
   } else {
-    fused_iter<C, T, I % C::R, I % C::NS>(S, xch, a, f, seed, src, dst, sg);
+    fused_iter<C, T, I % C::R, I % C::NS>(S, xch, a, f, seed, sg);
     if (++sg.p >= sg.pend) return false;
-    return fused_period<C, T, I + 1>(S, xch, a, f, seed, src, dst, sg);
+    return fused_period<C, T, I + 1>(S, xch, a, f, seed, sg);
   }
 }
 
@@ -425,19 +475,25 @@ __device__ __forceinline__ void map_tile(const FusedArgs& a, int t, int& tx, int
 }
 
 template <class C, typename T>
-__global__ __launch_bounds__(64 * C::WAVES, C::MINW) void k_fused(const typename C::V2* __restrict__ s,
-                                                         typename C::V2* __restrict__ d,
-                                                         FusedArgs a, FoldCoef<T> f,
-                                                         uint64_t seed) {
-  using V2 = typename C::V2;
+__global__ __launch_bounds__(64 * C::WAVES, 1) void k_fused(const typename C::V2* __restrict__ s,
+                                                            typename C::V2* __restrict__ d,
+                                                            FusedArgs a, FoldCoef<T> f,
+                                                            uint64_t seed) {
   constexpr int ROWS = C::ROWS, WAVES = C::WAVES, TL = C::TL;
   static_assert(ROWS % 4 == 0, "rows per wave must hold whole noise quads");
-  __shared__ V2 xch[TL][C::NS][WAVES][2][64];  // [level][ring][wave][first/last row][lane]
+  __shared__ typename C::V2 xch[TL][C::NS][WAVES][2][64];  // [level][ring][wave][row][lane]
   const Geom& g = a.g;
   FusedSeg sg;
   sg.lane = threadIdx.x & 63;
   sg.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  sg.pitchb = g.px * (int)sizeof(V2);
+  sg.wup = sg.wave == 0 ? WAVES - 1 : sg.wave - 1;
+  sg.wdn = sg.wave == WAVES - 1 ? 0 : sg.wave + 1;
+  sg.skip = 0;
+#pragma unroll
+  for (int l = 0; l < TL; ++l)
+    if (sg.wave * ROWS > C::need_hi(l) || sg.wave * ROWS + ROWS - 1 < l + 1) sg.skip |= 1 << l;
+  sg.pitchb = g.px * (int)sizeof(typename C::V2);
+  sg.pzb = (int)(gs::plane_elems(g) * (int64_t)sizeof(typename C::V2));
   const int nzv = a.nzv;
   // Work list of this workgroup: logical units lu = chunk * ntiles + tile, lu0, lu0 + lstep, ...
   // (sched 0: one "unit", the even share [u, uend) of all tile-planes).
@@ -461,7 +517,24 @@ __global__ __launch_bounds__(64 * C::WAVES, C::MINW) void k_fused(const typename
     if (lu0 >= lu1) return;
   }
   FusedState<C> S;
-  if constexpr (C::FOLD31) {
+  // a wave that skips a level still publishes that level's (never used) rows: keep them defined
+#pragma unroll
+  for (int l = 0; l < C::NO; ++l)
+#pragma unroll
+    for (int i = 0; i < C::NS; ++i)
+#pragma unroll
+      for (int j = 0; j < ROWS; ++j) S.OUT[l][i][j] = typename C::V2{(T)0, (T)0};
+  {
+    const T k0 = f.kc.x, k1 = f.kc.y;
+    if constexpr (sizeof(T) == 4) {
+      asm volatile("v_mov_b32 %0, %1" : "=v"(S.kc.x) : "s"(k0));
+      asm volatile("v_mov_b32 %0, %1" : "=v"(S.kc.y) : "s"(k1));
+    } else {
+      asm volatile("v_mov_b64 %0, %1" : "=v"(S.kc.x) : "s"(k0));
+      asm volatile("v_mov_b64 %0, %1" : "=v"(S.kc.y) : "s"(k1));
+    }
+  }
+  if constexpr (C::NOISE) {
     // exact: power-of-two scaling (gs::uniform_pm1 = int * 2^-31); a VGPR copy keeps the
     // coefficient out of the (full) SGPR budget
     const T c = f.ar * (T)4.656612873077392578125e-10;
@@ -498,10 +571,11 @@ __global__ __launch_bounds__(64 * C::WAVES, C::MINW) void k_fused(const typename
       const int x = X0 + sg.lane;
       const int ylo = Y0 + sg.wave * ROWS;
       // lane byte offset inside a plane (row ylo); negative values are out of range
-      sg.voff = ((ylo + g.H) * g.px + x + g.xo) * (int)sizeof(V2);
+      sg.voff = ((ylo + g.H) * g.px + x + g.xo) * (int)sizeof(typename C::V2);
       sg.gxu = g.ox + x;
       sg.gx = gwrap<C>(sg.gxu, g.Lx);
       sg.gy0 = g.oy + ylo;
+      sg.gx32 = (uint32_t)sg.gx;
       const int ox1 = min(X0 + TL + a.xstep, g.nx);
       const int oy0 = max(Y0 + TL, 0), oy1 = min(Y0 + TL + a.ystep, g.ny);
       const bool xin = x >= max(X0 + TL, 0) && x < ox1;
@@ -512,24 +586,27 @@ __global__ __launch_bounds__(64 * C::WAVES, C::MINW) void k_fused(const typename
           (g.ox + X0 < 0 || g.ox + X0 + 64 > g.Lx || g.oy + Y0 < 0 ||
            g.oy + Y0 + WAVES * ROWS > g.Ly || g.oz + z0 - TL < 0 || g.oz + z1 + TL > g.Lz);
       sg.z0 = z0;
-  #pragma unroll
+#pragma unroll
       for (int l = 0; l < TL; ++l)
-  #pragma unroll
-        for (int j = 0; j < ROWS; ++j) S.A[l][j].x = S.A[l][j].y = (T)0;
+#pragma unroll
+        for (int j = 0; j < ROWS; ++j) S.A[l][j] = typename C::V2{(T)0, (T)0};
       sg.p = z0 - TL;
       sg.ldend = z1 + TL;
       sg.pend = C::SKEW ? z1 + 2 * TL - 1 : z1 + TL;
-      const int64_t PZB = gs::plane_elems(g) * (int64_t)sizeof(V2);
-  #pragma unroll
+      // running plane pointers: next prefetch (p + PF) and this iteration's last-level output
+      const int qlast = C::SKEW ? sg.p - (2 * TL - 1) : sg.p - TL;
+      sg.ldp = (const char*)s + (int64_t)(sg.p + C::PF + g.H) * sg.pzb;
+      sg.stp = (char*)d + (int64_t)(qlast + g.H) * sg.pzb;
+#pragma unroll
       for (int k = 0; k < C::PF; ++k) {
-        {
-          const __amdgpu_buffer_rsrc_t r = plane_rsrc_p(s, sg.p + k + g.H, g.pz, PZB,
-                                                        sg.p + k < sg.ldend);
-  #pragma unroll
-          for (int j = 0; j < ROWS; ++j) S.LD[k][j] = bload(r, sg.voff + j * sg.pitchb, 0, (V2*)nullptr);
-        }
+        const int pl = (C::ABL & 2) ? 0 : sg.p + k + g.H;
+        const __amdgpu_buffer_rsrc_t r = plane_rsrc((const char*)s + (int64_t)pl * sg.pzb,
+                                                    sg.p + k < sg.ldend ? sg.pzb : 0);
+#pragma unroll
+        for (int j = 0; j < ROWS; ++j)
+          S.LD[k][j] = bload(r, sg.voff + j * sg.pitchb, (typename C::V2*)nullptr);
       }
-      while (fused_period<C, T, 0>(S, xch, a, f, seed, s, d, sg)) {
+      while (fused_period<C, T, 0>(S, xch, a, f, seed, sg)) {
       }
     }
   }  // work list
@@ -551,11 +628,11 @@ struct FusedLaunch {
     }
     return occ;
   }
-  static void run(const typename C::V2* s, typename C::V2* d, const FusedArgs& a0,
-                  const gs::Params& p, hipStream_t st) {
+  static void run(const void* s, void* d, const FusedArgs& a0, const gs::Params& p,
+                  hipStream_t st) {
     FusedArgs a = a0;
     a.xstep = 64 - 2 * C::TL;
-    a.ystep = (C::WAVES * C::ROWS - 2 * C::TL) & ~3;
+    a.ystep = C::YSTEP;
     a.ybase = -mod4(a.g.oy - C::TL);  // (oy + ybase - TL) % 4 == 0
     a.ntx = (a.g.nx + a.xstep - 1) / a.xstep;
     a.nty = (a.g.ny - a.ybase + a.ystep - 1) / a.ystep;
@@ -563,7 +640,7 @@ struct FusedLaunch {
     if (a.tmode != 0) {
       // inner rectangle: tiles whose level-0 input box [X0, X0 + 64) x [Y0, Y0 + rows) stays
       // inside the interior on every side whose halo is in flight
-      const int rows = C::WAVES * C::ROWS;
+      const int rows = C::RT;
       int x0 = 0, x1 = a.ntx, y0 = 0, y1 = a.nty;
       if (a.sides & 1) while (x0 < a.ntx && x0 * a.xstep - C::TL < 0) ++x0;
       if (a.sides & 2) while (x1 > x0 && (x1 - 1) * a.xstep - C::TL + 64 > a.g.nx) --x1;
@@ -622,12 +699,12 @@ struct FusedLaunch {
       nwg = 8 * M;
     }
     const FoldCoef<T> f = make_fold<T>(p);
-    k_fused<C, T><<<(unsigned)nwg, 64 * C::WAVES, 0, st>>>(s, d, a, f, p.seed);
+    k_fused<C, T><<<(unsigned)nwg, 64 * C::WAVES, 0, st>>>(
+        (const typename C::V2*)s, (typename C::V2*)d, a, f, p.seed);
   }
 };
 
-// Tuning hook: a non-default fp32 configuration "<rows>x<waves>:<prefetch>[s|w<n>]" chosen by
-// GS_FUSED_CFG at load time or gs_fused_select() at run time (index 0 = measured default).
+// Work-schedule override: GS_FUSED_SCHED at load time or gs_fused_sched() at run time.
 inline int& fused_sched_slot() {
   static int v = -1;
   if (v < 0) {
@@ -637,19 +714,43 @@ inline int& fused_sched_slot() {
   return v;
 }
 
-inline const char* const* fused_cfg_names(int* n) {
-  static const char* names[] = {"",       "4x8:1",  "4x8:2",  "4x8:4",   "8x4:1",   "8x4:2",
-                                "4x16:2", "8x8:2",  "4x8:3",  "8x4:2w3", "8x4:1w3", "4x8:2w4",
-                                "8x4:3",  "4x6:2",  "4x12:2", "4x4:2",   "4x12:3",  "8x4:1s",
-                                "8x4:4s", "4x8:1s", "4x8:4s", "abl1",   "abl2",    "abl3",
-                                "4x8:1w4", "4x16:1", "4x16:2w4", "4x8:2w3", "abl4", "4x8:1abl4",
-                                "4x12:2s", "4x12:1s", "4x6:2s", "4x12:1", "4x12:1s-abl1",
-                                "4x12:1s-abl2", "4x12:1s-abl8", "4x12:2s-abl8", "4x12:1s-abl16",
-                                "4x12:2s-abl16", "4x12:1s-abl32", "4x12:1s-abl64",
-                                "4x12:2s-abl64", "4x12:1s-abl128", "4x12:2s-abl128", "(unused)",
-                                "4x8:1s-abl64"};
-  *n = (int)(sizeof(names) / sizeof(names[0]));
-  return names;
+// Tile / prefetch configurations "<rows>x<waves>:<prefetch>[s]" (s = skewed single-barrier
+// pipeline).  Index 0 is the default (fp32: 4x12:2s, fp64: 4x8:1s, the measured winners at
+// L >= 256, profiles/r1_tune_*); the autotuner times the rest on the live problem.  An entry
+// whose name carries "-abl" exists only in GS_ABLATION builds (timing experiments).
+struct FusedCfgEntry {
+  const char* name;
+  bool f32, f64;  // instantiated for fp32 / fp64 (others fall back to the default)
+};
+
+inline const FusedCfgEntry* fused_cfg_table(int* n) {
+  static const FusedCfgEntry t[] = {
+      {"", true, true},          //  0 default
+      {"4x8:1", true, true},     //  1
+      {"4x8:2", true, false},    //  2
+      {"4x8:1s", true, true},    //  3
+      {"4x8:2s", true, false},   //  4
+      {"4x8:4s", true, false},   //  5
+      {"8x4:1", true, false},    //  6
+      {"8x4:2", true, false},    //  7
+      {"8x4:1s", true, false},   //  8
+      {"8x4:4s", true, false},   //  9
+      {"4x12:1", true, true},    // 10
+      {"4x12:2", true, false},   // 11
+      {"4x12:3", true, false},   // 12
+      {"4x12:1s", true, false},  // 13
+      {"4x12:2s", true, false},  // 14
+      {"4x6:2s", true, true},    // 15
+      {"4x6:2", false, true},    // 16
+      {"4x4:2", false, true},    // 17
+      {"4x16:1", true, false},   // 18
+#ifdef GS_ABLATION
+      {"4x12:2s-abl1", true, false},  // 19  no barriers
+      {"4x12:2s-abl2", true, false},  // 20  L2-resident loads
+#endif
+  };
+  *n = (int)(sizeof(t) / sizeof(t[0]));
+  return t;
 }
 
 inline int& fused_cfg_slot() {
@@ -657,13 +758,14 @@ inline int& fused_cfg_slot() {
   return v;
 }
 
+// index of configuration `e` ("" or null = default), -1 if unknown in this build
 inline int fused_cfg_lookup(const char* e) {
   int n = 0;
-  const char* const* names = fused_cfg_names(&n);
-  if (!e) return 0;
+  const FusedCfgEntry* t = fused_cfg_table(&n);
+  if (!e || !e[0]) return 0;
   for (int i = 1; i < n; ++i)
-    if (!strcmp(e, names[i])) return i;
-  return e[0] ? -1 : 0;
+    if (!strcmp(e, t[i].name)) return i;
+  return -1;
 }
 
 inline int fused_cfg_env() {
@@ -675,95 +777,77 @@ inline int fused_cfg_env() {
   return v;
 }
 
-template <typename T, int TL, bool PER, bool NZ>
-void run_fused_cfg(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, const FusedArgs& a,
-                   const gs::Params& p, hipStream_t st) {
-  if constexpr (sizeof(T) == 8 && !PER && NZ) {
+template <typename T, int TL, bool PER, bool NZ, bool Q32>
+void run_fused_cfg(const void* s, void* d, const FusedArgs& a, const gs::Params& p,
+                   hipStream_t st) {
+  // tile variants: non-periodic runs with noise and a 32-bit counter (the tuned production
+  // path); everything else runs the default shape
+  if constexpr (sizeof(T) == 8 && !PER && NZ && Q32) {
     switch (a.cfg) {  // fp64: only shapes that fit the register file without spills
       case 1: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ>, T>::run(s, d, a, p, st); return;
-      case 13: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
-      case 15: FusedLaunch<FCfg<T, TL, 4, 4, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
-      case 19: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, 1, true>, T>::run(s, d, a, p, st); return;
-      case 32: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, 1, true>, T>::run(s, d, a, p, st); return;
-      case 33: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ>, T>::run(s, d, a, p, st); return;
-      case 46: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, 1, true, 64>, T>::run(s, d, a, p, st); return;
+      case 10: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ>, T>::run(s, d, a, p, st); return;
+      case 15: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true>, T>::run(s, d, a, p, st); return;
+      case 16: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
+      case 17: FusedLaunch<FCfg<T, TL, 4, 4, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
       default: break;
     }
   }
-  if constexpr (sizeof(T) == 4 && !PER && NZ) {
+  if constexpr (sizeof(T) == 4 && !PER && NZ && Q32) {
     switch (a.cfg) {
       case 1: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ>, T>::run(s, d, a, p, st); return;
       case 2: FusedLaunch<FCfg<T, TL, 4, 8, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
-      case 3: FusedLaunch<FCfg<T, TL, 4, 8, 4, PER, NZ>, T>::run(s, d, a, p, st); return;
-      case 4: FusedLaunch<FCfg<T, TL, 8, 4, 1, PER, NZ>, T>::run(s, d, a, p, st); return;
-      case 5: FusedLaunch<FCfg<T, TL, 8, 4, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
-      case 6: FusedLaunch<FCfg<T, TL, 4, 16, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
-      case 7: FusedLaunch<FCfg<T, TL, 8, 8, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
-      case 8: FusedLaunch<FCfg<T, TL, 4, 8, 3, PER, NZ>, T>::run(s, d, a, p, st); return;
-      case 9: FusedLaunch<FCfg<T, TL, 8, 4, 2, PER, NZ, 3>, T>::run(s, d, a, p, st); return;
-      case 10: FusedLaunch<FCfg<T, TL, 8, 4, 1, PER, NZ, 3>, T>::run(s, d, a, p, st); return;
-      case 11: FusedLaunch<FCfg<T, TL, 4, 8, 2, PER, NZ, 4>, T>::run(s, d, a, p, st); return;
-      case 12: FusedLaunch<FCfg<T, TL, 8, 4, 3, PER, NZ>, T>::run(s, d, a, p, st); return;
-      case 13: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
-      case 14: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
-      case 15: FusedLaunch<FCfg<T, TL, 4, 4, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
-      case 16: FusedLaunch<FCfg<T, TL, 4, 12, 3, PER, NZ>, T>::run(s, d, a, p, st); return;
-      case 17: FusedLaunch<FCfg<T, TL, 8, 4, 1, PER, NZ, 1, true>, T>::run(s, d, a, p, st); return;
-      case 18: FusedLaunch<FCfg<T, TL, 8, 4, 4, PER, NZ, 1, true>, T>::run(s, d, a, p, st); return;
-      case 19: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, 1, true>, T>::run(s, d, a, p, st); return;
-      case 20: FusedLaunch<FCfg<T, TL, 4, 8, 4, PER, NZ, 1, true>, T>::run(s, d, a, p, st); return;
-      case 21: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, 1, false, 1>, T>::run(s, d, a, p, st); return;
-      case 22: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, 1, false, 2>, T>::run(s, d, a, p, st); return;
-      case 23: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, 1, false, 3>, T>::run(s, d, a, p, st); return;
-      case 24: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, 4>, T>::run(s, d, a, p, st); return;
-      case 25: FusedLaunch<FCfg<T, TL, 4, 16, 1, PER, NZ>, T>::run(s, d, a, p, st); return;
-      case 26: FusedLaunch<FCfg<T, TL, 4, 16, 2, PER, NZ, 4>, T>::run(s, d, a, p, st); return;
-      case 27: FusedLaunch<FCfg<T, TL, 4, 8, 2, PER, NZ, 3>, T>::run(s, d, a, p, st); return;
-      case 28: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, 1, false, 4>, T>::run(s, d, a, p, st); return;
-      case 29: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, 1, false, 4>, T>::run(s, d, a, p, st); return;
-      case 30: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, 1, true>, T>::run(s, d, a, p, st); return;
-      case 31: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, 1, true>, T>::run(s, d, a, p, st); return;
-      case 32: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, 1, true>, T>::run(s, d, a, p, st); return;
-      case 33: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ>, T>::run(s, d, a, p, st); return;
-      case 34: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, 1, true, 1>, T>::run(s, d, a, p, st); return;
-      case 35: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, 1, true, 2>, T>::run(s, d, a, p, st); return;
-      case 36: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, 1, true, 8>, T>::run(s, d, a, p, st); return;
-      case 37: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, 1, true, 8>, T>::run(s, d, a, p, st); return;
-      case 38: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, 1, true, 16>, T>::run(s, d, a, p, st); return;
-      case 39: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, 1, true, 16>, T>::run(s, d, a, p, st); return;
-      case 40: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, 1, true, 32>, T>::run(s, d, a, p, st); return;
-      case 41: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, 1, true, 64>, T>::run(s, d, a, p, st); return;
-      case 42: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, 1, true, 64>, T>::run(s, d, a, p, st); return;
-      case 43: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, 1, true, 128>, T>::run(s, d, a, p, st); return;
-      case 44: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, 1, true, 128>, T>::run(s, d, a, p, st); return;
-      default: break;
+      case 3: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true>, T>::run(s, d, a, p, st); return;
+      case 4: FusedLaunch<FCfg<T, TL, 4, 8, 2, PER, NZ, true>, T>::run(s, d, a, p, st); return;
+      case 5: FusedLaunch<FCfg<T, TL, 4, 8, 4, PER, NZ, true>, T>::run(s, d, a, p, st); return;
+      case 6: FusedLaunch<FCfg<T, TL, 8, 4, 1, PER, NZ>, T>::run(s, d, a, p, st); return;
+      case 7: FusedLaunch<FCfg<T, TL, 8, 4, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
+      case 8: FusedLaunch<FCfg<T, TL, 8, 4, 1, PER, NZ, true>, T>::run(s, d, a, p, st); return;
+      case 9: FusedLaunch<FCfg<T, TL, 8, 4, 4, PER, NZ, true>, T>::run(s, d, a, p, st); return;
+      case 10: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ>, T>::run(s, d, a, p, st); return;
+      case 11: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
+      case 12: FusedLaunch<FCfg<T, TL, 4, 12, 3, PER, NZ>, T>::run(s, d, a, p, st); return;
+      case 13: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true>, T>::run(s, d, a, p, st); return;
+      case 15: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true>, T>::run(s, d, a, p, st); return;
+      case 18: FusedLaunch<FCfg<T, TL, 4, 16, 1, PER, NZ>, T>::run(s, d, a, p, st); return;
+#ifdef GS_ABLATION
+      case 19: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 1>, T>::run(s, d, a, p, st); return;
+      case 20: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 2>, T>::run(s, d, a, p, st); return;
+#endif
+      default: break;  // 0 and 14: the default shape below
     }
   }
-  // measured defaults (MI355X, in-process A/B, profiles/r1_tune_inproc.json): fp32 uses the
-  // 4x12 tile with a 2-plane prefetch (best at T=2 for 256^3 and at T=3 for 512^3); fp64 4x8
   if constexpr (sizeof(T) == 4) {
-    FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ>, T>::run(s, d, a, p, st);
+    FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, Q32>, T>::run(s, d, a, p, st);
   } else {
-    FusedLaunch<FCfg<T, TL, 4, 8, 2, PER, NZ>, T>::run(s, d, a, p, st);
+    FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, Q32>, T>::run(s, d, a, p, st);
   }
 }
 
 template <typename T, int TL>
-void run_fused_tl(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, const FusedArgs& a,
-                  const gs::Params& p, hipStream_t st) {
+void run_fused_tl(const void* s, void* d, const FusedArgs& a, const gs::Params& p,
+                  hipStream_t st) {
   const bool per = a.g.periodic != 0, nz = p.noise != 0.0;
-  if (per) {
-    if (nz) run_fused_cfg<T, TL, true, true>(s, d, a, p, st);
-    else run_fused_cfg<T, TL, true, false>(s, d, a, p, st);
+  if (!nz) {
+    if (per) run_fused_cfg<T, TL, true, false, true>(s, d, a, p, st);
+    else run_fused_cfg<T, TL, false, false, true>(s, d, a, p, st);
+  } else if (a.q32) {
+    if (per) run_fused_cfg<T, TL, true, true, true>(s, d, a, p, st);
+    else run_fused_cfg<T, TL, false, true, true>(s, d, a, p, st);
   } else {
-    if (nz) run_fused_cfg<T, TL, false, true>(s, d, a, p, st);
-    else run_fused_cfg<T, TL, false, false>(s, d, a, p, st);
+    if (per) run_fused_cfg<T, TL, true, true, false>(s, d, a, p, st);
+    else run_fused_cfg<T, TL, false, true, false>(s, d, a, p, st);
   }
 }
 
 inline bool fused_supported(const Geom& g, int n) {
   if (n < 2 || n > 3 || g.H < n) return false;
   return !(g.periodic && (g.Ly % 4 != 0));  // noise quads would straddle the wrap
+}
+
+// whether the Philox counter q = gx + Lx * (gy4 + Ly4 * gz) of every cell fits 32 bits
+inline bool philox_q32(const Geom& g) {
+  const uint64_t Ly4 = ((uint64_t)g.Ly + 3) >> 2;
+  return (uint64_t)g.Lx * Ly4 * (uint64_t)g.Lz <= 0xFFFFFFFFull;
 }
 
 // cfg / sched < 0: the process-wide selection (GS_FUSED_CFG / GS_FUSED_SCHED or the
@@ -779,6 +863,8 @@ bool launch_fused(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, co
   if (zlen1 <= 0) zlen1 = 0;
   if (zlen0 <= 0 || zlo0 < 0 || zlo0 + zlen0 > g.nz || (zlen1 && (zlo1 < 0 || zlo1 + zlen1 > g.nz)))
     return false;
+  // one storage plane must fit a buffer descriptor's 32-bit range
+  if (gs::plane_elems(g) * (int64_t)sizeof(typename Vec2<T>::type) > 0x7ffffff0LL) return false;
   a.zlo[0] = zlo0; a.zlen[0] = zlen0;
   a.zlo[1] = zlo1; a.zlen[1] = zlen1;
   a.nzv = zlen0 + zlen1;
@@ -787,11 +873,13 @@ bool launch_fused(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, co
   a.sides = sides;
   a.g = g;
   a.t = t;
+  // GS_PHILOX_GENERIC=1 forces the 64-bit-counter Philox path (tests: both paths agree bitwise)
+  static const bool generic = getenv("GS_PHILOX_GENERIC") && atoi(getenv("GS_PHILOX_GENERIC")) != 0;
+  a.q32 = (philox_q32(g) && !generic) ? 1 : 0;
   a.cfg = cfg >= 0 ? cfg : fused_cfg_env();
   a.sched = sched >= 0 ? sched : fused_sched_slot();
   if (zlen1) a.sched = 0;  // two short runs: one workgroup per (tile, run)
   a.bcfix = g.periodic ? 0 : 1;
-  a.buf_bytes = gs::total_elems(g) * (int64_t)sizeof(typename Vec2<T>::type);
   if (n == 2) run_fused_tl<T, 2>(s, d, a, p, st);
   else run_fused_tl<T, 3>(s, d, a, p, st);
   return true;

@@ -11,7 +11,15 @@ Parity:
 Additions: checkpoint every ``checkpoint_freq`` steps and restart from ``restart_input`` (the
 reference parses these keys but ignores them, D6), a JSON-lines perf log, optional global
 diagnostics, and fault injection for restart testing (``GS_FAIL_AT_STEP=<n>`` makes every
-rank exit with status 3 right after step n has been computed and checkpointed).  Checkpoints
+rank exit with status 3 right after step n has been computed and checkpointed;
+``GS_RAISE_AT_STEP=<n>`` with ``GS_FAIL_RANK=<r>`` makes rank r alone raise an error there).
+
+Job-wide failure handling: the reference's julia_main catches, prints and
+returns 1 (GrayScott.jl:40-48), and an MPI error aborts the whole job.  Here a rank that fails
+in a multi-rank job aborts its RCCL communicator and exits at once (``os._exit(1)``, no
+clean-up that could block on a collective), so its peers see the broken connection (gloo) or
+the aborted communicator (RCCL watchdog) and fail too instead of waiting; every gloo
+collective is also bounded by GS_COMM_TIMEOUT (parallel/dist.py).  Checkpoints
 are written behind the simulation by default (``async_checkpoint``, io/checkpoint.py
 ``CheckpointWriter``): the data write runs on a host thread from the same snapshot as the output
 step, and is committed before the next snapshot, at the end, or before a fault-injected exit.
@@ -81,6 +89,8 @@ def run(settings: Settings, out=sys.stdout) -> dict:
     timer = PhaseTimer(sync=sim.synchronize)
     perf = PerfLog(settings.perf_log, enabled=(rank == 0))
     fail_at = int(os.environ.get("GS_FAIL_AT_STEP", "-1"))
+    raise_at = int(os.environ.get("GS_RAISE_AT_STEP", "-1"))
+    fail_rank = int(os.environ.get("GS_FAIL_RANK", "-1"))
     with timer.phase("io_init"):
         stream = SimulationOutput(settings, domain, ctx)
     step = 0
@@ -139,6 +149,9 @@ def run(settings: Settings, out=sys.stdout) -> dict:
             io_s += time.perf_counter() - t1
         perf.write(step=step, steps=nsteps, compute_s=dt_c, io_s=io_s,
                    mlups=cells * nsteps / max(dt_c, 1e-12) / 1e6, ranks=ctx.world_size)
+        if raise_at >= 0 and step >= raise_at and fail_rank in (-1, rank):
+            raise RuntimeError(f"injected failure on rank {rank} at step {step} "
+                               "(GS_RAISE_AT_STEP)")
         if fail_at >= 0 and step >= fail_at:
             if ckpt is not None:
                 ckpt.finish()
@@ -167,13 +180,35 @@ def main(args: Optional[Sequence[str]] = None) -> dict:
     return run(settings)
 
 
+def abort_job(code: int = 1) -> None:
+    """End this rank of a multi-rank job now: abort the RCCL communicator (peers blocked in a
+    halo exchange get an error) and exit without interpreter clean-up (which could block in a
+    collective).  Never returns."""
+    try:
+        from .ops import native
+        native.rccl_abort()
+    except Exception:
+        pass
+    try:
+        sys.stdout.flush()
+        sys.stderr.flush()
+    finally:
+        os._exit(code)
+
+
 def julia_main(args: Optional[Sequence[str]] = None) -> int:
-    """GrayScott.julia_main (GrayScott.jl:40-48): 0 on success, 1 on error."""
+    """GrayScott.julia_main (GrayScott.jl:40-48): 0 on success, 1 on error.  In a multi-rank
+    job an error ends this rank at once (``abort_job``) so the job fails fast."""
+    from .parallel.launch import launcher_env
     try:
         main(args)
     except SystemExit as e:
         return int(e.code or 0)
     except BaseException:
         traceback.print_exc()
+        if launcher_env()[1] > 1:
+            rank = launcher_env()[0]
+            print(f"rank {rank}: aborting the job", file=sys.stderr, flush=True)
+            abort_job(1)
         return 1
     return 0

@@ -142,6 +142,17 @@ class GrayScott:
             raise ValueError(f"unknown transport {kind!r}")
         self.transport = kind
 
+    def device_info(self) -> dict:
+        """Where this rank runs and what its halo transport sees (bench.py's ``world``)."""
+        info = {"rank": self.domain.rank, "backend": self.backend, "transport": self.transport}
+        if self.backend == "hip":
+            info["device"] = int(self.device.index)
+            info["pci"] = native.device_pci_bus_id()
+            rc = self.engine.rccl_info()
+            if rc is not None:
+                info["rccl_nranks"], info["rccl_rank"], info["rccl_device"] = rc
+        return info
+
     @property
     def overlapped(self) -> bool:
         """Whether full-depth passes overlap their halo exchange with the inner planes."""

@@ -48,6 +48,10 @@ class NativeLibraryMissing(RuntimeError):
 
 
 def lib_path(name: str) -> str:
+    """``libgs_<name>.so``; GS_HIP_VARIANT=abl selects the ablation build of the HIP library
+    (``make ablation``: timing experiments only, its ablation kernels compute wrong results)."""
+    if name == "hip" and os.environ.get("GS_HIP_VARIANT", "") == "abl":
+        return os.path.join(_LIB_DIR, "libgs_hip_abl.so")
     return os.path.join(_LIB_DIR, f"libgs_{name}.so")
 
 
@@ -104,6 +108,12 @@ def _declare(lib) -> None:
         lib.gs_rccl_unique_id.restype = c_int
         lib.gs_rccl_init.argtypes = [c_void_p, ctypes.c_char_p, c_int32, c_int32, c_int32]
         lib.gs_rccl_init.restype = c_int
+        lib.gs_rccl_info.argtypes = [c_void_p, c_int32, POINTER(c_int32)]
+        lib.gs_rccl_info.restype = c_int
+        lib.gs_rccl_abort.argtypes = []
+        lib.gs_rccl_abort.restype = c_int
+        lib.gs_device_pci.argtypes = [ctypes.c_char_p, c_int32]
+        lib.gs_device_pci.restype = c_int
     if hasattr(lib, "gs_fused_choice"):
         lib.gs_fused_choice.argtypes = [c_void_p, c_int32, c_int32, POINTER(c_int32),
                                         POINTER(ctypes.c_float)]
@@ -295,6 +305,30 @@ class Engine:
                   "rccl_init")
 
 
+    def rccl_info(self):
+        """(communicator size, rank in it, HIP device) of the RCCL transport, or None."""
+        if not hasattr(self.lib, "gs_rccl_info"):
+            return None
+        out = (c_int32 * 3)()
+        self._chk(self.lib.gs_rccl_info(self.h, DTYPE_CODES[self.dtype], out), "rccl_info")
+        return None if out[0] < 0 else (int(out[0]), int(out[1]), int(out[2]))
+
+
+def rccl_abort() -> None:
+    """Abort this process's RCCL communicator, if the HIP library is loaded and holds one."""
+    lib = _libs.get("hip")
+    if lib is not None and hasattr(lib, "gs_rccl_abort"):
+        lib.gs_rccl_abort()
+
+
+def device_pci_bus_id() -> str:
+    """PCI bus id of the current HIP device ("" when unavailable)."""
+    lib = load("hip")
+    buf = ctypes.create_string_buffer(64)
+    n = lib.gs_device_pci(buf, 64)
+    return buf.value.decode() if n > 0 else ""
+
+
 def rccl_unique_id() -> bytes:
     lib = load("hip")
     buf = ctypes.create_string_buffer(256)
@@ -321,6 +355,15 @@ def fused_sched(sched: int) -> None:
     lib.gs_fused_sched.restype = c_int
     if lib.gs_fused_sched(int(sched)) != 0:
         raise ValueError(f"unknown schedule {sched}")
+
+
+def fused_cfg_lookup(name: str) -> int:
+    """Index of fused-kernel configuration ``name`` in the loaded HIP library, -1 if this build
+    does not have it (the ablation variants exist only in ``make ablation`` builds)."""
+    lib = load("hip")
+    lib.gs_fused_cfg_lookup.argtypes = [ctypes.c_char_p]
+    lib.gs_fused_cfg_lookup.restype = c_int
+    return int(lib.gs_fused_cfg_lookup(name.encode()))
 
 
 def fused_cfg_name(index: int) -> str:

@@ -73,10 +73,14 @@ def candidates(L: int, nprocs: int, backend: str) -> List[Tuple]:
         return [([1, 1, 1], 0, "auto")]
     z = choose_dims(L, nprocs, "z", backend)
     bal = dims_create(nprocs)
+    # the reference's Dims_create grid first: it is always timed (bench.py reports it as
+    # ``reference_grid``), then the z slabs (overlapped and not: the overlap's split launches
+    # cost more than they hide unless the exchange is slow), then the variants
+    add(bal, 0)
     if backend == "hip" and L // nprocs >= 8:
         add(z, 0)
+        add(z, 0, "off")
         add(z, 2)
-    add(bal, 0)
     if backend == "hip":
         add(bal, 0, "off")
         add(bal, 2)
@@ -127,16 +131,30 @@ def time_data_path(settings, ctx, L: int, dims, fuse: int, steps: int = 30, warm
 
 def tune_data_path(settings, ctx, L: int, backend: str,
                    cands: Optional[Sequence[Tuple]] = None,
-                   steps: int = 120, warmup: int = 12, log=None) -> Dict:
+                   steps: int = 120, warmup: int = 12, log=None,
+                   budget_s: Optional[float] = None) -> Dict:
     """Self-check and time every candidate ``(dims, fuse[, overlap[, env]])``; returns
     ``{"dims", "fuse", "transport", "overlap", "inplace_halos", "env", "table"}`` for the fastest
-    correct one (identical on every rank; ``env`` must be set for the run that uses it)."""
+    correct one (identical on every rank; ``env`` must be set for the run that uses it).
+
+    ``budget_s`` bounds the whole tuning phase: once it is spent (rank 0's clock, agreed by all
+    ranks) the remaining candidates are skipped (``"skipped": "budget"`` in the table), but at
+    least two are always tried.  Once one candidate's transport passed its check, later
+    candidates do not retry the fallback transports: a failure there is the path's own."""
     from ..models.grayscott import default_fuse
 
     cands = list(cands) if cands is not None else candidates(L, ctx.world_size, backend)
     table = []
     best = None
-    for cand in cands:
+    t_start = time.perf_counter()
+    proven = None  # transport that passed a check on this node
+    for ci, cand in enumerate(cands):
+        over = budget_s is not None and time.perf_counter() - t_start > budget_s
+        if ci >= 2 and ctx.allreduce(1.0 if over else 0.0, "max") > 0:
+            table.append({"dims": list(cand[0]), "fuse": cand[1],
+                          "overlap_req": cand[2] if len(cand) > 2 else settings.overlap,
+                          "skipped": "budget"})
+            continue
         dims, fuse = cand[0], cand[1]
         ov0 = cand[2] if len(cand) > 2 else settings.overlap
         env0 = dict(cand[3]) if len(cand) > 3 else {}
@@ -150,9 +168,12 @@ def tune_data_path(settings, ctx, L: int, backend: str,
         if env0:
             row["env"] = env0
         chosen = None
-        for tr, ov, extra in ((settings.transport, ov0, {}),
-                              (settings.transport, "off", {"GS_INPLACE_HALO": "0"}),
-                              ("torch", "off", {"GS_INPLACE_HALO": "0"})):
+        attempts = [(settings.transport, ov0, {}),
+                    (settings.transport, "off", {"GS_INPLACE_HALO": "0"}),
+                    ("torch", "off", {"GS_INPLACE_HALO": "0"})]
+        if proven is not None:
+            attempts = [(proven, ov0, {})]
+        for tr, ov, extra in attempts:
             env = {**env0, **extra}
             with _env(env):
                 try:
@@ -162,6 +183,8 @@ def tune_data_path(settings, ctx, L: int, backend: str,
             ok = ctx.allreduce(1.0 if ok else 0.0, "min") > 0
             if ok:
                 chosen = (used, ov, env)
+                if not extra:
+                    proven = used
                 break
         if chosen is None:
             row.update(ok=False)
@@ -182,7 +205,7 @@ def tune_data_path(settings, ctx, L: int, backend: str,
             continue
         row.update(ok=True, transport=chosen[0], overlap=chosen[1], overlapped=ovd,
                    inplace_halos=chosen[2].get("GS_INPLACE_HALO") != "0",
-                   ms_per_step=round(1e3 * el / steps, 4))
+                   ms_per_step=round(1e3 * el / steps, 4), steps=steps)
         table.append(row)
         if log is not None and ctx.rank == 0:
             log(f"data path {row}")
@@ -191,6 +214,8 @@ def tune_data_path(settings, ctx, L: int, backend: str,
     if best is None:
         raise RuntimeError(f"no multi-rank data path passed its self-check: {table}")
     env = best[3][2]
+    if log is not None and ctx.rank == 0:
+        log(f"data-path tuning took {time.perf_counter() - t_start:.1f} s")
     return {"dims": best[1], "fuse": best[2], "transport": best[3][0], "overlap": best[3][1],
             "inplace_halos": env.get("GS_INPLACE_HALO") != "0", "env": env, "table": table}
 

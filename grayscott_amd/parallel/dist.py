@@ -10,10 +10,13 @@ from __future__ import annotations
 
 import os
 from dataclasses import dataclass
+from datetime import timedelta
 from typing import Any, List, Optional
 
 import torch
 import torch.distributed as dist
+
+from .launch import launcher_env  # noqa: F401  (re-exported: the launcher table lives there)
 
 
 @dataclass
@@ -78,30 +81,20 @@ class DistContext:
 _CTX: Optional[DistContext] = None
 
 
-# Launcher environments: torchrun, then the MPI / batch launchers the reference is run with
-# (`mpirun -n N`, test/functional/functional-GrayScott.jl:9; srun / jsrun in scripts/job_*.sh).
-_LAUNCHERS = (
-    ("RANK", "WORLD_SIZE", "LOCAL_RANK"),                                  # torchrun
-    ("PMI_RANK", "PMI_SIZE", "MPI_LOCALRANKID"),                           # MPICH / hydra
-    ("OMPI_COMM_WORLD_RANK", "OMPI_COMM_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_RANK"),  # Open MPI
-    ("SLURM_PROCID", "SLURM_NTASKS", "SLURM_LOCALID"),                     # srun
-)
-
-
-def launcher_env(env=None):
-    """(rank, world_size, local_rank) from the first launcher whose variables are set."""
-    env = os.environ if env is None else env
-    for rk, sz, lc in _LAUNCHERS:
-        if rk in env and sz in env:
-            rank = int(env[rk])
-            return rank, int(env[sz]), int(env.get(lc, rank))
-    return 0, 1, 0
+def comm_timeout_s() -> float:
+    """Seconds a control-plane collective or a device halo wait may block before the job is
+    declared dead (GS_COMM_TIMEOUT, default 900; the RCCL watchdog reads the same variable)."""
+    try:
+        return max(1.0, float(os.environ.get("GS_COMM_TIMEOUT", "900")))
+    except ValueError:
+        return 900.0
 
 
 def init_from_env(device: str = "cpu") -> DistContext:
-    """Initialise (once) from the launcher's environment (torchrun, mpiexec, srun).  Without
-    torchrun, the gloo rendezvous uses MASTER_ADDR (default 127.0.0.1: one node) and
-    MASTER_PORT (default 29531)."""
+    """Initialise (once) from the launcher's environment (torchrun, mpiexec, srun, or
+    ``parallel.launch.spawn_local``).  Without torchrun, the gloo rendezvous uses MASTER_ADDR
+    (default 127.0.0.1: one node) and MASTER_PORT (default 29531).  Every gloo collective is
+    bounded by GS_COMM_TIMEOUT seconds, so a dead peer turns into an error, not a hang."""
     global _CTX
     if _CTX is not None:
         return _CTX
@@ -112,7 +105,8 @@ def init_from_env(device: str = "cpu") -> DistContext:
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29531")
-        dist.init_process_group(backend="gloo", rank=rank, world_size=world)
+        dist.init_process_group(backend="gloo", rank=rank, world_size=world,
+                                timeout=timedelta(seconds=comm_timeout_s()))
         ctx.initialized_here = True
     _CTX = ctx
     return ctx

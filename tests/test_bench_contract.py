@@ -47,3 +47,51 @@ def test_bench_torchrun_two_ranks(decomp):
     tab = d["data_path_tuning"]
     assert len(tab) == 1 and tab[0]["ok"] and tab[0]["ms_per_step"] > 0
     assert d["config"]["dims"] == ([1, 1, 2] if decomp == "z" else [2, 1, 1])
+
+
+def test_bench_self_launch_two_ranks():
+    """`python bench.py --gpus 2` with no launcher starts both ranks itself (parallel/launch.py)
+    and prints exactly one JSON line (rank 0's)."""
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--backend", "CPU", "--L", "32",
+                        "--steps", "6", "--warmup", "2", "--decomposition", "balanced"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _last_json(r.stdout)
+    assert KEYS <= set(d)
+    assert d["world"]["ranks"] == 2 and len(d["world"]["per_rank"]) == 2
+    assert d["tuning_s"] >= 0 and d["wall_s"] > 0
+    assert d["reference_grid"]["dims"] == [2, 1, 1]
+    assert d["reference_grid"]["ms_per_step"] > 0
+
+
+def test_bench_self_launch_propagates_failure():
+    """A rank that fails makes the whole self-launched job fail (non-zero status, no hang)."""
+    env = dict(os.environ, OMP_NUM_THREADS="1", GS_COMM_TIMEOUT="60", GS_RAISE_AT_STEP="0",
+               GS_FAIL_RANK="1")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--backend", "CPU", "--L", "16",
+                        "--steps", "2", "--warmup", "1", "--decomposition", "balanced"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode != 0
+    assert "injected failure on rank 1" in r.stderr
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
+def test_spawn_local_fail_fast(tmp_path):
+    """spawn_local: one worker exits 3 at once, the other would sleep for minutes: the job ends
+    within the grace period with the failing worker's status."""
+    import time
+
+    from grayscott_amd.parallel.launch import spawn_local
+    prog = ("import os, sys, time\n"
+            "r = int(os.environ['RANK'])\n"
+            "assert os.environ['WORLD_SIZE'] == '2' and os.environ['MASTER_ADDR'] == '127.0.0.1'\n"
+            "sys.exit(3) if r == 1 else time.sleep(300)\n")
+    t0 = time.monotonic()
+    rc = spawn_local(2, [sys.executable, "-c", prog], grace=2.0)
+    assert rc == 3
+    assert time.monotonic() - t0 < 60

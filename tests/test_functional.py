@@ -163,3 +163,33 @@ def test_fault_injection_and_recovery(tmp_path):
     with BP4Reader(str(ref / "o.bp")) as a, BP4Reader(str(run / "o.bp")) as b:
         np.testing.assert_array_equal(a.read("U", -1), b.read("U", -1))
         np.testing.assert_array_equal(a.read("V", -1), b.read("V", -1))
+
+
+def test_one_failing_rank_ends_the_job(tmp_path):
+    """Job-wide failure handling: rank 1 of 4 raises at step 20; every rank exits
+    non-zero on its own (no launcher kills them), well within GS_COMM_TIMEOUT."""
+    import time
+
+    from grayscott_amd.parallel.launch import free_port as fp
+    from grayscott_amd.parallel.launch import worker_env
+    cfg = _cfg(tmp_path, "c.toml", steps=60, plotgap=10, L=24, output=str(tmp_path / "o.bp"))
+    port = fp()
+    extra = {"OMP_NUM_THREADS": "1", "GS_RAISE_AT_STEP": "20", "GS_FAIL_RANK": "1",
+             "GS_COMM_TIMEOUT": "120"}
+    t0 = time.monotonic()
+    procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "gray-scott.py"), cfg],
+                              cwd=str(tmp_path), env=worker_env(r, 4, port, extra=extra),
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+             for r in range(4)]
+    outs = []
+    try:
+        for p in procs:
+            outs.append(p.communicate(timeout=100))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    codes = [p.returncode for p in procs]
+    assert all(c != 0 for c in codes), (codes, [o[1][-800:] for o in outs])
+    assert "injected failure on rank 1" in outs[1][1]
+    assert time.monotonic() - t0 < 100
