@@ -134,7 +134,9 @@ struct Writer {
   Buf step_meta;        // serialized local step metadata (returned to the caller)
 };
 
-std::string g_err;
+// per thread: the output and checkpoint writers run their data writes on different host
+// threads, and an error message must reach the thread whose call failed
+thread_local std::string g_err;
 
 void write_all(FILE* f, const void* p, size_t n) {
   if (n && fwrite(p, 1, n, f) != n) throw std::runtime_error(std::string("write failed: ") + strerror(errno));
@@ -286,6 +288,67 @@ extern "C" {
 
 const char* bp4_last_error(void) { return g_err.c_str(); }
 int bp4_version(void) { return 4; }
+
+// Open a writer that continues an existing output (restart with the output history kept):
+// the first `steps_kept` steps stay, everything after them is cut off.  data_end: length to
+// keep of this rank's data.<rank> (-1: start a new subfile); md_end / idx_end (rank 0): lengths
+// to keep of md.0 / md.idx.  The lengths come from the index (grayscott_amd/io/bp4.py
+// append_plan).  New steps continue the step numbering; attributes are not written again.
+void* bp4_open_append(const char* path, const char* io_name, int32_t rank, int32_t nranks,
+                      int32_t column_major, uint32_t steps_kept, int64_t data_end,
+                      int64_t md_end, int64_t idx_end) {
+  Writer* w = nullptr;
+  try {
+    if (steps_kept == 0) throw std::runtime_error("append needs at least one kept step");
+    w = new Writer;
+    w->dir = path;
+    w->rank = rank;
+    w->nranks = nranks;
+    w->subfile = rank;
+    w->io_name = io_name;
+    w->column_major = column_major != 0;
+    w->step = steps_kept;
+    w->attrs_written = true;
+    mkdir_p(w->dir);
+    const std::string dname = w->dir + "/data." + std::to_string(w->subfile);
+    if (data_end >= 64) {
+      w->data = fopen(dname.c_str(), "r+b");
+      if (!w->data) throw std::runtime_error("cannot reopen " + dname + ": " + strerror(errno));
+      if (ftruncate(fileno(w->data), (off_t)data_end) != 0 || fseeko(w->data, 0, SEEK_END) != 0)
+        throw std::runtime_error("cannot truncate " + dname + ": " + strerror(errno));
+      w->data_pos = (uint64_t)data_end;
+    } else {
+      w->data = fopen(dname.c_str(), "wb");
+      if (!w->data) throw std::runtime_error("cannot open " + dname + ": " + strerror(errno));
+      Buf h;
+      make_header(h, 'D', false);
+      write_all(w->data, h.b.data(), h.size());
+      w->data_pos = 64;
+    }
+    if (rank == 0) {
+      w->md = fopen((w->dir + "/md.0").c_str(), "r+b");
+      w->idx = fopen((w->dir + "/md.idx").c_str(), "r+b");
+      if (!w->md || !w->idx) throw std::runtime_error("cannot reopen metadata files in " + w->dir);
+      if (md_end < 64 || idx_end < 64 || ftruncate(fileno(w->md), (off_t)md_end) != 0 ||
+          ftruncate(fileno(w->idx), (off_t)idx_end) != 0 || fseeko(w->md, 0, SEEK_END) != 0 ||
+          fseeko(w->idx, 0, SEEK_END) != 0)
+        throw std::runtime_error("cannot truncate the metadata of " + w->dir);
+      w->md_pos = (uint64_t)md_end;
+      const uint8_t active = 1;  // index table: writer open again
+      if (pwrite(fileno(w->idx), &active, 1, 38) != 1) throw std::runtime_error("pwrite failed");
+    }
+    return w;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    if (w) {
+      if (w->data) fclose(w->data);
+      if (w->md) fclose(w->md);
+      if (w->idx) fclose(w->idx);
+      delete w;
+    }
+    return nullptr;
+  }
+}
 
 void* bp4_open(const char* path, const char* io_name, int32_t rank, int32_t nranks,
                int32_t column_major) {

@@ -91,14 +91,22 @@ def run(settings: Settings, out=sys.stdout) -> dict:
     fail_at = int(os.environ.get("GS_FAIL_AT_STEP", "-1"))
     raise_at = int(os.environ.get("GS_RAISE_AT_STEP", "-1"))
     fail_rank = int(os.environ.get("GS_FAIL_RANK", "-1"))
-    with timer.phase("io_init"):
-        stream = SimulationOutput(settings, domain, ctx)
     step = 0
     if settings.restart:
         with timer.phase("restart"):
             step = do_restart(sim, settings, ctx)
         if rank == 0 and settings.verbose:
             print(f"Restarting from step {step} ({settings.restart_input})", file=out, flush=True)
+    with timer.phase("io_init"):
+        # a restarted run continues the existing output: its steps up to the restart step stay
+        stream = SimulationOutput(settings, domain, ctx,
+                                  append_after_step=step if settings.restart else None)
+    if (settings.restart and settings.plotgap > 0 and step > 0 and step % settings.plotgap == 0
+            and stream.last_step != step):
+        # the failed run had not committed this output step: the restored state is that step's
+        # state bit for bit (Philox keyed on global cell and step), so write it now
+        with timer.phase("output"):
+            stream.write_step(step, sim)
     first_step = step
     ckpt_on = settings.checkpoint and settings.checkpoint_freq > 0
     ckpt = (CheckpointWriter(settings, domain, ctx)

@@ -54,6 +54,9 @@ def _lib():
     if not getattr(lib, "_bp4_declared", False):
         lib.bp4_open.restype = c_void_p
         lib.bp4_open.argtypes = [c_char_p, c_char_p, c_int32, c_int32, c_int32]
+        lib.bp4_open_append.restype = c_void_p
+        lib.bp4_open_append.argtypes = [c_char_p, c_char_p, c_int32, c_int32, c_int32,
+                                        ctypes.c_uint32, c_int64, c_int64, c_int64]
         lib.bp4_last_error.restype = c_char_p
         lib.bp4_define_attribute.argtypes = [c_void_p, c_char_p, c_int32, c_void_p, c_int64]
         lib.bp4_define_attribute.restype = c_int32
@@ -89,11 +92,19 @@ class BP4Writer:
     """One rank's handle on a BP4 output.  Rank 0 also owns md.0 / md.idx."""
 
     def __init__(self, path: str, io_name: str, rank: int = 0, nranks: int = 1,
-                 column_major: bool = False):
+                 column_major: bool = False, append: Optional[Dict[str, Any]] = None):
+        """``append``: continue an existing file after its first ``append["steps"]`` steps (an
+        :func:`append_plan`, the same on every rank; later steps are cut off)."""
         self.lib = _lib()
         self.path, self.rank, self.nranks = path, rank, nranks
-        h = self.lib.bp4_open(path.encode(), io_name.encode(), rank, nranks,
-                              1 if column_major else 0)
+        if append:
+            h = self.lib.bp4_open_append(path.encode(), io_name.encode(), rank, nranks,
+                                         1 if column_major else 0, int(append["steps"]),
+                                         int(append["data_end"].get(rank, -1)),
+                                         int(append["md_end"]), int(append["idx_end"]))
+        else:
+            h = self.lib.bp4_open(path.encode(), io_name.encode(), rank, nranks,
+                                  1 if column_major else 0)
         if not h:
             raise BP4Error(self.lib.bp4_last_error().decode())
         self.h = c_void_p(h)
@@ -169,6 +180,44 @@ class BP4Writer:
         if getattr(self, "h", None):
             self.lib.bp4_close(self.h)
             self.h = None
+
+
+def append_plan(path: str, keep_until_step: int, step_var: str = "step") -> Optional[Dict[str, Any]]:
+    """How to continue the BP4 output at ``path`` after a restart at ``keep_until_step``: keep
+    the leading steps whose ``step_var`` value is <= ``keep_until_step`` and cut off the rest.
+    Returns ``{"steps", "last_step", "md_end", "idx_end", "data_end": {subfile: bytes}}`` or
+    None when there is nothing to keep (no file, unreadable, or no step qualifies).  Read by
+    one rank and broadcast; every rank then opens its subfile with ``BP4Writer(append=...)``."""
+    try:
+        rd = BP4Reader(path)
+    except (BP4Error, OSError, struct.error):
+        return None
+    try:
+        keep, last = 0, None
+        for i in range(rd.steps):
+            try:
+                v = int(rd.read(step_var, i))
+            except BP4Error:
+                break
+            if v > keep_until_step:
+                break
+            keep, last = i + 1, v
+        if keep == 0:
+            return None
+        data_end: Dict[int, int] = {}
+        for i in range(keep):
+            for pg in rd.process_groups(i):
+                k = int(pg["rank"])
+                fh = rd._file(k)
+                fh.seek(pg["offset"])
+                (ln,) = struct.unpack("<Q", fh.read(8))
+                data_end[k] = max(data_end.get(k, 0), int(pg["offset"]) + 8 + int(ln))
+        return {"steps": keep, "last_step": last, "md_end": int(rd.records[keep - 1][5]),
+                "idx_end": 64 + 64 * keep, "data_end": data_end, "shapes": {
+                    n: tuple(vi.shape) for n, vi in rd.variables(keep - 1).items()},
+                "dtypes": {n: str(vi.dtype) for n, vi in rd.variables(keep - 1).items()}}
+    finally:
+        rd.close()
 
 
 # ------------------------------------------------------------------------------------------

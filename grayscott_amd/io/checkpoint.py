@@ -110,7 +110,9 @@ class CheckpointWriter:
         from .output import _Job
         self.finish()
         w = _open_writer(self.tmp, self.settings, self.domain, self.ctx)
-        u, v, wait = snap if snap is not None else sim.snapshot_fields()
+        # its own snapshot buffers when not sharing the output step's: an output step still
+        # being written must not see them overwritten
+        u, v, wait = snap if snap is not None else sim.snapshot_fields("checkpoint")
 
         def job():
             wait()

@@ -12,9 +12,19 @@ Parity:
 Arrays are declared row-major like the ADIOS2 C++ gray-scott example: shape {Lz,Ly,Lx},
 start {oz,oy,ox}, count {nz,ny,nx} with x fastest in memory -- the same bytes as the Julia
 column-major (x,y,z) declaration.  Each rank writes its own ``data.<rank>`` subfile; rank 0
-gathers the per-rank step metadata over the control plane and writes md.0 / md.idx.
-Writes are synchronous with respect to the caller; the GPU->host copy uses the compaction
-kernel (no full-buffer D2H as in the reference, defect D1/K14).
+gathers the per-rank step metadata over the control plane and writes md.0 / md.idx.  The
+GPU->host copy uses the compaction kernel (no full-buffer D2H as in the reference, D1/K14).
+
+``async_output`` (default true): a step is written behind the simulation -- device snapshot and
+D2H on an I/O stream, the data write on a host thread; ``flush`` (called by the next
+``write_step`` and by ``close``) joins it and commits its metadata, so a step is complete in
+the file once the following step starts or the stream is closed.  ``async_output = false``
+writes each step before ``write_step`` returns.
+
+Restart (``append_after_step``): the output history is kept -- the existing file's steps up to
+the restart step stay, later ones (written after the checkpoint by the failed run) are cut off,
+and the run appends from there (the ADIOS2 append semantics the reference's restart hook,
+GrayScott.jl:77-78, implies).
 """
 from __future__ import annotations
 
@@ -69,20 +79,45 @@ def _prepare_dir(path: str, ctx: DistContext) -> None:
     ctx.barrier()
 
 
+def _append_plan(path: str, step: int, domain, dtype, ctx: DistContext):
+    """Rank 0 decides whether (and where) the existing output at ``path`` is continued; the
+    plan is broadcast so every rank opens its subfile consistently."""
+    plan = None
+    if ctx.rank == 0 and os.path.isdir(path):
+        from .bp4 import append_plan
+        plan = append_plan(path, step)
+        Lx, Ly, Lz = domain.L
+        if plan is not None and (plan["shapes"].get("U") != (Lz, Ly, Lx) or
+                                 plan["dtypes"].get("U") != np.dtype(dtype).name):
+            import warnings
+            warnings.warn(f"{path}: existing output has another grid or precision; "
+                          "starting a new file")
+            plan = None
+    return ctx.broadcast_object(plan, src=0)
+
+
 class SimulationOutput:
     """ADIOSStream equivalent (IO.jl:15-22)."""
 
     IO_NAME = "SimulationOutput"
 
     def __init__(self, settings, domain, ctx: Optional[DistContext] = None, path: Optional[str] = None,
-                 io_name: Optional[str] = None, schemas: bool = True):
+                 io_name: Optional[str] = None, schemas: bool = True,
+                 append_after_step: Optional[int] = None):
         self.ctx = ctx or DistContext()
         self.settings = settings
         self.domain = domain
         self.path = path or settings.output
-        _prepare_dir(self.path, self.ctx)
-        self.w = BP4Writer(self.path, io_name or self.IO_NAME, self.ctx.rank, self.ctx.world_size)
         dtype = _NP[settings.dtype_name]
+        plan = None
+        if append_after_step is not None:
+            plan = _append_plan(self.path, int(append_after_step), domain, dtype, self.ctx)
+        if plan is None:
+            _prepare_dir(self.path, self.ctx)
+        self.kept_steps = plan["steps"] if plan else 0
+        self.last_step = plan["last_step"] if plan else None
+        self.w = BP4Writer(self.path, io_name or self.IO_NAME, self.ctx.rank, self.ctx.world_size,
+                           append=plan)
         if self.ctx.rank == 0:
             for key in ("F", "k", "dt", "Du", "Dv", "noise"):
                 self.w.define_attribute(key, float(getattr(settings, key)))
@@ -95,7 +130,7 @@ class SimulationOutput:
         self.w.define_variable("U", dtype, (Lz, Ly, Lx), (oz, oy, ox), (nz, ny, nx))
         self.w.define_variable("V", dtype, (Lz, Ly, Lx), (oz, oy, ox), (nz, ny, nx))
         self.steps_written = 0
-        self.async_io = bool(getattr(settings, "async_output", False))
+        self.async_io = bool(getattr(settings, "async_output", True))
         self._pending = None
 
     def define_attribute(self, name, value) -> None:
@@ -124,9 +159,10 @@ class SimulationOutput:
         if not self.async_io:
             u, v = sim.get_fields()
             self.write_fields(step, u, v)
+            self.last_step = step
             return None
         self.flush()
-        snap = sim.snapshot_fields()
+        snap = sim.snapshot_fields("output")
         u, v, wait = snap
 
         def job():
@@ -138,6 +174,7 @@ class SimulationOutput:
             return self.w.end_step()
 
         self._pending = _Job(job)
+        self.last_step = step
         return snap
 
     def flush(self) -> None:

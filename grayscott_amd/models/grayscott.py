@@ -216,30 +216,43 @@ class GrayScott:
             return u.cpu().numpy(), v.cpu().numpy()
         return u.numpy(), v.numpy()
 
-    def snapshot_fields(self):
+    def snapshot_fields(self, slot: str = "output"):
         """Asynchronous ghost-stripped copy of u, v for output: the compaction
         kernel runs in stream order on the compute stream, the D2H copy into pinned host
         buffers on a separate I/O stream, so stepping continues while the copy (and the file
         write that follows it) is in flight.  Returns ``(u, v, wait)``: numpy views of the host
-        buffers and a callable that blocks until they are filled.  The buffers are reused by
-        the next call, so consume them (``wait`` + write) before snapshotting again."""
+        buffers and a callable that blocks until they are filled.
+
+        Each ``slot`` (one per consumer: "output", "checkpoint") has its own device and host
+        buffers, reused by that slot's next call: the consumer must be done with them (its
+        write joined) before snapshotting the same slot again.  The device buffers are not
+        overwritten before the previous D2H copy out of them has finished (the compute stream
+        waits for it), so consumers of different slots never race."""
         if self.backend != "hip":
             u, v = self.get_fields()
             return u, v, lambda: None
         tdt = _TORCH_DTYPES[self.dtype]
-        if getattr(self, "_snap", None) is None:
+        if getattr(self, "_snaps", None) is None:
+            self._snaps = {}
+            self._io_stream = torch.cuda.Stream(self.device)
+        if slot not in self._snaps:
             dev = [torch.empty(self.local_shape, dtype=tdt, device=self.device) for _ in range(2)]
             host = [torch.empty(self.local_shape, dtype=tdt, pin_memory=True) for _ in range(2)]
-            self._snap = (dev, host, torch.cuda.Stream(self.device), torch.cuda.Event(),
-                          torch.cuda.Event())
-        dev, host, io_stream, ready, done = self._snap
+            self._snaps[slot] = [dev, host, None]
+        dev, host, prev_done = self._snaps[slot]
+        cur = torch.cuda.current_stream(self.device)
+        if prev_done is not None:
+            cur.wait_event(prev_done)  # the previous D2H out of dev[] has finished
         self.engine.extract(dev[0].data_ptr(), dev[1].data_ptr())
-        ready.record(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(io_stream):
-            io_stream.wait_event(ready)
+        ready = torch.cuda.Event()
+        ready.record(cur)
+        done = torch.cuda.Event()
+        with torch.cuda.stream(self._io_stream):
+            self._io_stream.wait_event(ready)
             host[0].copy_(dev[0], non_blocking=True)
             host[1].copy_(dev[1], non_blocking=True)
-            done.record(io_stream)
+            done.record(self._io_stream)
+        self._snaps[slot][2] = done
         return host[0].numpy(), host[1].numpy(), done.synchronize
 
     def set_fields(self, u, v) -> None:

@@ -1,0 +1,10 @@
+# Full GPU check: pytest -m gpu, smoke(), the driver's bench command.
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/${GS_OUT:-full}
+mkdir -p $O
+cd $R
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gputest.log 2>&1 &&
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 &&
+timeout -k 10 150 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_driver.json 2> $O/bench_driver.err
+echo "exit $?"

@@ -43,8 +43,11 @@ def test_tune_data_path_two_ranks():
 
 def test_candidates_for_mi355x():
     from grayscott_amd.parallel.autotune import candidates
-    assert candidates(512, 8, "hip") == [([1, 1, 8], 0, "auto"), ([1, 1, 8], 2, "auto"),
-                                        ([2, 2, 2], 0, "auto"), ([2, 2, 2], 0, "off"),
-                                        ([2, 2, 2], 2, "auto"), ([1, 2, 4], 0, "auto"),
+    # the reference's Dims_create grid first (always timed, reported as reference_grid), then
+    # z slabs with and without overlap
+    assert candidates(512, 8, "hip") == [([2, 2, 2], 0, "auto"), ([1, 1, 8], 0, "auto"),
+                                        ([1, 1, 8], 0, "off"), ([1, 1, 8], 2, "auto"),
+                                        ([2, 2, 2], 0, "off"), ([2, 2, 2], 2, "auto"),
+                                        ([1, 2, 4], 0, "auto"),
                                         ([1, 1, 8], 0, "auto", {"GS_OVERLAP_RESERVE": "64"})]
     assert candidates(512, 1, "hip") == [([1, 1, 1], 0, "auto")]

@@ -136,33 +136,73 @@ def test_checkpoint_restart_bitwise(tmp_path):
                     restart_input="ck.bp"), 3, str(part))
     assert r.returncode == 0, r.stderr[-3000:]
     with BP4Reader(str(full / "o.bp")) as a, BP4Reader(str(part / "b.bp")) as b:
-        assert b.steps == 1 and b.read("step", 0) == 40
-        np.testing.assert_array_equal(a.read("U", -1), b.read("U", -1))
-        np.testing.assert_array_equal(a.read("V", -1), b.read("V", -1))
+        # a new output file starts with the restart step (the restored state, bit for bit)
+        assert [b.read("step", i) for i in range(b.steps)] == [20, 40]
+        for i in range(2):
+            np.testing.assert_array_equal(a.read("U", i), b.read("U", i))
+            np.testing.assert_array_equal(a.read("V", i), b.read("V", i))
 
 
 def test_fault_injection_and_recovery(tmp_path):
     """A run killed after step 30 resumes from its last checkpoint (step 30) and ends with the
-    same state as an uninterrupted run."""
+    same output history as an uninterrupted run: the same step list (the restart keeps the
+    steps written before the failure, cuts off nothing it needs, and rewrites the step the dead
+    run had not committed) and bitwise the same U/V at every step."""
     ref = tmp_path / "ref"
     ref.mkdir()
-    r = launch(_cfg(ref, "c.toml", L=20, steps=50, plotgap=50, output="o.bp"), 2, str(ref))
+    r = launch(_cfg(ref, "c.toml", L=20, steps=50, plotgap=10, output="o.bp"), 2, str(ref))
     assert r.returncode == 0, r.stderr[-3000:]
     run = tmp_path / "run"
     run.mkdir()
-    cfg = _cfg(run, "c.toml", L=20, steps=50, plotgap=50, output="o.bp", checkpoint=True,
+    cfg = _cfg(run, "c.toml", L=20, steps=50, plotgap=10, output="o.bp", checkpoint=True,
                checkpoint_freq=10, checkpoint_output="ck.bp")
     r = launch(cfg, 2, str(run), env={"GS_FAIL_AT_STEP": "30"})
     assert r.returncode != 0
     with BP4Reader(str(run / "ck.bp")) as ck:
         assert ck.read("step") == 30
-    cfg2 = _cfg(run, "c2.toml", L=20, steps=50, plotgap=50, output="o.bp", checkpoint=True,
+    with BP4Reader(str(run / "o.bp")) as b:
+        assert [b.read("step", i) for i in range(b.steps)] in ([10, 20], [10, 20, 30])
+    # restart with another rank count: the subfiles of the dead run's ranks stay referenced
+    cfg2 = _cfg(run, "c2.toml", L=20, steps=50, plotgap=10, output="o.bp", checkpoint=True,
                 checkpoint_freq=10, checkpoint_output="ck.bp", restart=True, restart_input="ck.bp")
-    r = launch(cfg2, 2, str(run))
+    r = launch(cfg2, 3, str(run))
     assert r.returncode == 0, r.stderr[-3000:]
     with BP4Reader(str(ref / "o.bp")) as a, BP4Reader(str(run / "o.bp")) as b:
-        np.testing.assert_array_equal(a.read("U", -1), b.read("U", -1))
-        np.testing.assert_array_equal(a.read("V", -1), b.read("V", -1))
+        steps_a = [a.read("step", i) for i in range(a.steps)]
+        steps_b = [b.read("step", i) for i in range(b.steps)]
+        assert steps_a == steps_b == [10, 20, 30, 40, 50]
+        for i in range(a.steps):
+            np.testing.assert_array_equal(a.read("U", i), b.read("U", i))
+            np.testing.assert_array_equal(a.read("V", i), b.read("V", i))
+        assert b.attributes["F"] == a.attributes["F"]
+
+
+def test_restart_cuts_off_later_output_steps(tmp_path):
+    """Restarting from an older checkpoint drops the output steps written after it and
+    continues the file from there (no duplicate or stale steps)."""
+    run = tmp_path / "run"
+    run.mkdir()
+    # checkpoints every 10 steps into separate files: keep the step-20 one aside
+    cfg = _cfg(run, "c.toml", L=16, steps=20, plotgap=5, output="o.bp", checkpoint=True,
+               checkpoint_freq=20, checkpoint_output="ck20.bp")
+    assert launch(cfg, 1, str(run)).returncode == 0
+    cfg = _cfg(run, "c1.toml", L=16, steps=35, plotgap=5, output="o.bp", restart=True,
+               restart_input="ck20.bp")
+    assert launch(cfg, 2, str(run)).returncode == 0
+    with BP4Reader(str(run / "o.bp")) as b:
+        assert [b.read("step", i) for i in range(b.steps)] == [5, 10, 15, 20, 25, 30, 35]
+    # now go back to step 20 again: 25..35 are cut off and rewritten
+    cfg = _cfg(run, "c2.toml", L=16, steps=30, plotgap=5, output="o.bp", restart=True,
+               restart_input="ck20.bp")
+    assert launch(cfg, 1, str(run)).returncode == 0
+    ref = tmp_path / "ref"
+    ref.mkdir()
+    assert launch(_cfg(ref, "c.toml", L=16, steps=30, plotgap=5, output="o.bp"), 1,
+                  str(ref)).returncode == 0
+    with BP4Reader(str(ref / "o.bp")) as a, BP4Reader(str(run / "o.bp")) as b:
+        assert [b.read("step", i) for i in range(b.steps)] == [5, 10, 15, 20, 25, 30]
+        for i in range(a.steps):
+            np.testing.assert_array_equal(a.read("U", i), b.read("U", i))
 
 
 def test_one_failing_rank_ends_the_job(tmp_path):

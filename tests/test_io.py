@@ -192,24 +192,51 @@ def test_async_output_matches_sync(tmp_path):
         np.testing.assert_array_equal(va, vb)
 
 
-def test_async_checkpoint_matches_sync(tmp_path):
-    """async_checkpoint (data written on a host thread, committed at the next event / end)
-    leaves the same checkpoint as the synchronous writer, including when it shares the
-    output step's snapshot (plotgap 3, checkpoint_freq 6) and when it does not (freq 4)."""
+def _async_vs_sync(tmp_path, backend, L, steps, plotgap, freqs):
+    """Run the driver with asynchronous output + checkpoints and fully synchronously; every
+    output step and the final checkpoint must be bitwise equal."""
     from grayscott_amd import driver
 
-    for freq in (6, 4):
-        res = {}
+    for freq in freqs:
+        res, outs = {}, {}
         for mode in (False, True):
-            s = Settings(L=20, steps=14, plotgap=3, noise=0.1, F=0.02, k=0.048, dt=1.0, Du=0.2,
-                         Dv=0.1, precision="Float32", backend="CPU", async_checkpoint=mode,
-                         checkpoint=True, checkpoint_freq=freq,
+            s = Settings(L=L, steps=steps, plotgap=plotgap, noise=0.1, F=0.02, k=0.048, dt=1.0,
+                         Du=0.2, Dv=0.1, precision="Float32", backend=backend,
+                         async_checkpoint=mode, async_output=mode, checkpoint=True,
+                         checkpoint_freq=freq,
                          checkpoint_output=str(tmp_path / f"ck_{freq}_{mode}.bp"),
                          output=str(tmp_path / f"gs_{freq}_{mode}.bp"))
             driver.run(s, out=open(os.devnull, "w"))
             assert not os.path.exists(s.checkpoint_output + ".tmp")
             with BP4Reader(s.checkpoint_output) as r:
                 res[mode] = (int(r.read("step")), r.read("U", -1), r.read("V", -1))
-        assert res[True][0] == res[False][0] == (14 // freq) * freq
+            with BP4Reader(s.output) as r:
+                outs[mode] = [(int(r.read("step", i)), r.read("U", i), r.read("V", i))
+                              for i in range(r.steps)]
+        assert res[True][0] == res[False][0] == (steps // freq) * freq
         np.testing.assert_array_equal(res[True][1], res[False][1])
         np.testing.assert_array_equal(res[True][2], res[False][2])
+        assert [o[0] for o in outs[True]] == [o[0] for o in outs[False]] == \
+            list(range(plotgap, steps + 1, plotgap))
+        for a, b in zip(outs[True], outs[False]):
+            np.testing.assert_array_equal(a[1], b[1])
+            np.testing.assert_array_equal(a[2], b[2])
+
+
+def test_async_checkpoint_matches_sync(tmp_path):
+    """async_checkpoint / async_output (data written on host threads, committed at the next
+    event / end) leave the same checkpoint and output as the synchronous writers, including
+    when the checkpoint shares the output step's snapshot (plotgap 3, checkpoint_freq 6) and
+    when it does not (freq 4)."""
+    _async_vs_sync(tmp_path, "CPU", 20, 14, 3, (6, 4))
+
+
+@pytest.mark.gpu
+def test_async_checkpoint_matches_sync_gpu(tmp_path):
+    """The same on the HIP path, where the snapshots live in reused pinned host buffers and
+    device staging buffers ordered by events: checkpoints that do not share an output step's
+    snapshot (freq 4 vs plotgap 3) must not disturb the output step still being written."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _async_vs_sync(tmp_path, "AMDGPU", 96, 40, 3, (4, 6))
