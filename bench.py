@@ -74,6 +74,9 @@ def main(argv=None) -> int:
         # self-launch: one worker per GPU, before anything initialises HIP in this process
         return spawn_local(ngpus, [sys.executable, os.path.abspath(__file__)] + argv,
                            timeout=args.timeout or None, cwd=ROOT)
+    # a blocked halo wait or control-plane collective becomes an error after this long (the
+    # driver's own limit is minutes; a hung rank must not eat it)
+    os.environ.setdefault("GS_COMM_TIMEOUT", "120")
     if ngpus != world:
         print(f"bench.py: --gpus {ngpus} but the launcher started {world} ranks", file=sys.stderr)
         return 2

@@ -115,6 +115,11 @@ class GrayScott:
             for k in chain:
                 try:
                     self._setup_transport(k)
+                    # a transport can set up and still fail on first use (e.g. NCCL through
+                    # torch with two ranks on one GPU): prove it with one exchange of the
+                    # (not yet initialised) buffers -- ghost cells only, refilled by init
+                    self.engine.exchange()
+                    self.engine.sync()
                     ok = self.ctx.allreduce(1.0, "min") if self.ctx.is_distributed else 1.0
                 except Exception as ex:  # pragma: no cover - exercised on multi-GPU nodes
                     errors.append(f"{k}: {ex}")

@@ -171,6 +171,8 @@ def tune_data_path(settings, ctx, L: int, backend: str,
         attempts = [(settings.transport, ov0, {}),
                     (settings.transport, "off", {"GS_INPLACE_HALO": "0"}),
                     ("torch", "off", {"GS_INPLACE_HALO": "0"})]
+        if backend == "hip":
+            attempts.append(("host", "off", {"GS_INPLACE_HALO": "0"}))
         if proven is not None:
             attempts = [(proven, ov0, {})]
         for tr, ov, extra in attempts:
