@@ -213,7 +213,10 @@ struct FCfg {
   static constexpr bool PERIODIC = PERIODIC_, NOISE = NOISE_, SKEW = SKEW_, Q32 = Q32_;
   static constexpr int ABL = ABL_;
   static constexpr int R = PF + 2;                    // level-0 ring slots
-  static constexpr int NS = SKEW ? 3 : 2;             // level-l output ring / xch buffers
+  // level-l output ring / xch buffers: 2 slots.  Skewed: level l+1 reads level l's outputs of
+  // the two previous iterations (input and centre), and the levels run top-down within an
+  // iteration, so level l overwrites its p-2 output only after level l+1 has consumed it.
+  static constexpr int NS = 2;
   static constexpr int PERIOD = gs_lcm(R, NS);
   static constexpr int NO = TL > 1 ? TL - 1 : 1;
   static constexpr int RT = ROWS * WAVES;                 // tile rows
@@ -355,7 +358,8 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
     if constexpr (!(C::ABL & 1)) __syncthreads();
   }
 #pragma unroll
-  for (int l = 0; l < TL; ++l) {
+  for (int li = 0; li < TL; ++li) {
+    const int l = C::SKEW ? TL - 1 - li : li;  // skewed: top level first (see NS)
     // input plane of consumer l and the centre plane one before it
     constexpr int kIn = C::SKEW ? (IS + NS - 1) % NS : IS;
     constexpr int kC = C::SKEW ? (IS + NS - 2) % NS : (IS + NS - 1) % NS;
@@ -744,9 +748,10 @@ inline const FusedCfgEntry* fused_cfg_table(int* n) {
       {"4x6:2", false, true},    // 16
       {"4x4:2", false, true},    // 17
       {"4x16:1", true, false},   // 18
+      {"4x16:1s", true, false},  // 19  64-row tile, 4 waves per SIMD (fits 128 VGPRs)
 #ifdef GS_ABLATION
-      {"4x12:2s-abl1", true, false},  // 19  no barriers
-      {"4x12:2s-abl2", true, false},  // 20  L2-resident loads
+      {"4x12:2s-abl1", true, false},  // 20  no barriers
+      {"4x12:2s-abl2", true, false},  // 21  L2-resident loads
 #endif
   };
   *n = (int)(sizeof(t) / sizeof(t[0]));
@@ -809,9 +814,10 @@ void run_fused_cfg(const void* s, void* d, const FusedArgs& a, const gs::Params&
       case 13: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true>, T>::run(s, d, a, p, st); return;
       case 15: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true>, T>::run(s, d, a, p, st); return;
       case 18: FusedLaunch<FCfg<T, TL, 4, 16, 1, PER, NZ>, T>::run(s, d, a, p, st); return;
+      case 19: FusedLaunch<FCfg<T, TL, 4, 16, 1, PER, NZ, true>, T>::run(s, d, a, p, st); return;
 #ifdef GS_ABLATION
-      case 19: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 1>, T>::run(s, d, a, p, st); return;
-      case 20: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 2>, T>::run(s, d, a, p, st); return;
+      case 20: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 1>, T>::run(s, d, a, p, st); return;
+      case 21: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 2>, T>::run(s, d, a, p, st); return;
 #endif
       default: break;  // 0 and 14: the default shape below
     }

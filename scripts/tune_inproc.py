@@ -25,6 +25,10 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--noise", type=float, default=0.1)
     ap.add_argument("--sched", type=int, nargs="+", default=[0])
+    ap.add_argument("--init", choices=["seed", "random"], default="seed",
+                    help="random: every timed run starts from the same u, v ~ U[0,1) state "
+                         "(the benchmark's; power-limited regime), after --warmup steps")
+    ap.add_argument("--warmup", type=int, default=12)
     a = ap.parse_args()
     import torch
     from grayscott_amd.models.grayscott import GrayScott
@@ -47,13 +51,17 @@ def main():
                     for sched in a.sched:
                         native.fused_select(cfg)
                         native.fused_sched(sched)
-                        sim.iterate(12)
+                        if a.init == "random":
+                            sim.randomize_fields(seed=2024)
+                            sim.set_step(0)
+                        sim.iterate(a.warmup)
                         torch.cuda.synchronize()
                         t0 = time.perf_counter()
                         sim.iterate(a.steps)
                         torch.cuda.synchronize()
                         dt = time.perf_counter() - t0
-                        key = f"L={L} fuse={fuse} cfg={cfg or 'default'} sched={sched}"
+                        key = (f"L={L} fuse={fuse} cfg={cfg or 'default'} sched={sched}"
+                               f"{' random' if a.init == 'random' else ''}")
                         results.setdefault(key, []).append(L ** 3 * a.steps / dt / 1e6)
         for sim in sims.values():
             sim.close()
