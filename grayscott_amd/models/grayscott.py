@@ -261,10 +261,15 @@ class GrayScott:
         return host[0].numpy(), host[1].numpy(), done.synchronize
 
     def set_fields(self, u, v) -> None:
-        """Overwrite the interior of the current state (restart)."""
+        """Overwrite the interior of the current state (restart).  ``u``, ``v``: (nz, ny, nx)
+        numpy arrays or torch tensors (any device)."""
         tdt = _TORCH_DTYPES[self.dtype]
-        tu = torch.as_tensor(np.ascontiguousarray(u)).to(device=self.device, dtype=tdt).contiguous()
-        tv = torch.as_tensor(np.ascontiguousarray(v)).to(device=self.device, dtype=tdt).contiguous()
+
+        def dev(a):
+            a = a if isinstance(a, torch.Tensor) else torch.as_tensor(np.ascontiguousarray(a))
+            return a.to(device=self.device, dtype=tdt).contiguous()
+
+        tu, tv = dev(u), dev(v)
         if tuple(tu.shape) != self.local_shape or tuple(tv.shape) != self.local_shape:
             raise ValueError(f"expected local arrays of shape {self.local_shape}")
         self.engine.insert(tu.data_ptr(), tv.data_ptr())
