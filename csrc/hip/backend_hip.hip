@@ -100,6 +100,15 @@ class HipBackend final : public gs::Backend {
     HIP_CHECK(hipGetLastError());
   }
 
+  void fill_boxes(int b, const Box* boxes, int n, double u, double v) override {
+    if (n > 6) {
+      gs::Backend::fill_boxes(b, boxes, n, u, v);
+      return;
+    }
+    gsk::launch_fill_boxes<T>(buf_[b], g_, boxes, n, (T)u, (T)v, stream_);
+    HIP_CHECK(hipGetLastError());
+  }
+
   void seed(int b) override {
     gsk::launch_seed<T>(buf_[b], g_, stream_);
     HIP_CHECK(hipGetLastError());

@@ -51,6 +51,41 @@ void launch_fill(typename Vec2<T>::type* f, const Geom& g, const Box& b, T u, T 
   k_fill<T><<<blocks, 256, 0, s>>>(f, g, b, u, v);
 }
 
+// up to 6 boxes in one launch (blockIdx.y = box): the outer ghost faces of a buffer
+struct FillBoxes {
+  Box box[6];
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_fill_boxes(typename Vec2<T>::type* __restrict__ f, Geom g,
+                                                    FillBoxes bs, T u, T v) {
+  const Box b = bs.box[blockIdx.y];
+  const uint32_t n = (uint32_t)gs::box_cells(b);  // a ghost face of one sub-domain: < 2^31
+  const uint32_t bnx = (uint32_t)b.nx, bny = (uint32_t)b.ny;
+  typename Vec2<T>::type c;
+  c.x = u;
+  c.y = v;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t r = i / bnx;
+    const uint32_t z = r / bny;
+    f[gs::lin(g, b.x0 + (int)(i - r * bnx), b.y0 + (int)(r - z * bny), b.z0 + (int)z)] = c;
+  }
+}
+
+template <typename T>
+void launch_fill_boxes(typename Vec2<T>::type* f, const Geom& g, const Box* boxes, int n, T u, T v,
+                       hipStream_t s) {
+  FillBoxes bs{};
+  int64_t mx = 0;
+  for (int i = 0; i < n; ++i) {
+    bs.box[i] = boxes[i];
+    mx = std::max<int64_t>(mx, gs::box_cells(boxes[i]));
+  }
+  if (n <= 0 || mx == 0) return;
+  const int bx = (int)std::max<int64_t>(1, std::min<int64_t>((mx + 255) / 256, 2048));
+  k_fill_boxes<T><<<dim3(bx, n, 1), 256, 0, s>>>(f, g, bs, u, v);
+}
+
 template <typename T>
 void launch_seed(typename Vec2<T>::type* f, const Geom& g, hipStream_t s) {
   // global cube [L/2-6, L/2+6]^3 clipped to this rank

@@ -32,6 +32,10 @@ class Backend {
   virtual ~Backend() {}
   // fill box of buffer b with a constant (u,v) pair
   virtual void fill_box(int b, const Box& box, double u, double v) = 0;
+  // several boxes of buffer b with one (u,v) pair (the outer ghost faces: one launch on GPU)
+  virtual void fill_boxes(int b, const Box* boxes, int n, double u, double v) {
+    for (int i = 0; i < n; ++i) fill_box(b, boxes[i], u, v);
+  }
   // one explicit Euler step over `region`, reading buffer src at time t, writing dst
   virtual void step(int src, int dst, const Box& region, int64_t t) = 0;
   // temporally blocked kernel: n steps over the interior, src at time t -> dst at t+n.
@@ -239,6 +243,8 @@ class Engine {
     if (bc_parity_[b] == par) return;
     const double u = bc_u(t);
     const int H = g.H;
+    Box faces[6];
+    int nf = 0;
     for (int a = 0; a < 3; ++a)
       for (int s = -1; s <= 1; s += 2) {
         int dd[3] = {0, 0, 0};
@@ -250,8 +256,9 @@ class Engine {
         const int n = a == 0 ? g.nx : (a == 1 ? g.ny : g.nz);
         *o = s < 0 ? -H : n;
         *c = H;
-        be_->fill_box(b, bx, u, 0.0);
+        faces[nf++] = bx;
       }
+    if (nf) be_->fill_boxes(b, faces, nf, u, 0.0);
     bc_parity_[b] = par;
   }
 
