@@ -168,7 +168,7 @@ print(max(np.abs(out[0][0] - out[1][0]).max(), np.abs(out[0][1] - out[1][1]).max
 @pytest.mark.parametrize("cfg,sched", [
     ("4x8:1", 0), ("8x4:1", 0), ("4x12:2", 0), ("8x4:1s", 0), ("8x4:4s", 0), ("4x8:1s", 0),
     ("4x8:4s", 0), ("", 1), ("8x4:2", 1), ("4x8:4s", 1), ("", 2), ("4x8:1", 2), ("4x8:2", 0),
-    ("4x12:3", 2), ("4x12:1s", 2), ("4x12:2s", 1), ("4x12:1", 0)])
+    ("4x12:3", 2), ("4x12:1s", 2), ("4x12:2s", 1), ("4x12:1", 0), ("4x16:1s", 2)])
 @pytest.mark.parametrize("fuse", [2, 3])
 def test_fused_tuning_configs_agree(cfg, sched, fuse):
     """Every selectable fused-kernel configuration / schedule reproduces the single-step path."""
