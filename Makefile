@@ -38,6 +38,11 @@ $(OUT)/libgs_hip_abl.so: $(HIP_SRC) $(HDRS)
 
 ablation: $(OUT)/libgs_hip_abl.so
 
+# no VALU-write -> DPP-read hazard in the shipped code object (the fused kernel's DPP sums are
+# inline asm without wait states; scripts/check_dpp_hazards.py, tests/test_isa_hazards.py)
+check-isa: $(OUT)/libgs_hip.so
+	python3 scripts/check_dpp_hazards.py $(OUT)/libgs_hip.so
+
 SELFTEST_TMP ?= /tmp
 SELFTEST_SRC := csrc/tools/core_selftest.cpp $(CORE_SRC)
 
@@ -73,4 +78,4 @@ clean:
 	rm -f $(OUT)/*.so
 	rm -rf build
 
-.PHONY: all clean selftest asan tsan tools ablation
+.PHONY: all clean selftest asan tsan tools ablation check-isa

@@ -23,7 +23,8 @@
 // r2_power_probe.txt: the same dispatch runs at the full clock on smooth data and ~20 % slower
 // on rough data, with identical cycle counts), so every VALU instruction counts:
 //  * fp32 arithmetic on the interleaved (u, v) pairs is packed (v_pk_add/v_pk_mul/v_pk_fma_f32);
-//  * the x-neighbour pair sum is one DPP move + one DPP add;
+//  * the x-neighbour pair sum and the y/z partial sum are two DPP adds, with no hazard wait
+//    states (checked on the built code object);
 //  * the LDS row exchange wraps around (wave 0 reads the last wave's row: a tile-halo row whose
 //    value never reaches an output), so the exchange has no branches or register copies;
 //  * waves whose rows are all outside a level's dependency cone skip that level (the row slack
@@ -127,6 +128,12 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return r;
 }
 
+__device__ __forceinline__ uint32_t xor3v(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 constexpr uint32_t kPhM0 = 0xD2511F53u, kPhM1 = 0xCD9E8D57u;
 constexpr uint32_t kPhW0 = 0x9E3779B9u, kPhW1 = 0xBB67AE85u;
 
@@ -137,9 +144,11 @@ constexpr uint32_t kPhW0 = 0x9E3779B9u, kPhW1 = 0xBB67AE85u;
 // SALU ops.
 //   Q32 (c1 = 0): round 1's second product and the round-2 first product see only
 //   wave-uniform words, so rounds 1-3 cost 1 + 3 + 4 VALU instead of 4 + 4 + 4.
-template <bool Q32>
+//   KV: the round keys of rounds 4-10 come from VGPRs (kv, filled once per kernel) instead of
+//   being rebuilt on the SALU at every call.
+template <bool Q32, bool KV = false>
 __device__ __forceinline__ gs::U4 philox_dev(uint32_t c0, uint32_t c1, uint64_t step,
-                                             uint64_t seed) {
+                                             uint64_t seed, const uint32_t* kv = nullptr) {
   uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
   uint32_t s0 = (uint32_t)step, s1 = (uint32_t)(step >> 32);
   asm volatile("" : "+s"(k0), "+s"(k1), "+s"(s0), "+s"(s1));
@@ -183,11 +192,17 @@ __device__ __forceinline__ gs::U4 philox_dev(uint32_t c0, uint32_t c1, uint64_t 
   for (int r = 3; r < 10; ++r) {
     const uint64_t m0 = (uint64_t)kPhM0 * c0;
     const uint64_t m1 = (uint64_t)kPhM1 * c2;
-    const uint32_t n0 = xor3((uint32_t)(m1 >> 32), c1, k0);
-    const uint32_t n2 = xor3((uint32_t)(m0 >> 32), c3, k1);
+    uint32_t n0, n2;
+    if constexpr (KV) {
+      n0 = xor3v((uint32_t)(m1 >> 32), c1, kv[2 * (r - 3)]);
+      n2 = xor3v((uint32_t)(m0 >> 32), c3, kv[2 * (r - 3) + 1]);
+    } else {
+      n0 = xor3((uint32_t)(m1 >> 32), c1, k0);
+      n2 = xor3((uint32_t)(m0 >> 32), c3, k1);
+      k0 += kPhW0;
+      k1 += kPhW1;
+    }
     c0 = n0; c1 = (uint32_t)m1; c2 = n2; c3 = (uint32_t)m0;
-    k0 += kPhW0;
-    k1 += kPhW1;
   }
   return gs::U4{c0, c1, c2, c3};
 }
@@ -196,11 +211,12 @@ __device__ __forceinline__ gs::U4 philox_dev(uint32_t c0, uint32_t c1, uint64_t 
 //   ROWS x WAVES : rows per wave x waves per workgroup (tile height = ROWS*WAVES)
 //   PF           : level-0 prefetch distance in planes (register ring of PF+2 planes)
 //   SKEW         : level l consumes level l-1's output of the previous iteration, so all
-//                  levels share ONE workgroup barrier per plane (output ring of 3)
+//                  levels share ONE workgroup barrier per plane
 //   Q32          : the Philox counter fits 32 bits (rounds 1-3 partly on the SALU)
 //   ABL          : ablations for timing experiments, GS_ABLATION builds only (results are
 //                  WRONG by design): bit0 no workgroup barriers, bit1 every level-0 load reads
-//                  plane 0 (L2-resident)
+//                  plane 0 (L2-resident); bit2 (exact) Philox round keys 4-10 in VGPRs; bit3
+//                  (exact) the x-neighbour sums' leading s_nop restored
 constexpr int gs_gcd(int a, int b) { return b == 0 ? a : gs_gcd(b, a % b); }
 constexpr int gs_lcm(int a, int b) { return a / gs_gcd(a, b) * b; }
 
@@ -212,6 +228,7 @@ struct FCfg {
   static constexpr int TL = TL_, ROWS = ROWS_, WAVES = WAVES_, PF = PF_;
   static constexpr bool PERIODIC = PERIODIC_, NOISE = NOISE_, SKEW = SKEW_, Q32 = Q32_;
   static constexpr int ABL = ABL_;
+  static constexpr bool KV = (ABL_ & 4) != 0;
   static constexpr int R = PF + 2;                    // level-0 ring slots
   // level-l output ring / xch buffers: 2 slots.  Skewed: level l+1 reads level l's outputs of
   // the two previous iterations (input and centre), and the levels run top-down within an
@@ -230,6 +247,7 @@ struct FusedState {
   using V2 = typename C::V2;
   typename C::T ar31;  // dt * noise * 2^-31 held in a VGPR (an SGPR copy spills)
   typename C::V2 kc;   // (dt F, 0) held in VGPRs (the first packed FMA's addend)
+  uint32_t kv[C::KV ? 14 : 1];  // Philox round keys of rounds 4-10 (C::KV)
   V2 LD[C::R][C::ROWS];
   V2 OUT[C::NO][C::NS][C::ROWS];
   V2 A[C::TL][C::ROWS];
@@ -256,37 +274,37 @@ __device__ __forceinline__ int64_t gwrap(int64_t v, int64_t L) {
   else return v;
 }
 
-// left + right x-neighbours in two instructions: one DPP move and one DPP add.  Same rounding
-// as lane_from_left(v) + lane_from_right(v).  The leading s_nop covers the VALU-write -> DPP
-// read hazard the compiler cannot see through inline asm.
-__device__ __forceinline__ float lane_pair_sum(float v) {
-  float t, r;
-  asm volatile(
-      "s_nop 1\n\t"
-      "v_mov_b32_dpp %1, %2 wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %0, %2, %1 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1"
-      : "=v"(r), "=&v"(t)
-      : "v"(v));
-  return r;
-}
-__device__ __forceinline__ double lane_pair_sum(double v) {
-  return lane_from_left(v) + lane_from_right(v);
-}
-
-// v[lane-1] + v[lane+1] + s in two DPP adds (the right neighbour is added to s first):
-// folds the y/z partial sum into the x-neighbour instructions.
+// v[lane-1] + v[lane+1] + s in two DPP adds (the right neighbour is added to s first): the
+// y/z partial sum folds into the x-neighbour instructions.  Lanes without a source read 0
+// (bound_ctrl); they only feed tile-halo cells.
+//   No hazard wait states: a DPP read of a VGPR needs 2 wait states after a VALU write of it,
+//   and the DPP sources here are level-0 planes (written by buffer loads, not the VALU) or
+//   level outputs written in an earlier pipeline iteration.  The compiler cannot see through
+//   the asm, so the built code object is checked instead: scripts/check_dpp_hazards.py scans
+//   every DPP instruction of libgs_hip.so (`make check-isa`, tests/test_isa_hazards.py).  The
+//   ablation bit 8 restores the leading `s_nop 1` (2.8 % slower, profiles/r2_ab_dpp_nop.txt).
+template <bool NOP>
 __device__ __forceinline__ float lane_pair_sum_add(float v, float s) {
   float t, r;
-  asm volatile(
-      "s_nop 1\n\t"
-      "v_add_f32_dpp %1, %2, %3 wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %0, %2, %1 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1"
-      : "=v"(r), "=&v"(t)
-      : "v"(v), "v"(s));
+  if constexpr (NOP) {
+    asm volatile(
+        "s_nop 1\n\t"
+        "v_add_f32_dpp %1, %2, %3 wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_add_f32_dpp %0, %2, %1 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+        : "=v"(r), "=&v"(t)
+        : "v"(v), "v"(s));
+  } else {
+    asm volatile(
+        "v_add_f32_dpp %1, %2, %3 wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_add_f32_dpp %0, %2, %1 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+        : "=v"(r), "=&v"(t)
+        : "v"(v), "v"(s));
+  }
   return r;
 }
+template <bool NOP>
 __device__ __forceinline__ double lane_pair_sum_add(double v, double s) {
-  return lane_from_left(v) + lane_from_right(v) + s;
+  return lane_from_left(v) + lane_from_right(v) + s;  // compiler DPP moves (hazards handled)
 }
 
 // One (u, v) pair from LDS as a single 8-byte ds_read_b64.
@@ -311,7 +329,8 @@ __device__ __forceinline__ typename C::V2 cell_update(typename C::V2& A, typenam
   using V2 = typename C::V2;
   const V2 s = A + in;
   const V2 yz = (ym + yp) + c;
-  A = V2{lane_pair_sum_add(in.x, yz.x), lane_pair_sum_add(in.y, yz.y)};
+  constexpr bool nop = (C::ABL & 8) != 0;
+  A = V2{lane_pair_sum_add<nop>(in.x, yz.x), lane_pair_sum_add<nop>(in.y, yz.y)};
   // uvv in both halves: (cu cv, cv cv) then (cu cv cv, cu cv cv)
   const V2 t = c * c.yy;
   const V2 uvv = t.xx * c.yy;
@@ -387,13 +406,13 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
             const uint32_t Ly4 = (uint32_t)((g.Ly + 3) >> 2);
             const uint32_t gy4 = (uint32_t)(gwrap<C>(sg.gy0 + 4 * m, g.Ly) >> 2);
             const uint32_t qu = (uint32_t)g.Lx * (gy4 + Ly4 * (uint32_t)gz);
-            blk = philox_dev<true>(qu + sg.gx32, 0u, tstep, seed);
+            blk = philox_dev<true, C::KV>(qu + sg.gx32, 0u, tstep, seed, S.kv);
           } else {
             const int64_t gyq = gwrap<C>(sg.gy0 + 4 * m, g.Ly);
             const uint64_t Ly4 = ((uint64_t)g.Ly + 3) >> 2;
             const uint64_t qq = (uint64_t)sg.gx + (uint64_t)g.Lx * ((uint64_t)(gyq >> 2) +
                                                                    Ly4 * (uint64_t)gz);
-            blk = philox_dev<false>((uint32_t)qq, (uint32_t)(qq >> 32), tstep, seed);
+            blk = philox_dev<false, C::KV>((uint32_t)qq, (uint32_t)(qq >> 32), tstep, seed, S.kv);
           }
         }
 #pragma unroll
@@ -536,6 +555,15 @@ __global__ __launch_bounds__(64 * C::WAVES, 1) void k_fused(const typename C::V2
     } else {
       asm volatile("v_mov_b64 %0, %1" : "=v"(S.kc.x) : "s"(k0));
       asm volatile("v_mov_b64 %0, %1" : "=v"(S.kc.y) : "s"(k1));
+    }
+  }
+  if constexpr (C::KV) {
+#pragma unroll
+    for (int r = 3; r < 10; ++r) {
+      const uint32_t k0 = (uint32_t)seed + (uint32_t)r * kPhW0;
+      const uint32_t k1 = (uint32_t)(seed >> 32) + (uint32_t)r * kPhW1;
+      asm volatile("v_mov_b32 %0, %1" : "=v"(S.kv[2 * (r - 3)]) : "s"(k0));
+      asm volatile("v_mov_b32 %0, %1" : "=v"(S.kv[2 * (r - 3) + 1]) : "s"(k1));
     }
   }
   if constexpr (C::NOISE) {
@@ -752,6 +780,10 @@ inline const FusedCfgEntry* fused_cfg_table(int* n) {
 #ifdef GS_ABLATION
       {"4x12:2s-abl1", true, false},  // 20  no barriers
       {"4x12:2s-abl2", true, false},  // 21  L2-resident loads
+      {"4x12:1s-abl4", true, false},  // 22  Philox keys in VGPRs (exact)
+      {"4x12:2s-abl4", true, false},  // 23  Philox keys in VGPRs (exact)
+      {"4x12:1s-abl8", true, false},  // 24  DPP sums with the s_nop (exact)
+      {"4x12:1s-abl12", true, false}, // 25  abl4 + abl8 (exact)
 #endif
   };
   *n = (int)(sizeof(t) / sizeof(t[0]));
@@ -818,6 +850,10 @@ void run_fused_cfg(const void* s, void* d, const FusedArgs& a, const gs::Params&
 #ifdef GS_ABLATION
       case 20: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 1>, T>::run(s, d, a, p, st); return;
       case 21: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 2>, T>::run(s, d, a, p, st); return;
+      case 22: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;
+      case 23: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;
+      case 24: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 8>, T>::run(s, d, a, p, st); return;
+      case 25: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 12>, T>::run(s, d, a, p, st); return;
 #endif
       default: break;  // 0 and 14: the default shape below
     }
