@@ -28,6 +28,9 @@ def main():
     ap.add_argument("--reps", type=int, default=40)
     ap.add_argument("--out", default="")
     ap.add_argument("--packed", action="store_true")
+    ap.add_argument("--one-sided", action="store_true",
+                    help="packed: the rank of a non-periodic grid at the low corner (neighbours "
+                         "only at +x, +y, +z: BASELINE config 3's 2x2x2 ranks all look like this)")
     a = ap.parse_args()
     import torch
     from grayscott_amd.models.grayscott import GrayScott
@@ -44,9 +47,11 @@ def main():
             sim.init_fields()
             lib, h = sim.engine.lib, sim.engine.h
 
+            sides = 2 | 8 if a.one_sided else 15
+
             def run(z0, n0, z1, n1, tiles=0):
                 native.check(lib, lib.gs_fused_runs_raw(h, k, z0, n0, z1, n1, tiles,
-                                                        15 if tiles else 0), "fused_runs")
+                                                        sides if tiles else 0), "fused_runs")
 
             def timed(*runs):
                 for _ in range(3):
@@ -63,7 +68,10 @@ def main():
                 return e0.elapsed_time(e1) / a.reps * 1e3  # us
 
             full = timed((0, nz, 0, 0))
-            if a.packed:
+            if a.packed and a.one_sided:
+                ins = [(0, nz - k, 0, 0, 1)]
+                shs = [(nz - k, k, 0, 0), (0, nz - k, 0, 0, 2)]
+            elif a.packed:
                 ins = [(k, nz - 2 * k, 0, 0, 1)]
                 shs = [(0, k, nz - k, k), (k, nz - 2 * k, 0, 0, 2)]
             else:
@@ -72,7 +80,8 @@ def main():
             inner = timed(*ins)
             shell = timed(*shs)
             both = timed(*(ins + shs))
-            row = {"local": [a.L, a.L, nz], "k": k, "packed": a.packed, "full_us": round(full, 1),
+            row = {"local": [a.L, a.L, nz], "k": k, "packed": a.packed,
+                   "one_sided": a.one_sided, "full_us": round(full, 1),
                    "inner_us": round(inner, 1), "shell_us": round(shell, 1),
                    "inner_plus_shell_us": round(both, 1),
                    "full_mlups": round(a.L * a.L * nz * k / full, 0),
