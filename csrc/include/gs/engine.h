@@ -284,9 +284,13 @@ class Engine {
         // slabs (and, packed plans, the ring tiles) follow once the halos have landed.
         ensure_bc(cur_, t_);  // before the fork: the exchanged planes carry these ghosts
         be_->comm_fork();
+        // the inner launch waits for a mark the comm stream records just before the exchange,
+        // so RCCL's kernel reaches the GPU first (see advance_chained)
+        be_->mark(3, true);
         be_->comm_select(true);
         exchange_start();
         be_->comm_select(false);
+        be_->wait_mark(3, false);
         const Split sp = overlap_split(k);
         if (sp.z1 > sp.z0) {
           TraceRange tr("gs.fused_inner");
@@ -344,6 +348,13 @@ class Engine {
   // outputs are at least k away from every face with a neighbour.  Both buffers' outer ghosts
   // are set before the chain (their time parities stay fixed through it), so no fill runs
   // inside.
+  //   The inner launch waits for mark 2 through a cross-stream hop while the RCCL kernel
+  // follows the shell on its own stream, so RCCL's kernel reaches the GPU first.  That order
+  // matters: RCCL's kernel (64 workgroups of 256 threads at 132 VGPRs on the loopback) does not
+  // fit beside a fused-kernel workgroup, and started after the inner launch it waits for that
+  // launch to end (93 us instead of 19).  Running the shell after inner_p instead (on either
+  // stream) measured 146 us per pass vs 136 us for this schedule (512 x 512 x 64, k = 3, RCCL
+  // loopback; profiles/r2_overlap_schedules.txt).
   void advance_chained(int k, int64_t npass) {
     const Split sp = overlap_split(k);
     ensure_bc(cur_, t_);
@@ -401,12 +412,12 @@ class Engine {
   void shell_runs(int src, int dst, int k, int64_t t, const Split& sp, bool ring_on_comm) {
     const int nz = cfg_.g.nz;
     const bool ring = sp.sides && sp.z1 > sp.z0;
+    const int la = sp.z0, lb = nz - (sp.z1 > sp.z0 ? sp.z1 : sp.z0);
     if (ring) {
       if (ring_on_comm) be_->comm_select(true);
       be_->fused_runs(src, dst, k, t, sp.z0, sp.z1 - sp.z0, 0, 0, false, 2, sp.sides);
       if (ring_on_comm) be_->comm_select(false);
     }
-    const int la = sp.z0, lb = nz - (sp.z1 > sp.z0 ? sp.z1 : sp.z0);
     if (la > 0) be_->fused_runs(src, dst, k, t, 0, la, nz - lb, lb);
     else if (lb > 0) be_->fused_runs(src, dst, k, t, nz - lb, lb, 0, 0);
     if (ring && ring_on_comm) be_->comm_join();

@@ -16,6 +16,7 @@ import dataclasses
 import glob
 import os
 import sys
+import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
@@ -29,7 +30,7 @@ def run(a):
     torch.cuda.set_device(0)
     L = (a.L, a.L, a.nz)
     s = Settings(L=a.L, precision="Float32", F=0.02, k=0.048, dt=1.0, Du=0.2, Dv=0.1, noise=0.1,
-                 backend="AMDGPU", overlap="on")
+                 backend="AMDGPU", overlap=a.overlap)
     dom = init_domain(L, 1, 0, periodic=True)
     if a.mode == "zplanes":  # only the z wraps: whole-plane in-place messages
         nbr = [r if (i // 9 == 1 and (i // 3) % 3 == 1) or i == 13 else -1
@@ -41,10 +42,14 @@ def run(a):
     sim.iterate(a.fuse * 4)
     sim.synchronize()
     torch.cuda.synchronize()
+    t0 = time.perf_counter()
     sim.iterate(a.fuse * a.passes)
     sim.synchronize()
     torch.cuda.synchronize()
-    print(f"mode={a.mode} overlapped={sim.overlapped} transport={sim.transport}", flush=True)
+    us = (time.perf_counter() - t0) / a.passes * 1e6
+    print(f"mode={a.mode} overlap={a.overlap} overlapped={sim.overlapped} "
+          f"transport={sim.transport} chain={os.environ.get('GS_OVERLAP_CHAIN', '1')} "
+          f"fuse={a.fuse} us_per_pass={us:.1f}", flush=True)
     sim.close()
 
 
@@ -74,6 +79,7 @@ def main():
     ap.add_argument("--nz", type=int, default=64)
     ap.add_argument("--fuse", type=int, default=3)
     ap.add_argument("--passes", type=int, default=6)
+    ap.add_argument("--overlap", choices=["on", "off"], default="on")
     ap.add_argument("--summarise", default="")
     a = ap.parse_args()
     if a.summarise:
