@@ -216,7 +216,8 @@ __device__ __forceinline__ gs::U4 philox_dev(uint32_t c0, uint32_t c1, uint64_t 
 //   ABL          : ablations for timing experiments, GS_ABLATION builds only (results are
 //                  WRONG by design): bit0 no workgroup barriers, bit1 every level-0 load reads
 //                  plane 0 (L2-resident); bit2 (exact) Philox round keys 4-10 in VGPRs; bit3
-//                  (exact) the x-neighbour sums' leading s_nop restored
+//                  (exact) the x-neighbour sums' leading s_nop restored; bit4 (exact) the
+//                  pipeline fill computes every level (no FILL skip)
 constexpr int gs_gcd(int a, int b) { return b == 0 ? a : gs_gcd(b, a % b); }
 constexpr int gs_lcm(int a, int b) { return a / gs_gcd(a, b) * b; }
 
@@ -237,6 +238,16 @@ struct FCfg {
   static constexpr int PERIOD = gs_lcm(R, NS);
   static constexpr int NO = TL > 1 ? TL - 1 : 1;
   static constexpr int RT = ROWS * WAVES;                 // tile rows
+  // waves per SIMD the register budget must allow (__launch_bounds__' second argument is
+  // waves per EU on gfx9): fp32 4-row tiles of 8 or 16 waves need 4 (<= 128 VGPRs: two
+  // 8-wave workgroups or one 16-wave workgroup per CU); 12- and 6-wave tiles fill 3 (one or
+  // two workgroups per CU, <= 168 VGPRs); the 8-row and fp64 tiles keep the compiler's choice
+  static constexpr int WPEU =
+      (sizeof(T) == 4 && ROWS == 4) ? ((WAVES == 8 || WAVES == 16) ? 4 : 3) : 1;
+  // pipeline-fill level skip (fused_iter FILL periods): its second copy of the unrolled body
+  // costs ~16 VGPRs, free only where the budget is 168 (WPEU 3); with 128 it spills or halves
+  // the occupancy (4x8:1s: -10 % at L=512, profiles/r2_fill_skip.txt)
+  static constexpr bool FILLSKIP = WPEU == 3 && !(ABL_ & 16);
   static constexpr int YSTEP = (RT - 2 * TL) & ~3;        // output rows per tile
   // rows of output level L = l + 1 that some stored output depends on: [l + 1, hi(l)]
   static constexpr int need_hi(int l) { return 2 * TL + YSTEP - 2 - l; }
@@ -345,7 +356,7 @@ __device__ __forceinline__ typename C::V2 cell_update(typename C::V2& A, typenam
 // Non-skewed: level l+1 is computed from level l of the SAME iteration (one barrier per level).
 // Skewed: level l+1 consumes level l's output of the PREVIOUS iteration, so every level's
 // input rows are published before a single barrier; level l produces plane p - (2l + 1).
-template <class C, typename T, int IR, int IS>
+template <class C, typename T, int IR, int IS, bool FILL>
 __device__ __forceinline__ void fused_iter(FusedState<C>& S,
                                            typename C::V2 (*xch)[C::NS][C::WAVES][2][64],
                                            const FusedArgs& a, const FoldCoef<T>& f,
@@ -390,7 +401,26 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
       if constexpr (!(C::ABL & 1)) __syncthreads();
     }
     const int q = C::SKEW ? p - (2 * l + 1) : p - l - 1;  // plane produced by level l+1
-    if (!((sg.skip >> l) & 1)) {  // wave-uniform
+    // level l+1 is needed on planes [z0 - (T-1) + l, z1 + (T-1) - l) only (the dependency
+    // cone of the segment's outputs), and the plane just below that range builds the running
+    // partial sum A the first needed plane consumes.  The pipeline fill and drain iterations
+    // compute it outside that range too: the first periods of a segment (FILL) skip those
+    // level computations (uniform branches; the last level's stores stay unconditional -- to
+    // the empty descriptor -- so every iteration keeps the same VMEM count for the counted
+    // vmcnt waits).  In p: skewed q >= lo - 1 <=> p - z0 >= 3l + 1 - T and q < hi <=>
+    // pend - p > T - 1 - l; non-skewed p - z0 >= 2l + 1 - T (no drain).  The steady-state
+    // periods carry no checks, so their registers and schedule are unchanged.
+    bool need = true;
+    if constexpr (FILL) {
+      const int d = p - sg.z0, e = sg.pend - p;
+      need = d >= (C::SKEW ? 3 * l + 1 - TL : 2 * l + 1 - TL) && (!C::SKEW || e > TL - 1 - l);
+      if (!need && l + 1 == TL && !((sg.skip >> l) & 1)) {
+        const __amdgpu_buffer_rsrc_t w = plane_rsrc(sg.stp, 0);
+#pragma unroll
+        for (int j = 0; j < ROWS; ++j) bstore(w, (int)0x80000000, in[j]);
+      }
+    }
+    if (need && !((sg.skip >> l) & 1)) {  // wave-uniform
       const V2 up = lds_load2(&xch[l][IS][sg.wup][1][sg.lane]);
       const V2 dn = lds_load2(&xch[l][IS][sg.wdn][0][sg.lane]);
       const int64_t gz = gwrap<C>(g.oz + q, g.Lz);
@@ -452,7 +482,7 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
 }
 
 // Unrolled walk over one ring period; returns false when the segment is done.
-template <class C, typename T, int I>
+template <class C, typename T, int I, bool FILL>
 __device__ __forceinline__ bool fused_period(FusedState<C>& S,
                                              typename C::V2 (*xch)[C::NS][C::WAVES][2][64],
                                              const FusedArgs& a, const FoldCoef<T>& f,
@@ -460,9 +490,9 @@ __device__ __forceinline__ bool fused_period(FusedState<C>& S,
   if constexpr (I == C::PERIOD) {
     return true;
   } else {
-    fused_iter<C, T, I % C::R, I % C::NS>(S, xch, a, f, seed, sg);
+    fused_iter<C, T, I % C::R, I % C::NS, FILL>(S, xch, a, f, seed, sg);
     if (++sg.p >= sg.pend) return false;
-    return fused_period<C, T, I + 1>(S, xch, a, f, seed, sg);
+    return fused_period<C, T, I + 1, FILL>(S, xch, a, f, seed, sg);
   }
 }
 
@@ -498,7 +528,7 @@ __device__ __forceinline__ void map_tile(const FusedArgs& a, int t, int& tx, int
 }
 
 template <class C, typename T>
-__global__ __launch_bounds__(64 * C::WAVES, 1) void k_fused(const typename C::V2* __restrict__ s,
+__global__ __launch_bounds__(64 * C::WAVES, C::WPEU) void k_fused(const typename C::V2* __restrict__ s,
                                                             typename C::V2* __restrict__ d,
                                                             FusedArgs a, FoldCoef<T> f,
                                                             uint64_t seed) {
@@ -638,7 +668,17 @@ __global__ __launch_bounds__(64 * C::WAVES, 1) void k_fused(const typename C::V2
         for (int j = 0; j < ROWS; ++j)
           S.LD[k][j] = bload(r, sg.voff + j * sg.pitchb, (typename C::V2*)nullptr);
       }
-      while (fused_period<C, T, 0>(S, xch, a, f, seed, sg)) {
+      // pipeline fill: the first periods skip level work outside the outputs' dependency
+      // cone (fused_iter, FILL); every level is needed from iteration 3T-1 (skewed) / 2T on
+      bool more = true;
+      if constexpr (C::FILLSKIP) {
+        constexpr int kFillIters = C::SKEW ? 3 * TL - 1 : 2 * TL;
+        constexpr int kFillPeriods = (kFillIters + C::PERIOD - 1) / C::PERIOD;
+#pragma unroll 1
+        for (int np = 0; np < kFillPeriods && more; ++np)
+          more = fused_period<C, T, 0, true>(S, xch, a, f, seed, sg);
+      }
+      while (more && fused_period<C, T, 0, false>(S, xch, a, f, seed, sg)) {
       }
     }
   }  // work list
@@ -784,6 +824,8 @@ inline const FusedCfgEntry* fused_cfg_table(int* n) {
       {"4x12:2s-abl4", true, false},  // 23  Philox keys in VGPRs (exact)
       {"4x12:1s-abl8", true, false},  // 24  DPP sums with the s_nop (exact)
       {"4x12:1s-abl12", true, false}, // 25  abl4 + abl8 (exact)
+      {"4x12:1s-abl16", true, false}, // 26  pipeline fill computes every level (exact)
+      {"4x8:1s-abl16", true, false},  // 27  pipeline fill computes every level (exact)
 #endif
   };
   *n = (int)(sizeof(t) / sizeof(t[0]));
@@ -854,6 +896,8 @@ void run_fused_cfg(const void* s, void* d, const FusedArgs& a, const gs::Params&
       case 23: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;
       case 24: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 8>, T>::run(s, d, a, p, st); return;
       case 25: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 12>, T>::run(s, d, a, p, st); return;
+      case 26: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 27: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
 #endif
       default: break;  // 0 and 14: the default shape below
     }
