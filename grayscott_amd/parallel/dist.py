@@ -8,7 +8,9 @@ environment (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR / MASTER_PORT); the *d
 """
 from __future__ import annotations
 
+import contextlib
 import os
+import sys
 from dataclasses import dataclass
 from datetime import timedelta
 from typing import Any, List, Optional
@@ -105,11 +107,32 @@ def init_from_env(device: str = "cpu") -> DistContext:
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29531")
-        dist.init_process_group(backend="gloo", rank=rank, world_size=world,
-                                timeout=timedelta(seconds=comm_timeout_s()))
+        with _stdout_to_stderr():  # gloo prints its connection report on fd 1
+            dist.init_process_group(backend="gloo", rank=rank, world_size=world,
+                                    timeout=timedelta(seconds=comm_timeout_s()))
         ctx.initialized_here = True
     _CTX = ctx
     return ctx
+
+
+@contextlib.contextmanager
+def _stdout_to_stderr():
+    """Send what native code writes to fd 1 to fd 2 for the duration (stdout carries the
+    benchmark's one JSON line; the gloo rendezvous prints "[Gloo] Rank 0 is connected to ..."
+    there)."""
+    sys.stdout.flush()
+    try:
+        saved = os.dup(1)
+    except OSError:  # no usable fd 1
+        yield
+        return
+    try:
+        os.dup2(2, 1)
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
 
 
 def reset() -> None:

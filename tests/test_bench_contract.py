@@ -43,6 +43,7 @@ def test_bench_torchrun_two_ranks(decomp):
                        env=dict(os.environ, OMP_NUM_THREADS="1"))
     assert r.returncode == 0, r.stderr[-3000:]
     d = _last_json(r.stdout)
+    assert len(r.stdout.strip().splitlines()) == 1, r.stdout[-2000:]
     assert KEYS <= set(d)
     tab = d["data_path_tuning"]
     assert len(tab) == 1 and tab[0]["ok"] and tab[0]["ms_per_step"] > 0
@@ -60,6 +61,8 @@ def test_bench_self_launch_two_ranks():
                        cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     d = _last_json(r.stdout)
+    # stdout is that one line and nothing else (the gloo rendezvous report goes to stderr)
+    assert len(r.stdout.strip().splitlines()) == 1, r.stdout[-2000:]
     assert KEYS <= set(d)
     assert d["world"]["ranks"] == 2 and len(d["world"]["per_rank"]) == 2
     assert d["tuning_s"] >= 0 and d["wall_s"] > 0
