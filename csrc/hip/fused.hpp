@@ -242,12 +242,14 @@ struct FCfg {
   // waves per EU on gfx9): fp32 4-row tiles of 8 or 16 waves need 4 (<= 128 VGPRs: two
   // 8-wave workgroups or one 16-wave workgroup per CU); 12- and 6-wave tiles fill 3 (one or
   // two workgroups per CU, <= 168 VGPRs); the 8-row and fp64 tiles keep the compiler's choice
+  //   fp64 4-row tiles of 6 or 8 waves run one workgroup per CU at any count <= 256 (2)
   static constexpr int WPEU =
-      (sizeof(T) == 4 && ROWS == 4) ? ((WAVES == 8 || WAVES == 16) ? 4 : 3) : 1;
+      (sizeof(T) == 4 && ROWS == 4) ? ((WAVES == 8 || WAVES == 16) ? 4 : 3)
+      : (sizeof(T) == 8 && ROWS == 4 && (WAVES == 6 || WAVES == 8)) ? 2 : 1;
   // pipeline-fill level skip (fused_iter FILL periods): its second copy of the unrolled body
-  // costs ~16 VGPRs, free only where the budget is 168 (WPEU 3); with 128 it spills or halves
-  // the occupancy (4x8:1s: -10 % at L=512, profiles/r2_fill_skip.txt)
-  static constexpr bool FILLSKIP = WPEU == 3 && !(ABL_ & 16);
+  // costs ~16 VGPRs, free only where the budget is 168 or 256 (WPEU 3 / 2); with 128 it spills
+  // or halves the occupancy (4x8:1s: -10 % at L=512, profiles/r2_fill_skip.txt)
+  static constexpr bool FILLSKIP = (WPEU == 3 || WPEU == 2) && !(ABL_ & 16);
   static constexpr int YSTEP = (RT - 2 * TL) & ~3;        // output rows per tile
   // rows of output level L = l + 1 that some stored output depends on: [l + 1, hi(l)]
   static constexpr int need_hi(int l) { return 2 * TL + YSTEP - 2 - l; }
@@ -825,7 +827,8 @@ inline const FusedCfgEntry* fused_cfg_table(int* n) {
       {"4x12:1s-abl8", true, false},  // 24  DPP sums with the s_nop (exact)
       {"4x12:1s-abl12", true, false}, // 25  abl4 + abl8 (exact)
       {"4x12:1s-abl16", true, false}, // 26  pipeline fill computes every level (exact)
-      {"4x8:1s-abl16", true, false},  // 27  pipeline fill computes every level (exact)
+      {"4x8:1s-abl16", true, true},   // 27  pipeline fill computes every level (exact)
+      {"4x6:2s-abl16", true, true},   // 28  pipeline fill computes every level (exact)
 #endif
   };
   *n = (int)(sizeof(t) / sizeof(t[0]));
@@ -868,6 +871,10 @@ void run_fused_cfg(const void* s, void* d, const FusedArgs& a, const gs::Params&
       case 15: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true>, T>::run(s, d, a, p, st); return;
       case 16: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
       case 17: FusedLaunch<FCfg<T, TL, 4, 4, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
+#ifdef GS_ABLATION
+      case 27: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 28: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+#endif
       default: break;
     }
   }
@@ -898,6 +905,7 @@ void run_fused_cfg(const void* s, void* d, const FusedArgs& a, const gs::Params&
       case 25: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 12>, T>::run(s, d, a, p, st); return;
       case 26: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
       case 27: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 28: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
 #endif
       default: break;  // 0 and 14: the default shape below
     }
