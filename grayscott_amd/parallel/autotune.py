@@ -88,6 +88,7 @@ def candidates(L: int, nprocs: int, backend: str) -> List[Tuple]:
         # 64-lane x tiles, and only one tile ring (the y face) outside the overlap
         if nprocs >= 4 and nprocs % 2 == 0 and L // (nprocs // 2) >= 8:
             add([1, 2, nprocs // 2], 0)
+            add([1, 2, nprocs // 2], 0, "off")
         # z slabs with more workgroup slots left free for RCCL's kernel next to the inner
         # update (16 by default): trades inner-kernel throughput for halo bandwidth
         if L // nprocs >= 8:

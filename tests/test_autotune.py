@@ -48,6 +48,6 @@ def test_candidates_for_mi355x():
     assert candidates(512, 8, "hip") == [([2, 2, 2], 0, "auto"), ([1, 1, 8], 0, "auto"),
                                         ([1, 1, 8], 0, "off"), ([1, 1, 8], 2, "auto"),
                                         ([2, 2, 2], 0, "off"), ([2, 2, 2], 2, "auto"),
-                                        ([1, 2, 4], 0, "auto"),
+                                        ([1, 2, 4], 0, "auto"), ([1, 2, 4], 0, "off"),
                                         ([1, 1, 8], 0, "auto", {"GS_OVERLAP_RESERVE": "64"})]
     assert candidates(512, 1, "hip") == [([1, 1, 1], 0, "auto")]
