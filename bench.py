@@ -33,6 +33,7 @@ import sys
 import time
 
 T_START = time.perf_counter()
+_JSON_FD = 1  # the original stdout (main() points fd 1 at stderr for the run)
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -81,6 +82,12 @@ def main(argv=None) -> int:
     if ngpus != world:
         print(f"bench.py: --gpus {ngpus} but the launcher started {world} ranks", file=sys.stderr)
         return 2
+    # stdout carries exactly one line, the JSON record: whatever the libraries print on fd 1
+    # (RCCL's version banner, gloo's rendezvous report) goes to stderr instead
+    global _JSON_FD
+    sys.stdout.flush()
+    _JSON_FD = os.dup(1)
+    os.dup2(2, 1)
     try:
         return run(args)
     except BaseException:
@@ -270,7 +277,7 @@ def run(args) -> int:
         }
         if ref_grid is not None and ctx.world_size == 8 and ref_grid["dims"] == [2, 2, 2]:
             rec["config3_2x2x2"] = ref_grid
-        print(json.dumps(rec), flush=True)
+        os.write(_JSON_FD, (json.dumps(rec) + "\n").encode())
     sim.close()
     ctx.finalize()
     return 0 if check.get("golden_ok", True) else 1
