@@ -10,6 +10,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <chrono>
 #include <stdexcept>
 #include <string>
@@ -36,6 +37,9 @@
   } while (0)
 
 namespace {
+
+constexpr int kIpcHandleBytes = 2 * (int)sizeof(hipIpcMemHandle_t);
+constexpr int kIpcTabStride = 2 + 3 * gs::kMaxMsgs;
 
 using gs::Box;
 using gs::Geom;
@@ -84,6 +88,7 @@ class HipBackend final : public gs::Backend {
     xs_ = stream_;
   }
   ~HipBackend() override {
+    ipc_release();
     if (comm_ && comm_ != shared_comm().comm) ncclCommDestroy(comm_);
     if (ws_) (void)hipFree(ws_);
     if (ev_) (void)hipEventDestroy(ev_);
@@ -191,9 +196,9 @@ class HipBackend final : public gs::Backend {
   void wait_mark(int which, bool on_comm) override {
     HIP_CHECK(hipStreamWaitEvent(on_comm ? comm_stream_ : stream_, marks_[which & 3], 0));
   }
-  bool has_native_transport() const override { return comm_ != nullptr; }
+  bool has_native_transport() const override { return comm_ != nullptr || ipc_; }
   bool can_exchange_inplace(const gs::HaloPlan& p) const override {
-    if (!comm_ || !p.zplanes || inplace_off_) return false;
+    if (!comm_ || ipc_ || !p.zplanes || inplace_off_) return false;
     if (!loopback_)
       for (int i = 0; i < p.nrecv; ++i)
         if (p.recv[i].peer == rank_) return false;
@@ -204,7 +209,7 @@ class HipBackend final : public gs::Backend {
   // sends and receives them in place.  Same message order as the packed path (sends ascend
   // in direction, receives descend), which keeps two messages to one peer matched.
   bool native_exchange_inplace(int b, const gs::HaloPlan& p) override {
-    if (!comm_ || !p.zplanes || inplace_off_) return false;
+    if (!comm_ || ipc_ || !p.zplanes || inplace_off_) return false;
     if (!loopback_)
       for (int i = 0; i < p.nrecv; ++i)
         if (p.recv[i].peer == rank_) return false;
@@ -355,19 +360,208 @@ class HipBackend final : public gs::Backend {
 
   void pack(int b, const gs::HaloPlan& p) override {
     if (p.nsend == 0) return;
+    if (ipc_) {
+      ipc_pack(b, p);
+      return;
+    }
     gsk::launch_pack<T, true>(buf_[b], send_, g_, p.send, p.nsend, xs_);
     HIP_CHECK(hipGetLastError());
   }
   void unpack(int b, const gs::HaloPlan& p) override {
     if (p.nrecv == 0) return;
+    if (ipc_) {
+      ipc_unpack(b, p);
+      return;
+    }
     gsk::launch_pack<T, false>(buf_[b], recv_, g_, p.recv, p.nrecv, xs_);
     HIP_CHECK(hipGetLastError());
   }
+
+  // ---------------------------------------------------------------------------------------
+  // IPC peer-write transport (transport = "ipc").  Each rank exports a landing buffer (two
+  // slots of its plan's receive layout) and a flag array, both uncached device memory, through
+  // hipIpcGetMemHandle; every rank maps its neighbours' (hipIpcOpenMemHandle).  Exchange n:
+  //   pack:   [wait freed_P >= n-2 for each send peer P: its slot n&1 was unpacked]
+  //           -> one pack launch that stores every message straight into the receiving
+  //              peer's landing slot n&1 (over xGMI) -> ready_P[me] = n
+  //   unpack: [wait ready[P] >= n for each receive peer P] -> unpack from my slot n&1
+  //           -> freed_P[me] = n
+  // All of it is stream-ordered device work on the halo stream (no host handshake), so the
+  // scheduler's free-running passes and the comm/compute overlap work unchanged: the flags
+  // are monotonic sequence numbers, which a consumer can wait on ahead of time, unlike
+  // events.  Uncached memory keeps the landing data and the flags coherent between the GPUs
+  // (no stale L2 lines on either side).  Messages to this rank itself (periodic wrap) go
+  // through the local send / receive buffers and self copies, unless loopback is on, in
+  // which case they take the landing-buffer path too (single-GPU test of the protocol).
+  // Flags: flags_[r] = last exchange rank r has landed here; flags_[nranks + r] = last
+  // exchange whose landing slot rank r has consumed (i.e. its slot is free for reuse).
+  void ipc_export(const gs::HaloPlan& p, int nranks, int rank, char* out) {
+    ipc_release();
+    rank_ = rank;
+    ipc_nranks_ = nranks;
+    landing_cells_ = std::max<int64_t>(p.recv_cells, 1);
+    HIP_CHECK(hipExtMallocWithFlags((void**)&landing_, 2 * landing_cells_ * sizeof(V2),
+                                    hipDeviceMallocUncached));
+    HIP_CHECK(hipExtMallocWithFlags((void**)&flags_, 2 * (size_t)nranks * sizeof(uint64_t),
+                                    hipDeviceMallocUncached));
+    HIP_CHECK(hipMemset(flags_, 0, 2 * (size_t)nranks * sizeof(uint64_t)));
+    HIP_CHECK(hipDeviceSynchronize());
+    HIP_CHECK(hipHostMalloc((void**)&ipc_err_, sizeof(int), hipHostMallocMapped));
+    *ipc_err_ = 0;
+    HIP_CHECK(hipHostGetDevicePointer((void**)&ipc_err_dev_, ipc_err_, 0));
+    hipIpcMemHandle_t h[2];
+    HIP_CHECK(hipIpcGetMemHandle(&h[0], landing_));
+    HIP_CHECK(hipIpcGetMemHandle(&h[1], flags_));
+    memcpy(out, h, sizeof(h));
+    int khz = 0;
+    HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev_));
+    const double to = getenv("GS_COMM_TIMEOUT") ? atof(getenv("GS_COMM_TIMEOUT")) : 900.0;
+    ipc_ticks_ = (uint64_t)(std::max(1.0, to) * (double)std::max(khz, 1) * 1000.0);
+    xn_ = 0;
+  }
+
+  // handles: nranks x kIpcHandleBytes (every rank's ipc_export output); tabs: per rank
+  // kIpcTabStride int64 = {nrecv, recv_cells, nrecv x (peer, offset, cells)} of its plan
+  void ipc_connect(const gs::HaloPlan& p, const char* handles, const int64_t* tabs) {
+    if (!landing_) throw std::runtime_error("ipc_connect before ipc_export");
+    auto peer_index = [&](int r) -> int {
+      for (size_t i = 0; i < peers_.size(); ++i)
+        if (peers_[i].rank == r) return (int)i;
+      if (r < 0 || r >= ipc_nranks_) throw std::runtime_error("ipc: peer rank out of range");
+      PeerMap pm{r, nullptr, nullptr, std::max<int64_t>(tabs[(int64_t)r * kIpcTabStride + 1], 1),
+                 false};
+      if (r == rank_) {
+        pm.landing = landing_;
+        pm.flags = flags_;
+      } else {
+        hipIpcMemHandle_t h[2];
+        memcpy(h, handles + (size_t)r * kIpcHandleBytes, sizeof(h));
+        HIP_CHECK(hipIpcOpenMemHandle((void**)&pm.landing, h[0], hipIpcMemLazyEnablePeerAccess));
+        HIP_CHECK(hipIpcOpenMemHandle((void**)&pm.flags, h[1], hipIpcMemLazyEnablePeerAccess));
+        pm.opened = true;
+      }
+      peers_.push_back(pm);
+      return (int)peers_.size() - 1;
+    };
+    send_peers_.clear();
+    recv_peers_.clear();
+    for (int i = 0; i < p.nsend; ++i) {
+      const gs::HaloMsg& m = p.send[i];
+      send_peer_[i] = -1;
+      if (m.peer == rank_ && !loopback_) continue;  // self copy through send_ / recv_
+      const int idx = peer_index(m.peer);
+      send_peer_[i] = idx;
+      if (std::find(send_peers_.begin(), send_peers_.end(), idx) == send_peers_.end())
+        send_peers_.push_back(idx);
+      // the k-th send to P matches the k-th receive at P from this rank (make_halo_plan)
+      int k = 0;
+      for (int j = 0; j < i; ++j) k += p.send[j].peer == m.peer ? 1 : 0;
+      const int64_t* t = tabs + (int64_t)m.peer * kIpcTabStride;
+      int64_t off = -1;
+      for (int j = 0, seen = 0; j < (int)t[0]; ++j) {
+        const int64_t* e = t + 2 + 3 * j;
+        if (e[0] != rank_) continue;
+        if (seen++ == k) {
+          if (e[2] != gs::box_cells(m.box))
+            throw std::runtime_error("ipc: message sizes of a send / receive pair differ");
+          off = e[1];
+          break;
+        }
+      }
+      if (off < 0) throw std::runtime_error("ipc: peer has no matching receive");
+      send_off_[i] = off;
+    }
+    for (int i = 0; i < p.nrecv; ++i) {
+      const gs::HaloMsg& m = p.recv[i];
+      recv_peer_[i] = -1;
+      if (m.peer == rank_ && !loopback_) continue;
+      const int idx = peer_index(m.peer);
+      recv_peer_[i] = idx;
+      if (std::find(recv_peers_.begin(), recv_peers_.end(), idx) == recv_peers_.end())
+        recv_peers_.push_back(idx);
+    }
+    ipc_ = true;
+  }
+
+  void ipc_pack(int b, const gs::HaloPlan& p) {
+    ++xn_;
+    const int64_t slot = (int64_t)(xn_ & 1);
+    if (xn_ > 2 && !send_peers_.empty()) {
+      gsk::IpcFlags w{};
+      for (int idx : send_peers_) {
+        w.f[w.n] = flags_ + ipc_nranks_ + peers_[idx].rank;
+        w.want[w.n++] = xn_ - 2;
+      }
+      gsk::k_ipc_wait<<<1, 64, 0, xs_>>>(w, ipc_ticks_, ipc_err_dev_);
+    }
+    V2* ptrs[gs::kMaxMsgs];
+    for (int i = 0; i < p.nsend; ++i) {
+      const int idx = send_peer_[i];
+      ptrs[i] = idx < 0 ? send_ + p.send[i].offset
+                        : peers_[idx].landing + slot * peers_[idx].slot_cells + send_off_[i];
+    }
+    gsk::launch_pack_ptrs<T, true>(buf_[b], ptrs, g_, p.send, p.nsend, xs_);
+    if (!send_peers_.empty()) {
+      gsk::IpcFlags s{};
+      for (int idx : send_peers_) {
+        s.f[s.n] = peers_[idx].flags + rank_;
+        s.want[s.n++] = xn_;
+      }
+      gsk::k_ipc_signal<<<1, 64, 0, xs_>>>(s);
+    }
+    HIP_CHECK(hipGetLastError());
+  }
+
+  void ipc_unpack(int b, const gs::HaloPlan& p) {
+    const int64_t slot = (int64_t)(xn_ & 1);
+    if (!recv_peers_.empty()) {
+      gsk::IpcFlags w{};
+      for (int idx : recv_peers_) {
+        w.f[w.n] = flags_ + peers_[idx].rank;
+        w.want[w.n++] = xn_;
+      }
+      gsk::k_ipc_wait<<<1, 64, 0, xs_>>>(w, ipc_ticks_, ipc_err_dev_);
+    }
+    V2* ptrs[gs::kMaxMsgs];
+    for (int i = 0; i < p.nrecv; ++i)
+      ptrs[i] = (recv_peer_[i] < 0 ? recv_ : landing_ + slot * landing_cells_) + p.recv[i].offset;
+    gsk::launch_pack_ptrs<T, false>(buf_[b], ptrs, g_, p.recv, p.nrecv, xs_);
+    if (!recv_peers_.empty()) {
+      gsk::IpcFlags s{};
+      for (int idx : recv_peers_) {
+        s.f[s.n] = peers_[idx].flags + ipc_nranks_ + rank_;
+        s.want[s.n++] = xn_;
+      }
+      gsk::k_ipc_signal<<<1, 64, 0, xs_>>>(s);
+    }
+    HIP_CHECK(hipGetLastError());
+  }
+
+  void ipc_release() {
+    if (landing_ || !peers_.empty()) {
+      (void)hipDeviceSynchronize();
+      for (PeerMap& pm : peers_)
+        if (pm.opened) {
+          (void)hipIpcCloseMemHandle(pm.landing);
+          (void)hipIpcCloseMemHandle(pm.flags);
+        }
+    }
+    peers_.clear();
+    if (landing_) (void)hipFree(landing_);
+    if (flags_) (void)hipFree(flags_);
+    if (ipc_err_) (void)hipHostFree(ipc_err_);
+    landing_ = nullptr;
+    flags_ = nullptr;
+    ipc_err_ = ipc_err_dev_ = nullptr;
+    ipc_ = false;
+  }
+  bool ipc_active() const { return ipc_; }
   void self_copy(int64_t so, int64_t d, int64_t n) override {
     HIP_CHECK(hipMemcpyAsync(recv_ + d, send_ + so, sizeof(V2) * n, hipMemcpyDeviceToDevice, xs_));
   }
 
   bool native_exchange(const gs::HaloPlan& p) override {
+    if (ipc_) return true;  // the IPC pack already stored every message at its peer
     if (!comm_) return false;
     NCCL_CHECK(ncclGroupStart());
     for (int i = 0; i < p.nsend; ++i) {
@@ -394,7 +588,7 @@ class HipBackend final : public gs::Backend {
   // transport error or no completion within timeout_s aborts the communicator and throws, so
   // one failed rank ends the job instead of hanging it.
   void wait_all(double timeout_s) override {
-    if (!comm_) {
+    if (!comm_ && !ipc_) {
       HIP_CHECK(hipStreamSynchronize(stream_));
       HIP_CHECK(hipStreamSynchronize(comm_stream_));
       return;
@@ -404,18 +598,22 @@ class HipBackend final : public gs::Backend {
     for (;;) {
       const hipError_t a = hipStreamQuery(stream_);
       const hipError_t b = hipStreamQuery(comm_stream_);
+      // an IPC wait kernel that gave up (peer silent for GS_COMM_TIMEOUT) reports here
+      if (ipc_err_ && __atomic_load_n(ipc_err_, __ATOMIC_ACQUIRE) != 0)
+        throw std::runtime_error("IPC halo exchange: a peer did not signal within "
+                                 "GS_COMM_TIMEOUT seconds (device wait timed out)");
       if (a == hipSuccess && b == hipSuccess) return;
       if (a != hipErrorNotReady) HIP_CHECK(a);
       if (b != hipErrorNotReady) HIP_CHECK(b);
       ncclResult_t async = ncclSuccess;
-      NCCL_CHECK(ncclCommGetAsyncError(comm_, &async));
+      if (comm_) NCCL_CHECK(ncclCommGetAsyncError(comm_, &async));
       if (async != ncclSuccess) {
         abort_comm();
         throw std::runtime_error(std::string("RCCL asynchronous error: ") + ncclGetErrorString(async));
       }
       const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
       if (timeout_s > 0 && el > timeout_s) {
-        abort_comm();
+        if (comm_) abort_comm();
         throw std::runtime_error("halo exchange watchdog: device work not finished after " +
                                  std::to_string(timeout_s) + " s (GS_COMM_TIMEOUT)");
       }
@@ -500,6 +698,27 @@ class HipBackend final : public gs::Backend {
   ncclComm_t comm_ = nullptr;
   int rank_ = 0;
   bool loopback_ = false;
+  // IPC peer-write transport (ipc_export / ipc_connect)
+  struct PeerMap {
+    int rank;
+    V2* landing;     // the peer's landing buffer (2 slots of slot_cells), mapped here
+    uint64_t* flags;  // the peer's flag array, mapped here
+    int64_t slot_cells;
+    bool opened;     // opened through IPC (not this rank's own buffers)
+  };
+  bool ipc_ = false;
+  int ipc_nranks_ = 0;
+  V2* landing_ = nullptr;
+  uint64_t* flags_ = nullptr;
+  int* ipc_err_ = nullptr;
+  int* ipc_err_dev_ = nullptr;
+  int64_t landing_cells_ = 0;
+  uint64_t xn_ = 0;  // exchanges issued
+  uint64_t ipc_ticks_ = 0;
+  std::vector<PeerMap> peers_;
+  std::vector<int> send_peers_, recv_peers_;  // distinct peers (indices into peers_)
+  int send_peer_[gs::kMaxMsgs], recv_peer_[gs::kMaxMsgs];
+  int64_t send_off_[gs::kMaxMsgs];  // offset of send message i in its peer's landing slot
   bool tuned_[4] = {false, false, false, false};
   int cfg_[4] = {-1, -1, -1, -1};
   int sched_[4] = {-1, -1, -1, -1};
@@ -559,6 +778,37 @@ int gs_rccl_abort(void) {
   const ncclResult_t r = ncclCommAbort(sc.comm);
   sc = SharedComm{};
   return r == ncclSuccess ? 0 : -1;
+}
+
+// IPC peer-write transport.  gs_ipc_export allocates and exports this engine's landing buffer
+// and flags (out: kIpcHandleBytes, returned); every rank then passes all ranks' exports and
+// receive tables (per rank kIpcTabStride int64: nrecv, recv_cells, nrecv x (peer, offset,
+// cells)) to gs_ipc_connect.
+int gs_ipc_handle_bytes(void) { return kIpcHandleBytes; }
+int gs_ipc_tab_stride(void) { return kIpcTabStride; }
+int gs_ipc_export(gs_engine* e, int32_t dtype, int32_t nranks, int32_t rank, char* out) {
+  try {
+    gs::Backend* b = e->eng->backend();
+    const gs::HaloPlan& p = e->eng->plan();
+    if (dtype == gs::kF32) static_cast<HipBackend<float>*>(b)->ipc_export(p, nranks, rank, out);
+    else static_cast<HipBackend<double>*>(b)->ipc_export(p, nranks, rank, out);
+    return kIpcHandleBytes;
+  } catch (const std::exception& ex) {
+    g_gs_err = ex.what();
+    return -1;
+  }
+}
+int gs_ipc_connect(gs_engine* e, int32_t dtype, const char* handles, const int64_t* tabs) {
+  try {
+    gs::Backend* b = e->eng->backend();
+    const gs::HaloPlan& p = e->eng->plan();
+    if (dtype == gs::kF32) static_cast<HipBackend<float>*>(b)->ipc_connect(p, handles, tabs);
+    else static_cast<HipBackend<double>*>(b)->ipc_connect(p, handles, tabs);
+    return 0;
+  } catch (const std::exception& ex) {
+    g_gs_err = ex.what();
+    return -1;
+  }
 }
 
 // PCI bus id of the current HIP device ("0000:05:00.0"); returns its length or -1

@@ -112,7 +112,9 @@ void launch_seed(typename Vec2<T>::type* f, const Geom& g, hipStream_t s) {
 // ------------------------------------------------------------------------------------------
 struct PackArgs {
   Box box[gs::kMaxMsgs];
-  int64_t off[gs::kMaxMsgs];
+  // each message's packed cells: a local send / receive buffer, or (IPC transport) the
+  // landing buffer of the peer that receives it, mapped into this process
+  void* ptr[gs::kMaxMsgs];
   // first workgroup of each message (prefix sum of its share), n messages, kPackItems cells
   // per thread: the grid is sized by the messages' cells, not (largest message) x (count)
   int32_t b0[gs::kMaxMsgs + 1];
@@ -128,12 +130,11 @@ constexpr int kPackItems = 4;
 // launched ~20k mostly empty workgroups for a 256^3 rank and took ~10 us per pack / unpack.
 template <typename T, bool PACK>
 __global__ __launch_bounds__(256) void k_pack(typename Vec2<T>::type* __restrict__ f,
-                                              typename Vec2<T>::type* __restrict__ buf, Geom g,
-                                              PackArgs a) {
+                                              Geom g, PackArgs a) {
   int m = 0;
   while (m + 1 < a.n && (int)blockIdx.x >= a.b0[m + 1]) ++m;
   const Box b = a.box[m];
-  typename Vec2<T>::type* p = buf + a.off[m];
+  typename Vec2<T>::type* __restrict__ p = (typename Vec2<T>::type*)a.ptr[m];
   // a message box holds < 2^31 cells (halo slabs of one sub-domain): 32-bit index math
   // (the 64-bit divisions dominated this kernel)
   const uint32_t n = (uint32_t)gs::box_cells(b);
@@ -162,22 +163,65 @@ __global__ __launch_bounds__(256) void k_pack(typename Vec2<T>::type* __restrict
   }
 }
 
+// msgs[i]'s packed cells live at ptrs[i] (any mix of local and peer-mapped buffers)
 template <typename T, bool PACK>
-void launch_pack(typename Vec2<T>::type* f, typename Vec2<T>::type* buf, const Geom& g,
-                 const gs::HaloMsg* msgs, int n, hipStream_t st) {
+void launch_pack_ptrs(typename Vec2<T>::type* f, typename Vec2<T>::type* const* ptrs,
+                      const Geom& g, const gs::HaloMsg* msgs, int n, hipStream_t st) {
   PackArgs a;
   a.n = n;
   int32_t nb = 0;
   for (int i = 0; i < n; ++i) {
     a.box[i] = msgs[i].box;
-    a.off[i] = msgs[i].offset;
+    a.ptr[i] = ptrs[i];
     a.b0[i] = nb;
     const int64_t c = gs::box_cells(msgs[i].box);
     nb += (int32_t)std::max<int64_t>(1, (c + 256 * kPackItems - 1) / (256 * kPackItems));
   }
   a.b0[n] = nb;
   if (nb == 0) return;
-  k_pack<T, PACK><<<dim3(nb, 1, 1), 256, 0, st>>>(f, buf, g, a);
+  k_pack<T, PACK><<<dim3(nb, 1, 1), 256, 0, st>>>(f, g, a);
+}
+
+// msgs[i]'s packed cells at buf + msgs[i].offset (the plan's send / receive buffer layout)
+template <typename T, bool PACK>
+void launch_pack(typename Vec2<T>::type* f, typename Vec2<T>::type* buf, const Geom& g,
+                 const gs::HaloMsg* msgs, int n, hipStream_t st) {
+  typename Vec2<T>::type* ptrs[gs::kMaxMsgs];
+  for (int i = 0; i < n; ++i) ptrs[i] = buf + msgs[i].offset;
+  launch_pack_ptrs<T, PACK>(f, ptrs, g, msgs, n, st);
+}
+
+// ------------------------------------------------------------------------------------------
+// IPC peer-write transport: sequence flags in uncached (fine-grained) memory shared between the
+// ranks of a node.  A wait kernel polls up to kMaxMsgs flags until each reaches its target
+// (system-scope acquire loads, one lane per flag) or until `ticks` of the 100 MHz wall clock
+// have passed -- then it reports through a host-mapped word and exits, so a dead peer never
+// leaves a wave spinning.  A signal kernel publishes one sequence number per flag with
+// system-scope release stores (vector stores; the writes of earlier kernels on the stream are
+// complete at the kernel boundary).
+// ------------------------------------------------------------------------------------------
+struct IpcFlags {
+  uint64_t* f[gs::kMaxMsgs];
+  uint64_t want[gs::kMaxMsgs];
+  int32_t n;
+};
+
+__global__ __launch_bounds__(64) void k_ipc_wait(IpcFlags a, uint64_t ticks, int* err) {
+  const int i = threadIdx.x;
+  if (i >= a.n) return;
+  const uint64_t t0 = wall_clock64();
+  while (__hip_atomic_load(a.f[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < a.want[i]) {
+    if (wall_clock64() - t0 > ticks) {
+      __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+__global__ __launch_bounds__(64) void k_ipc_signal(IpcFlags a) {
+  const int i = threadIdx.x;
+  if (i < a.n) __hip_atomic_store(a.f[i], a.want[i], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -262,10 +262,11 @@ class Engine {
     bc_parity_[b] = par;
   }
 
-  // whether full-depth passes run as a chain on two streams (advance_chained)
+  // whether full-depth passes run as a chain on two streams (advance_chained): any device
+  // transport (RCCL in place or packed, IPC peer writes) -- a host callback serialises anyway
   bool chained(int k) const {
     return chain_ && overlapped(k) && tfn_ == nullptr &&
-           (plan_.zplanes ? be_->can_exchange_inplace(plan_) : be_->has_native_transport());
+           (be_->can_exchange_inplace(plan_) || be_->has_native_transport());
   }
 
   void advance(int64_t nsteps) {

@@ -137,6 +137,20 @@ class GrayScott:
             uid = native.rccl_unique_id() if self.ctx.rank == 0 else None
             uid = self.ctx.broadcast_object(uid, src=0)
             self.engine.rccl_init(uid, self.ctx.world_size, self.ctx.rank)
+        elif kind == "ipc":
+            # direct peer writes into the neighbours' landing buffers over xGMI, ordered by
+            # device-side sequence flags (HipBackend::ipc_export / ipc_connect)
+            if self.backend != "hip":
+                raise ValueError("the ipc transport needs backend = AMDGPU/HIP")
+            h = self.engine.ipc_export(self.ctx.world_size, self.ctx.rank)
+            plan = self.engine.plan()
+            mine = (plan["recv_cells"], [(m["peer"], m["offset"], m["cells"]) for m in plan["recv"]])
+            handles = self.ctx.allgather_object(h)
+            tables = self.ctx.allgather_object(mine)
+            self.engine.ipc_connect(handles, tables)
+            # no rank may store into a peer's landing buffer before that peer has mapped all of
+            # its own neighbours (the flags start at zero on every rank)
+            self.ctx.barrier()
         elif kind in ("torch", "host"):
             stage = kind == "host" and self.backend == "hip"
             group = self.ctx.nccl_group() if (self.backend == "hip" and not stage) else None
@@ -337,5 +351,10 @@ class GrayScott:
             self._io_stream.synchronize()  # no D2H copy may still read the snapshot buffers
             self._snaps = None
         if getattr(self, "engine", None) is not None:
+            if self.transport == "ipc":
+                # peers store into this rank's landing buffer and flags until their last
+                # exchange has finished: every rank drains its streams before any rank frees
+                self.engine.sync()
+                self.ctx.barrier()
             self.engine.close()
             self.engine = None

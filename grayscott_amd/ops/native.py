@@ -114,6 +114,15 @@ def _declare(lib) -> None:
         lib.gs_rccl_abort.restype = c_int
         lib.gs_device_pci.argtypes = [ctypes.c_char_p, c_int32]
         lib.gs_device_pci.restype = c_int
+    if hasattr(lib, "gs_ipc_export"):
+        lib.gs_ipc_handle_bytes.argtypes = []
+        lib.gs_ipc_handle_bytes.restype = c_int
+        lib.gs_ipc_tab_stride.argtypes = []
+        lib.gs_ipc_tab_stride.restype = c_int
+        lib.gs_ipc_export.argtypes = [c_void_p, c_int32, c_int32, c_int32, ctypes.c_char_p]
+        lib.gs_ipc_export.restype = c_int
+        lib.gs_ipc_connect.argtypes = [c_void_p, c_int32, ctypes.c_char_p, POINTER(c_int64)]
+        lib.gs_ipc_connect.restype = c_int
     if hasattr(lib, "gs_fused_choice"):
         lib.gs_fused_choice.argtypes = [c_void_p, c_int32, c_int32, POINTER(c_int32),
                                         POINTER(ctypes.c_float)]
@@ -304,6 +313,30 @@ class Engine:
         self._chk(self.lib.gs_rccl_init(self.h, uid, nranks, rank, DTYPE_CODES[self.dtype]),
                   "rccl_init")
 
+
+    def ipc_export(self, nranks: int, rank: int) -> bytes:
+        """IPC transport, step 1: allocate and export this engine's landing buffer and flags."""
+        if not hasattr(self.lib, "gs_ipc_export"):
+            raise RuntimeError("the IPC transport needs the HIP backend")
+        buf = ctypes.create_string_buffer(int(self.lib.gs_ipc_handle_bytes()))
+        n = self.lib.gs_ipc_export(self.h, DTYPE_CODES[self.dtype], int(nranks), int(rank), buf)
+        if n < 0:
+            raise RuntimeError(f"ipc_export failed: {last_error(self.lib)}")
+        return buf.raw[:n]
+
+    def ipc_connect(self, handles, recv_tables) -> None:
+        """IPC transport, step 2: map the neighbours' exports.  ``handles[r]``: rank r's
+        ``ipc_export`` bytes; ``recv_tables[r]``: (recv_cells, [(peer, offset, cells), ...]) of
+        rank r's halo plan."""
+        stride = int(self.lib.gs_ipc_tab_stride())
+        tab = (c_int64 * (stride * len(handles)))()
+        for r, (rcells, msgs) in enumerate(recv_tables):
+            base = r * stride
+            tab[base], tab[base + 1] = len(msgs), int(rcells)
+            for j, (peer, off, cells) in enumerate(msgs):
+                tab[base + 2 + 3 * j:base + 5 + 3 * j] = [int(peer), int(off), int(cells)]
+        self._chk(self.lib.gs_ipc_connect(self.h, DTYPE_CODES[self.dtype], b"".join(handles), tab),
+                  "ipc_connect")
 
     def rccl_info(self):
         """(communicator size, rank in it, HIP device) of the RCCL transport, or None."""

@@ -61,6 +61,13 @@ class DistContext:
         dist.gather_object(obj, out, dst=dst)
         return out
 
+    def allgather_object(self, obj: Any) -> List[Any]:
+        if not self.is_distributed:
+            return [obj]
+        out = [None] * self.world_size
+        dist.all_gather_object(out, obj)
+        return out
+
     def broadcast_object(self, obj: Any, src: int = 0) -> Any:
         if not self.is_distributed:
             return obj

@@ -12,7 +12,8 @@ Deliberate fixes: ``precision`` is whitelisted instead of ``ev
 
 Extension keys (not in the reference, all optional, documented in README):
   ``periodic`` (bool), ``seed`` (int, noise stream key), ``fuse_steps`` (int, steps fused per
-  halo exchange / temporal blocking depth, 0 = auto), ``transport`` ("auto"|"rccl"|"torch"),
+  halo exchange / temporal blocking depth, 0 = auto), ``transport`` ("auto"|"rccl"|"ipc"|"torch"|"host";
+  "ipc": direct peer writes over xGMI, opt-in),
   ``output_engine`` ("bp4"), ``perf_log`` (path of a JSON-lines perf log), ``diagnostics`` (bool),
   ``decomposition`` ("auto"|"balanced"|"z": process grid, see parallel/decomp.choose_dims;
   "tune": self-check and time the candidate grids / fuse depths, parallel/autotune.py),
