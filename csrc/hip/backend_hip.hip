@@ -381,11 +381,15 @@ class HipBackend final : public gs::Backend {
   // IPC peer-write transport (transport = "ipc").  Each rank exports a landing buffer (two
   // slots of its plan's receive layout) and a flag array, both uncached device memory, through
   // hipIpcGetMemHandle; every rank maps its neighbours' (hipIpcOpenMemHandle).  Exchange n:
-  //   pack:   [wait freed_P >= n-2 for each send peer P: its slot n&1 was unpacked]
-  //           -> one pack launch that stores every message straight into the receiving
-  //              peer's landing slot n&1 (over xGMI) -> ready_P[me] = n
-  //   unpack: [wait ready[P] >= n for each receive peer P] -> unpack from my slot n&1
-  //           -> freed_P[me] = n
+  //   pack:   one launch that stores every message straight into the receiving peer's
+  //           landing slot n&1 (over xGMI)
+  //   unpack: one single-wave launch: ready_P[me] = n for each send peer P, then wait for
+  //           ready[P] >= n for each receive peer P -> unpack from my slot n&1
+  // Slot reuse needs no flag of its own when the neighbour relation is symmetric (always, for
+  // a Cartesian grid): P's ready(n-1) follows P's unpack of exchange n-2 in P's stream order,
+  // and this rank waits for ready(n-1) (its unpack n-1) before its pack n, so P's slot n&1 is
+  // free by then.  Otherwise (asymmetric peer sets) the receiver also publishes
+  // freed_P[me] = n after its unpack and the sender waits for freed >= n-2 before packing.
   // All of it is stream-ordered device work on the halo stream (no host handshake), so the
   // scheduler's free-running passes and the comm/compute overlap work unchanged: the flags
   // are monotonic sequence numbers, which a consumer can wait on ahead of time, unlike
@@ -480,13 +484,17 @@ class HipBackend final : public gs::Backend {
       if (std::find(recv_peers_.begin(), recv_peers_.end(), idx) == recv_peers_.end())
         recv_peers_.push_back(idx);
     }
+    std::vector<int> a = send_peers_, b = recv_peers_;
+    std::sort(a.begin(), a.end());
+    std::sort(b.begin(), b.end());
+    ipc_symmetric_ = a == b && !(getenv("GS_IPC_FREED") && atoi(getenv("GS_IPC_FREED")) != 0);
     ipc_ = true;
   }
 
   void ipc_pack(int b, const gs::HaloPlan& p) {
     ++xn_;
     const int64_t slot = (int64_t)(xn_ & 1);
-    if (xn_ > 2 && !send_peers_.empty()) {
+    if (!ipc_symmetric_ && xn_ > 2 && !send_peers_.empty()) {
       gsk::IpcFlags w{};
       for (int idx : send_peers_) {
         w.f[w.n] = flags_ + ipc_nranks_ + peers_[idx].rank;
@@ -501,32 +509,30 @@ class HipBackend final : public gs::Backend {
                         : peers_[idx].landing + slot * peers_[idx].slot_cells + send_off_[i];
     }
     gsk::launch_pack_ptrs<T, true>(buf_[b], ptrs, g_, p.send, p.nsend, xs_);
-    if (!send_peers_.empty()) {
-      gsk::IpcFlags s{};
+    HIP_CHECK(hipGetLastError());
+  }
+
+  // the engine calls unpack on the stream of the same exchange's pack, with nothing between
+  // them on that stream, so the 'ready' signal is issued here, fused with the wait
+  void ipc_unpack(int b, const gs::HaloPlan& p) {
+    const int64_t slot = (int64_t)(xn_ & 1);
+    if (!send_peers_.empty() || !recv_peers_.empty()) {
+      gsk::IpcFlags s{}, w{};
       for (int idx : send_peers_) {
         s.f[s.n] = peers_[idx].flags + rank_;
         s.want[s.n++] = xn_;
       }
-      gsk::k_ipc_signal<<<1, 64, 0, xs_>>>(s);
-    }
-    HIP_CHECK(hipGetLastError());
-  }
-
-  void ipc_unpack(int b, const gs::HaloPlan& p) {
-    const int64_t slot = (int64_t)(xn_ & 1);
-    if (!recv_peers_.empty()) {
-      gsk::IpcFlags w{};
       for (int idx : recv_peers_) {
         w.f[w.n] = flags_ + peers_[idx].rank;
         w.want[w.n++] = xn_;
       }
-      gsk::k_ipc_wait<<<1, 64, 0, xs_>>>(w, ipc_ticks_, ipc_err_dev_);
+      gsk::k_ipc_signal_wait<<<1, 64, 0, xs_>>>(s, w, ipc_ticks_, ipc_err_dev_);
     }
     V2* ptrs[gs::kMaxMsgs];
     for (int i = 0; i < p.nrecv; ++i)
       ptrs[i] = (recv_peer_[i] < 0 ? recv_ : landing_ + slot * landing_cells_) + p.recv[i].offset;
     gsk::launch_pack_ptrs<T, false>(buf_[b], ptrs, g_, p.recv, p.nrecv, xs_);
-    if (!recv_peers_.empty()) {
+    if (!ipc_symmetric_ && !recv_peers_.empty()) {
       gsk::IpcFlags s{};
       for (int idx : recv_peers_) {
         s.f[s.n] = peers_[idx].flags + ipc_nranks_ + rank_;
@@ -707,6 +713,7 @@ class HipBackend final : public gs::Backend {
     bool opened;     // opened through IPC (not this rank's own buffers)
   };
   bool ipc_ = false;
+  bool ipc_symmetric_ = false;  // send peers == receive peers: no 'freed' flags needed
   int ipc_nranks_ = 0;
   V2* landing_ = nullptr;
   uint64_t* flags_ = nullptr;

@@ -224,6 +224,23 @@ __global__ __launch_bounds__(64) void k_ipc_signal(IpcFlags a) {
   if (i < a.n) __hip_atomic_store(a.f[i], a.want[i], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// signal, then wait, in one launch (the pack -> signal -> wait -> unpack chain of one exchange
+// has one launch fewer); signalling first keeps two ranks waiting on each other deadlock-free
+__global__ __launch_bounds__(64) void k_ipc_signal_wait(IpcFlags s, IpcFlags w, uint64_t ticks,
+                                                        int* err) {
+  const int i = threadIdx.x;
+  if (i < s.n) __hip_atomic_store(s.f[i], s.want[i], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (i >= w.n) return;
+  const uint64_t t0 = wall_clock64();
+  while (__hip_atomic_load(w.f[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < w.want[i]) {
+    if (wall_clock64() - t0 > ticks) {
+      __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // ghost-stripped interior <-> contiguous (z,y,x) arrays (get_fields, Simulation_CPU.jl:125)
 // ------------------------------------------------------------------------------------------

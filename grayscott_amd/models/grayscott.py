@@ -354,7 +354,9 @@ class GrayScott:
             if self.transport == "ipc":
                 # peers store into this rank's landing buffer and flags until their last
                 # exchange has finished: every rank drains its streams before any rank frees
-                self.engine.sync()
-                self.ctx.barrier()
+                try:
+                    self.engine.sync()
+                finally:
+                    self.ctx.barrier()
             self.engine.close()
             self.engine = None

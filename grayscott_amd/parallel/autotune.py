@@ -11,7 +11,10 @@ one-GPU box:
 * the balanced ``MPI_Dims_create`` grid (2x2x2 on 8 GPUs): 4x less halo per link, spread over
   up to six links, but packed (pack / RCCL / unpack) and not overlapped;
 * ``1 x 2 x N/2``: z slabs split once along y -- half the plane bytes per link, one tile ring;
-* the fuse depth T (steps per exchange): the same bytes per step, fewer messages at larger T.
+* the fuse depth T (steps per exchange): the same bytes per step, fewer messages at larger T;
+* the device transport: RCCL point-to-point, or the IPC peer-write transport (the pack kernel
+  stores straight into the neighbours' landing buffers, device-side flags order the exchange;
+  no RCCL kernel, no host handshake) -- its candidates carry ``transport = "ipc"``.
 
 ``tune_data_path`` first checks every candidate's exact data path against the golden model on
 a small grid (``selfcheck``), then times a short run of each on the real problem, with every
@@ -61,8 +64,10 @@ def selfcheck(ctx, backend: str, dims, fuse: int, transport: str, overlap: str, 
 
 
 def candidates(L: int, nprocs: int, backend: str) -> List[Tuple]:
-    """(dims, fuse, overlap[, env]) candidates worth timing for ``nprocs`` ranks on an L^3 grid
-    (fuse 0 = auto; env: engine knobs set for that candidate)."""
+    """(dims, fuse, overlap[, env[, transport]]) candidates worth timing for ``nprocs`` ranks on
+    an L^3 grid (fuse 0 = auto; env: engine knobs set for that candidate; transport: a fixed
+    halo transport instead of the run's own, with no fallback).  GS_TUNE_IPC=0 leaves out the
+    IPC peer-write candidates."""
     out: List[Tuple] = []
 
     def add(d, f, ov="auto"):
@@ -93,6 +98,13 @@ def candidates(L: int, nprocs: int, backend: str) -> List[Tuple]:
         # update (16 by default): trades inner-kernel throughput for halo bandwidth
         if L // nprocs >= 8:
             out.append((list(z), 0, "auto", {"GS_OVERLAP_RESERVE": "64"}))
+        # the IPC peer-write transport on the two main grids, overlapped and not
+        if os.environ.get("GS_TUNE_IPC", "1") != "0":
+            if L // nprocs >= 8:
+                out.append((list(z), 0, "auto", {}, "ipc"))
+                out.append((list(z), 0, "off", {}, "ipc"))
+            out.append((list(bal), 0, "auto", {}, "ipc"))
+            out.append((list(bal), 0, "off", {}, "ipc"))
     return out
 
 
@@ -159,15 +171,18 @@ def tune_data_path(settings, ctx, L: int, backend: str,
         dims, fuse = cand[0], cand[1]
         ov0 = cand[2] if len(cand) > 2 else settings.overlap
         env0 = dict(cand[3]) if len(cand) > 3 else {}
+        tr0 = cand[4] if len(cand) > 4 else None
         dom = init_domain(L, ctx.world_size, ctx.rank, periodic=False, dims=dims)
         f = fuse if fuse > 0 else default_fuse(backend, dom, settings.dtype_name)
         f = max(1, min(f, min(dom.proc_sizes)))
         if any(r["dims"] == list(dims) and r["fuse"] == f and r["overlap_req"] == ov0
-               and r.get("env", {}) == env0 for r in table):
+               and r.get("env", {}) == env0 and r.get("transport_req") == tr0 for r in table):
             continue  # "auto" resolved to a depth already in the list
         row = {"dims": list(dims), "fuse": f, "overlap_req": ov0}
         if env0:
             row["env"] = env0
+        if tr0:
+            row["transport_req"] = tr0
         chosen = None
         attempts = [(settings.transport, ov0, {}),
                     (settings.transport, "off", {"GS_INPLACE_HALO": "0"}),
@@ -176,6 +191,10 @@ def tune_data_path(settings, ctx, L: int, backend: str,
             attempts.append(("host", "off", {"GS_INPLACE_HALO": "0"}))
         if proven is not None:
             attempts = [(proven, ov0, {})]
+        if tr0:
+            # a fixed transport: no fallback chain; a peer that never signals ends its device
+            # waits after 20 s instead of GS_COMM_TIMEOUT
+            attempts = [(tr0, ov0, {"GS_COMM_TIMEOUT": "20"})]
         for tr, ov, extra in attempts:
             env = {**env0, **extra}
             with _env(env):
@@ -185,8 +204,8 @@ def tune_data_path(settings, ctx, L: int, backend: str,
                     ok, used = False, None
             ok = ctx.allreduce(1.0 if ok else 0.0, "min") > 0
             if ok:
-                chosen = (used, ov, env)
-                if not extra:
+                chosen = (used, ov, {**env0, **(extra if not tr0 else {})})
+                if not extra and not tr0:
                     proven = used
                 break
         if chosen is None:

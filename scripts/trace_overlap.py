@@ -36,7 +36,7 @@ def run(a):
         nbr = [r if (i // 9 == 1 and (i // 3) % 3 == 1) or i == 13 else -1
                for i, r in enumerate(dom.nbr27)]
         dom = dataclasses.replace(dom, periodic=False, nbr27=nbr)
-    sim = GrayScott(s, dom, fuse=a.fuse, loopback=True)
+    sim = GrayScott(s, dom, fuse=a.fuse, loopback=True, transport=a.transport)
     sim.init_fields()
     sim.randomize_fields(seed=1)
     sim.iterate(a.fuse * 4)
@@ -60,7 +60,7 @@ def summarise(root):
             rows += list(csv.DictReader(fh))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     last = [r for r in rows if "k_fused" in r["Kernel_Name"] or "ccl" in r["Kernel_Name"].lower()
-            or "k_pack" in r["Kernel_Name"]][-24:]
+            or "k_pack" in r["Kernel_Name"] or "k_ipc" in r["Kernel_Name"]][-24:]
     t0 = int(last[0]["Start_Timestamp"])
     print(f"{'start_us':>9} {'end_us':>9} {'dur_us':>7} queue  kernel")
     for r in last:
@@ -81,6 +81,7 @@ def main():
     ap.add_argument("--passes", type=int, default=6)
     ap.add_argument("--overlap", choices=["on", "off"], default="on")
     ap.add_argument("--summarise", default="")
+    ap.add_argument("--transport", choices=["rccl", "ipc"], default="rccl")
     a = ap.parse_args()
     if a.summarise:
         summarise(a.summarise)

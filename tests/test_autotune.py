@@ -49,5 +49,15 @@ def test_candidates_for_mi355x():
                                         ([1, 1, 8], 0, "off"), ([1, 1, 8], 2, "auto"),
                                         ([2, 2, 2], 0, "off"), ([2, 2, 2], 2, "auto"),
                                         ([1, 2, 4], 0, "auto"), ([1, 2, 4], 0, "off"),
-                                        ([1, 1, 8], 0, "auto", {"GS_OVERLAP_RESERVE": "64"})]
+                                        ([1, 1, 8], 0, "auto", {"GS_OVERLAP_RESERVE": "64"}),
+                                        ([1, 1, 8], 0, "auto", {}, "ipc"),
+                                        ([1, 1, 8], 0, "off", {}, "ipc"),
+                                        ([2, 2, 2], 0, "auto", {}, "ipc"),
+                                        ([2, 2, 2], 0, "off", {}, "ipc")]
     assert candidates(512, 1, "hip") == [([1, 1, 1], 0, "auto")]
+
+
+def test_candidates_without_ipc(monkeypatch):
+    from grayscott_amd.parallel.autotune import candidates
+    monkeypatch.setenv("GS_TUNE_IPC", "0")
+    assert all(len(c) < 5 for c in candidates(512, 8, "hip"))

@@ -75,6 +75,20 @@ def test_ipc_loopback_periodic_packed(L, fuse, prec, overlap):
     np.testing.assert_array_equal(v1, v0)
 
 
+def test_ipc_loopback_freed_flags(monkeypatch):
+    """GS_IPC_FREED=1: the explicit slot-release protocol (receiver publishes 'freed', sender
+    waits for it), used when send and receive peer sets differ, gives the same result."""
+    monkeypatch.setenv("GS_IPC_FREED", "1")
+    L = 40
+    dom = init_domain(L, 1, 0, periodic=True)
+    s = _settings(L, overlap="on")
+    u0, v0, _ = _run(dom, s, 3, 23, loopback=False)
+    u1, v1, i1 = _run(dom, s, 3, 23, transport="ipc", loopback=True)
+    assert i1["transport"] == "ipc"
+    np.testing.assert_array_equal(u1, u0)
+    np.testing.assert_array_equal(v1, v0)
+
+
 @pytest.mark.parametrize("chain", ["1", "0"])
 def test_ipc_loopback_zplanes_chained(chain, monkeypatch):
     """z wraps only: whole-plane messages through the landing buffer, overlapped passes chained
