@@ -23,8 +23,11 @@ def _worker(rank, world, port, out):
     s = Settings(L=24, precision="Float32", F=0.02, k=0.048, dt=1.0, Du=0.2, Dv=0.1, noise=0.1,
                  backend="CPU", transport="auto")
     assert candidates(24, 2, "cpu") == [([2, 1, 1], 0, "auto")]
-    r = tune_data_path(s, ctx, 24, "cpu", cands=[([1, 1, 2], 1), ([2, 1, 1], 0)], steps=4,
-                       warmup=1)
+    # the third candidate pins the IPC transport, which the CPU backend cannot run: it must be
+    # reported as failed without disturbing the others (no fallback chain for pinned transports)
+    r = tune_data_path(s, ctx, 24, "cpu", cands=[([1, 1, 2], 1), ([2, 1, 1], 0),
+                                                  ([1, 1, 2], 1, "auto", {}, "ipc")],
+                       steps=4, warmup=1)
     with open(os.path.join(out, f"r{rank}.json"), "w") as fh:
         json.dump(r, fh)
     ctx.finalize()
@@ -36,8 +39,9 @@ def test_tune_data_path_two_ranks():
                            start_method="spawn")
         r0, r1 = (json.load(open(os.path.join(out, f"r{i}.json"))) for i in range(2))
     assert r0["dims"] == r1["dims"] and r0["dims"] in ([1, 1, 2], [2, 1, 1])
-    assert [row["dims"] for row in r0["table"]] == [[1, 1, 2], [2, 1, 1]]
-    assert all(row["ok"] and row["ms_per_step"] > 0 for row in r0["table"])
+    assert [row["dims"] for row in r0["table"]] == [[1, 1, 2], [2, 1, 1], [1, 1, 2]]
+    assert all(row["ok"] and row["ms_per_step"] > 0 for row in r0["table"][:2])
+    assert r0["table"][2]["transport_req"] == "ipc" and r0["table"][2]["ok"] is False
     assert r0["transport"] == "torch" and r0["fuse"] == 1
 
 

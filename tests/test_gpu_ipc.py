@@ -126,3 +126,17 @@ def test_ipc_multiprocess_matches_single_rank(world, L, fuse, prec, extra):
     assert all(m["transport"] == "ipc" for m in meta)
     np.testing.assert_array_equal(un, u1)
     np.testing.assert_array_equal(vn, v1)
+
+
+def test_ipc_halo_poisoning():
+    """Every non-interior cell (ghosts, padding, halos) NaN-poisoned before the run: the IPC
+    exchange must refill every ghost a stencil reads."""
+    steps = 10
+    u1, v1, _ = run_ranks(1, _cfg(36, steps, 3))
+    cfg = _cfg(36, steps, 3, decomposition="balanced", overlap="on")
+    cfg["poison"] = True
+    un, vn, meta = run_ranks(4, cfg)
+    assert all(m["transport"] == "ipc" for m in meta)
+    assert np.isfinite(un).all() and np.isfinite(vn).all()
+    np.testing.assert_array_equal(un, u1)
+    np.testing.assert_array_equal(vn, v1)
