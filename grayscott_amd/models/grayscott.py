@@ -142,15 +142,27 @@ class GrayScott:
             # device-side sequence flags (HipBackend::ipc_export / ipc_connect)
             if self.backend != "hip":
                 raise ValueError("the ipc transport needs backend = AMDGPU/HIP")
-            h = self.engine.ipc_export(self.ctx.world_size, self.ctx.rank)
+            # every rank runs the same collectives whatever fails locally, then all agree: a
+            # rank that cannot export or map must not leave its peers in a collective it skips
+            err = None
+            try:
+                h = self.engine.ipc_export(self.ctx.world_size, self.ctx.rank)
+            except Exception as ex:  # pragma: no cover - GPU-only failure path
+                err, h = ex, b""
             plan = self.engine.plan()
             mine = (plan["recv_cells"], [(m["peer"], m["offset"], m["cells"]) for m in plan["recv"]])
             handles = self.ctx.allgather_object(h)
             tables = self.ctx.allgather_object(mine)
-            self.engine.ipc_connect(handles, tables)
-            # no rank may store into a peer's landing buffer before that peer has mapped all of
-            # its own neighbours (the flags start at zero on every rank)
-            self.ctx.barrier()
+            if err is None and all(handles):
+                try:
+                    self.engine.ipc_connect(handles, tables)
+                except Exception as ex:  # pragma: no cover - GPU-only failure path
+                    err = ex
+            elif err is None:
+                err = RuntimeError("a peer could not export its IPC buffers")
+            # also: no rank stores into a peer's landing buffer before every rank has mapped
+            if self.ctx.allreduce(0.0 if err else 1.0, "min") <= 0:
+                raise RuntimeError(f"ipc transport set-up failed on some rank: {err}")
         elif kind in ("torch", "host"):
             stage = kind == "host" and self.backend == "hip"
             group = self.ctx.nccl_group() if (self.backend == "hip" and not stage) else None
