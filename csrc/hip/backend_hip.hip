@@ -421,6 +421,8 @@ class HipBackend final : public gs::Backend {
     HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev_));
     const double to = getenv("GS_COMM_TIMEOUT") ? atof(getenv("GS_COMM_TIMEOUT")) : 900.0;
     ipc_ticks_ = (uint64_t)(std::max(1.0, to) * (double)std::max(khz, 1) * 1000.0);
+    const double emu = getenv("GS_IPC_EMULATE_US") ? atof(getenv("GS_IPC_EMULATE_US")) : 0.0;
+    ipc_emulate_ticks_ = (uint64_t)(std::max(0.0, emu) * (double)std::max(khz, 1) / 1000.0);
     xn_ = 0;
   }
 
@@ -526,7 +528,7 @@ class HipBackend final : public gs::Backend {
         w.f[w.n] = flags_ + peers_[idx].rank;
         w.want[w.n++] = xn_;
       }
-      gsk::k_ipc_signal_wait<<<1, 64, 0, xs_>>>(s, w, ipc_ticks_, ipc_err_dev_);
+      gsk::k_ipc_signal_wait<<<1, 64, 0, xs_>>>(s, w, ipc_ticks_, ipc_err_dev_, ipc_emulate_ticks_);
     }
     V2* ptrs[gs::kMaxMsgs];
     for (int i = 0; i < p.nrecv; ++i)
@@ -722,6 +724,7 @@ class HipBackend final : public gs::Backend {
   int64_t landing_cells_ = 0;
   uint64_t xn_ = 0;  // exchanges issued
   uint64_t ipc_ticks_ = 0;
+  uint64_t ipc_emulate_ticks_ = 0;  // GS_IPC_EMULATE_US: minimum exchange wait (modelling)
   std::vector<PeerMap> peers_;
   std::vector<int> send_peers_, recv_peers_;  // distinct peers (indices into peers_)
   int send_peer_[gs::kMaxMsgs], recv_peer_[gs::kMaxMsgs];

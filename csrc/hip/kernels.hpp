@@ -226,12 +226,16 @@ __global__ __launch_bounds__(64) void k_ipc_signal(IpcFlags a) {
 
 // signal, then wait, in one launch (the pack -> signal -> wait -> unpack chain of one exchange
 // has one launch fewer); signalling first keeps two ranks waiting on each other deadlock-free
+//   min_ticks > 0 (GS_IPC_EMULATE_US, modelling only): the launch also lasts at least that long,
+//   so a one-GPU loopback run can stand in for a slower inter-GPU link when timing overlap
 __global__ __launch_bounds__(64) void k_ipc_signal_wait(IpcFlags s, IpcFlags w, uint64_t ticks,
-                                                        int* err) {
+                                                        int* err, uint64_t min_ticks) {
   const int i = threadIdx.x;
-  if (i < s.n) __hip_atomic_store(s.f[i], s.want[i], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  if (i >= w.n) return;
   const uint64_t t0 = wall_clock64();
+  if (i < s.n) __hip_atomic_store(s.f[i], s.want[i], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (min_ticks && i == 0)
+    while (wall_clock64() - t0 < min_ticks) __builtin_amdgcn_s_sleep(1);
+  if (i >= w.n) return;
   while (__hip_atomic_load(w.f[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < w.want[i]) {
     if (wall_clock64() - t0 > ticks) {
       __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
