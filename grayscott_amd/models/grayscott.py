@@ -37,12 +37,13 @@ def default_fuse(backend: str, domain: CartDomain, dtype: str = "float32") -> in
         nx, ny, nz = domain.proc_sizes
         return max(1, min(2, nx, ny, nz))
     # The temporally blocked kernel cuts HBM traffic per step by T; a deeper halo also cuts
-    # the RCCL round trips.  Measured on MI355X (profiles/r1_tune_fuse_depth.txt): with the
-    # current T=3 kernel, T=3 wins from 256^2 x-y planes up (L=256: 431k vs 424k MLUPS,
-    # L=384: 528k vs 516k, L=512: 615k vs ~500k; even at L=192); T=2 on small planes
-    # (L=128), where the 2T-cell tile halo costs more than the saved traffic.
+    # the RCCL round trips.  Measured on MI355X with the round-2 kernel
+    # (profiles/r2_fuse_small.txt; round 1: profiles/r1_tune_fuse_depth.txt): T=3 wins from
+    # 192^2 x-y planes up (L=192: 407-411k vs 370-403k MLUPS, L=256: 495-505k vs 459-468k);
+    # T=2 on smaller planes (L=128: 224-227k vs 191-192k, L=64: 54k vs 42k), where the
+    # 2T-cell tile halo costs more than the saved traffic.
     nx, ny, nz = domain.proc_sizes
-    t = 2 if min(nx, ny) <= 192 else 3
+    t = 2 if min(nx, ny) < 160 else 3
     return max(1, min(t, nx, ny, nz))
 
 
