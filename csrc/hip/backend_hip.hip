@@ -78,9 +78,16 @@ class HipBackend final : public gs::Backend {
     HIP_CHECK(hipGetDevice(&dev_));
     HIP_CHECK(hipMalloc(&ws_, sizeof(double) * 6 * kStatBlocks));
     HIP_CHECK(hipEventCreateWithFlags(&ev_, hipEventDisableTiming));
-    HIP_CHECK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
-    HIP_CHECK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
-    for (hipEvent_t& e : marks_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    // cross-stream ordering events: both streams run on this device, so a device-scope
+    // release is enough (GS_XSTREAM_EVENT: 0 default system scope, 1 device-scope release,
+    // 2 no system fence) -- the system-scope fence writes back and invalidates the L2s
+    const char* xe = getenv("GS_XSTREAM_EVENT");
+    const int xmode = xe ? atoi(xe) : 0;
+    const unsigned xflags = hipEventDisableTiming |
+        (xmode == 1 ? hipEventReleaseToDevice : xmode == 2 ? hipEventDisableSystemFence : 0u);
+    HIP_CHECK(hipEventCreateWithFlags(&ev_fork_, xflags));
+    HIP_CHECK(hipEventCreateWithFlags(&ev_join_, xflags));
+    for (hipEvent_t& e : marks_) HIP_CHECK(hipEventCreateWithFlags(&e, xflags));
     // halo traffic on its own high-priority stream so it overlaps the inner-plane kernel
     int lo = 0, hi = 0;
     HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
