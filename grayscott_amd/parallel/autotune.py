@@ -200,8 +200,13 @@ def tune_data_path(settings, ctx, L: int, backend: str,
             with _env(env):
                 try:
                     ok, err, used = selfcheck(ctx, backend, dims, f, tr, ov)
-                except Exception:  # a path that cannot even be set up is skipped
+                    if not ok:
+                        row.setdefault("check_errors", []).append(
+                            f"{tr}: max |err| {err:.3g} vs golden")
+                except Exception as ex:  # a path that cannot even be set up is skipped
                     ok, used = False, None
+                    # reported in the bench JSON (data_path_tuning): why a transport failed
+                    row.setdefault("check_errors", []).append(f"{tr}: {str(ex)[:160]}")
             ok = ctx.allreduce(1.0 if ok else 0.0, "min") > 0
             if ok:
                 chosen = (used, ov, {**env0, **(extra if not tr0 else {})})

@@ -42,6 +42,7 @@ def test_tune_data_path_two_ranks():
     assert [row["dims"] for row in r0["table"]] == [[1, 1, 2], [2, 1, 1], [1, 1, 2]]
     assert all(row["ok"] and row["ms_per_step"] > 0 for row in r0["table"][:2])
     assert r0["table"][2]["transport_req"] == "ipc" and r0["table"][2]["ok"] is False
+    assert "ipc" in r0["table"][2]["check_errors"][0]
     assert r0["transport"] == "torch" and r0["fuse"] == 1
 
 
