@@ -1,3 +1,4 @@
+# NOTE: the wide-copy path (GS_IPC_COPY_RUNS) was rejected and removed (profiles/r2_ipc_copy_rejected.txt); kept as the record of how it was measured.
 # IPC z-plane plans through the wide contiguous copy (k_copy_runs) vs the cell-wise pack kernel.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
