@@ -431,7 +431,14 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
 #pragma unroll
       for (int m = 0; m < ROWS / 4; ++m) {
         gs::U4 blk{0, 0, 0, 0};
+        // ABL bit 32 (exact): the Philox draw only on lanes inside the level's x dependency cone
+        // [l+1, 63-l) (the other lanes' values never reach a stored output): an exec-masked
+        // draw, so the inactive lanes do not switch -- energy per cell update in the
+        // power-limited regime
         if constexpr (C::NOISE) {
+          bool draw = true;
+          if constexpr ((C::ABL & 32) != 0) draw = sg.lane >= l + 1 && sg.lane < 63 - l;
+          if (draw) {
           if constexpr (C::Q32) {
             // counter q = gx + Lx * (gy4 + Ly4 * gz) < 2^32: uniform part + lane part (a
             // quad never straddles the periodic wrap: Ly % 4 == 0 there)
@@ -445,6 +452,7 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
             const uint64_t qq = (uint64_t)sg.gx + (uint64_t)g.Lx * ((uint64_t)(gyq >> 2) +
                                                                    Ly4 * (uint64_t)gz);
             blk = philox_dev<false, C::KV>((uint32_t)qq, (uint32_t)(qq >> 32), tstep, seed, S.kv);
+          }
           }
         }
 #pragma unroll
@@ -829,6 +837,7 @@ inline const FusedCfgEntry* fused_cfg_table(int* n) {
       {"4x12:1s-abl16", true, false}, // 26  pipeline fill computes every level (exact)
       {"4x8:1s-abl16", true, true},   // 27  pipeline fill computes every level (exact)
       {"4x6:2s-abl16", true, true},   // 28  pipeline fill computes every level (exact)
+      {"4x12:1s-abl32", true, false}, // 29  Philox only on lanes in the x cone (exact)
 #endif
   };
   *n = (int)(sizeof(t) / sizeof(t[0]));
@@ -906,6 +915,7 @@ void run_fused_cfg(const void* s, void* d, const FusedArgs& a, const gs::Params&
       case 26: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
       case 27: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
       case 28: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 29: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 32>, T>::run(s, d, a, p, st); return;
 #endif
       default: break;  // 0 and 14: the default shape below
     }
