@@ -9,6 +9,7 @@ run() { tag=$1; shift; timeout -k 10 200 python bench.py "$@" > $O/$tag.json 2> 
 run L512_f32_driver --steps 20 --warmup 5
 run L64_f32 --L 64 --steps 2000 --warmup 100
 run L128_f32 --L 128 --steps 1000 --warmup 60
+run L192_f32 --L 192 --steps 1000 --warmup 60
 run L256_f32 --L 256 --steps 1000 --warmup 60
 run L512_f32 --L 512 --steps 400 --warmup 40
 run L1024_f32 --L 1024 --steps 60 --warmup 6
