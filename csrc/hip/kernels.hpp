@@ -206,10 +206,10 @@ struct IpcFlags {
   int32_t n;
 };
 
-__global__ __launch_bounds__(64) void k_ipc_wait(IpcFlags a, uint64_t ticks, int* err) {
+// lane i < a.n polls flag i until it reaches its target or `ticks` have passed since t0
+__device__ __forceinline__ void ipc_poll(const IpcFlags& a, uint64_t t0, uint64_t ticks, int* err) {
   const int i = threadIdx.x;
   if (i >= a.n) return;
-  const uint64_t t0 = wall_clock64();
   while (__hip_atomic_load(a.f[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < a.want[i]) {
     if (wall_clock64() - t0 > ticks) {
       __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -217,6 +217,10 @@ __global__ __launch_bounds__(64) void k_ipc_wait(IpcFlags a, uint64_t ticks, int
     }
     __builtin_amdgcn_s_sleep(2);
   }
+}
+
+__global__ __launch_bounds__(64) void k_ipc_wait(IpcFlags a, uint64_t ticks, int* err) {
+  ipc_poll(a, wall_clock64(), ticks, err);
 }
 
 __global__ __launch_bounds__(64) void k_ipc_signal(IpcFlags a) {
@@ -235,14 +239,7 @@ __global__ __launch_bounds__(64) void k_ipc_signal_wait(IpcFlags s, IpcFlags w, 
   if (i < s.n) __hip_atomic_store(s.f[i], s.want[i], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   if (min_ticks && i == 0)
     while (wall_clock64() - t0 < min_ticks) __builtin_amdgcn_s_sleep(1);
-  if (i >= w.n) return;
-  while (__hip_atomic_load(w.f[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < w.want[i]) {
-    if (wall_clock64() - t0 > ticks) {
-      __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      return;
-    }
-    __builtin_amdgcn_s_sleep(2);
-  }
+  ipc_poll(w, t0, ticks, err);
 }
 
 // ------------------------------------------------------------------------------------------
