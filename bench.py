@@ -15,13 +15,17 @@ process per GPU over a 127.0.0.1 rendezvous; this parent never touches the GPU) 
 the job's status.  Rank 0 prints ONE JSON line.
 
 Checks of the timed path:
-  * N = 1: after the timed region, the tuned kernel's first steps from the benchmark's initial
-    state are compared with the native OpenMP golden model (same Philox stream):
-    ``check.max_abs_err`` (a failure makes the run exit non-zero);
-  * N > 1 (before timing): every candidate data path (z slabs / the reference's Dims_create grid, fuse depth,
-    overlap) is checked against the golden model on a small grid and timed on the real problem
-    (parallel/autotune.py); the fastest one is used, and the reference grid's own timing is
-    reported (``reference_grid``; ``config3_2x2x2`` at N = 8, BASELINE config 3).
+  * any N, after the timed region: the state is reset to the benchmark's initial state (the
+    random init is a function of the global cell, so every rank regenerates its block), the
+    timed configuration -- decomposition, transport, overlap, fuse depth, precision, size --
+    runs ``--check-steps`` steps, and each rank compares its block with the native OpenMP
+    golden model run on that block grown by the same number of cells on every side with a
+    neighbour (the cone the steps depend on): ``check.max_abs_err`` over all ranks (a failure
+    makes the run exit non-zero);
+  * N > 1 (before timing): every candidate data path (z slabs / the reference's Dims_create
+    grid, overlap, transport) is checked against the golden model on a small grid and timed on
+    the real problem (parallel/autotune.py); the fastest one is used, and the reference grid's
+    own timing is reported (``reference_grid``; ``config3_2x2x2`` at N = 8, BASELINE config 3).
 The JSON also records what RCCL saw: communicator size and each rank's device and PCI bus id.
 """
 from __future__ import annotations
@@ -100,36 +104,50 @@ def main(argv=None) -> int:
         raise
 
 
-def golden_check(sim, settings, dom, nsteps: int):
-    """Advance the benchmark state ``nsteps`` steps on the tuned path and on the native OpenMP
-    golden model (CPU backend, single-step kernel, same Philox stream), compare, then restore
-    the state and step counter.  Returns the max |difference| over u and v."""
+def golden_check(sim, settings, dom, nsteps: int, init_seed):
+    """Reset the (distributed) state to the benchmark's initial state, advance it ``nsteps``
+    steps on the timed path, and compare this rank's block with the native OpenMP golden model
+    (CPU backend, single-step kernel, same Philox stream) run on the block grown by ``nsteps``
+    cells on every side with a neighbour: outside-in errors of the grown box's artificial
+    boundary travel one cell per step, so the block itself is exact.  ``init_seed``: the random
+    init's seed (None: the reference's seed cube).  Returns this rank's max |difference|."""
     import copy
 
     import numpy as np
 
     from grayscott_amd.models.grayscott import GrayScott
+    from grayscott_amd.parallel.decomp import CartDomain
     from grayscott_amd.parallel.dist import DistContext
 
-    t0 = sim.step
-    u0, v0 = sim.get_fields()
+    sim.engine.init_fields()
+    if init_seed is not None:
+        sim.randomize_fields(seed=init_seed)
     sim.iterate(nsteps)
     ug, vg = sim.get_fields()
+    lo, hi = [], []
+    for a in range(3):
+        o, n, L = dom.proc_offsets[a], dom.proc_sizes[a], dom.L[a]
+        lo.append(max(0, o - nsteps))
+        hi.append(min(L, o + n + nsteps))
+    sub = CartDomain(nprocs=1, rank=0, L=tuple(dom.L), dims=[1, 1, 1], coords=(0, 0, 0),
+                     proc_sizes=[h - l for l, h in zip(lo, hi)], proc_offsets=lo,
+                     periodic=False, nbr27=[-1] * 27)
     cs = copy.copy(settings)
-    cs.backend, cs.fuse_steps = "CPU", 1
-    cpu = GrayScott(cs, dom, DistContext())
+    cs.backend, cs.fuse_steps, cs.transport = "CPU", 1, "none"
+    cpu = GrayScott(cs, sub, DistContext())
     try:
-        cpu.init_fields()
-        cpu.set_fields(u0, v0)
-        cpu.set_step(t0)
+        cpu.engine.init_fields()
+        if init_seed is not None:
+            cpu.randomize_fields(seed=init_seed)
         cpu.iterate(nsteps)
         uc, vc = cpu.get_fields()
     finally:
         cpu.close()
-    err = float(max(np.abs(ug - uc).max(), np.abs(vg - vc).max()))
-    sim.set_fields(u0, v0)
-    sim.set_step(t0)
-    return err
+    (ox, oy, oz), (nx, ny, nz) = dom.proc_offsets, dom.proc_sizes
+    blk = (slice(oz - lo[2], oz - lo[2] + nz), slice(oy - lo[1], oy - lo[1] + ny),
+           slice(ox - lo[0], ox - lo[0] + nx))
+    err = float(max(np.abs(ug - uc[blk]).max(), np.abs(vg - vc[blk]).max()))
+    return err if err == err else float("inf")
 
 
 def run(args) -> int:
@@ -173,14 +191,11 @@ def run(args) -> int:
         sim.randomize_fields(seed=2024)
 
     check = {}
-    do_golden = (args.check == "golden" or
-                 (args.check == "auto" and ctx.world_size == 1 and backend == "hip"))
+    # the golden check of the timed path runs after timing (a seconds-long CPU golden run
+    # before the timed region would leave the GPU idle right before it, and its clocks take
+    # milliseconds to come back); the initial state is regenerated then
+    do_golden = (args.check == "golden" or (args.check == "auto" and backend == "hip"))
     do_golden = do_golden and args.check_steps > 0
-    if do_golden:
-        # the benchmark's initial state, for the golden check of the tuned path after timing
-        # (checked afterwards: a seconds-long CPU golden run before the timed region would leave
-        # the GPU idle right before it, and its clocks take milliseconds to come back)
-        init_state = sim.get_fields_device()  # on the device: no host copy before timing
 
     def sync():
         sim.synchronize()
@@ -205,9 +220,8 @@ def run(args) -> int:
     world_info = ctx.gather_object(sim.device_info())
     if do_golden:
         t_chk = time.perf_counter()
-        sim.set_fields(*init_state)
-        sim.set_step(0)
-        err = golden_check(sim, settings, dom, args.check_steps)
+        err = golden_check(sim, settings, dom, args.check_steps,
+                           2024 if args.init == "random" else None)
         err = ctx.allreduce(err, "max")
         tol = 2e-5 if settings.dtype_name == "float32" else 1e-12
         check.update(golden_steps=args.check_steps, max_abs_err=err, golden_tol=tol,

@@ -146,6 +146,22 @@ class CpuBackend final : public gs::Backend {
       }
   }
 
+  void randomize(int b, uint64_t seed, double lo, double hi) override {
+    T* f = buf_[b];
+    const Geom g = g_;
+#pragma omp parallel for collapse(2) schedule(static)
+    for (int z = 0; z < g.nz; ++z)
+      for (int y = 0; y < g.ny; ++y) {
+        T* row = f + 2 * gs::lin(g, 0, y, z);
+        for (int x = 0; x < g.nx; ++x) {
+          double u, v;
+          gs::random_init_cell(g.ox + x, g.oy + y, g.oz + z, g.Lx, g.Ly, seed, lo, hi, &u, &v);
+          row[2 * x] = (T)u;
+          row[2 * x + 1] = (T)v;
+        }
+      }
+  }
+
   void insert(int b, const void* ui, const void* vi) override {
     T* f = buf_[b];
     const T* u = (const T*)ui;

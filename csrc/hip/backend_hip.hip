@@ -38,7 +38,9 @@
 
 namespace {
 
-constexpr int kIpcHandleBytes = 2 * (int)sizeof(hipIpcMemHandle_t);
+// an IPC export: the landing-buffer and flag handles, then the device's PCI bus id
+constexpr int kIpcPciBytes = 32;
+constexpr int kIpcHandleBytes = 2 * (int)sizeof(hipIpcMemHandle_t) + kIpcPciBytes;
 constexpr int kIpcTabStride = 2 + 3 * gs::kMaxMsgs;
 
 using gs::Box;
@@ -78,16 +80,11 @@ class HipBackend final : public gs::Backend {
     HIP_CHECK(hipGetDevice(&dev_));
     HIP_CHECK(hipMalloc(&ws_, sizeof(double) * 6 * kStatBlocks));
     HIP_CHECK(hipEventCreateWithFlags(&ev_, hipEventDisableTiming));
-    // cross-stream ordering events: both streams run on this device, so a device-scope
-    // release is enough (GS_XSTREAM_EVENT: 0 default system scope, 1 device-scope release,
-    // 2 no system fence) -- the system-scope fence writes back and invalidates the L2s
-    const char* xe = getenv("GS_XSTREAM_EVENT");
-    const int xmode = xe ? atoi(xe) : 0;
-    const unsigned xflags = hipEventDisableTiming |
-        (xmode == 1 ? hipEventReleaseToDevice : xmode == 2 ? hipEventDisableSystemFence : 0u);
-    HIP_CHECK(hipEventCreateWithFlags(&ev_fork_, xflags));
-    HIP_CHECK(hipEventCreateWithFlags(&ev_join_, xflags));
-    for (hipEvent_t& e : marks_) HIP_CHECK(hipEventCreateWithFlags(&e, xflags));
+    // cross-stream ordering events (a device-scope release measured the same,
+    // profiles/r2_xstream_event.txt, so the default flags stay)
+    HIP_CHECK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
+    for (hipEvent_t& e : marks_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     // halo traffic on its own high-priority stream so it overlaps the inner-plane kernel
     int lo = 0, hi = 0;
     HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -181,7 +178,7 @@ class HipBackend final : public gs::Backend {
     }
     const bool ok = gsk::launch_fused<T>(buf_[src], buf_[dst], g_, p_, n, t, xs_,
                                          pin ? -1 : c, pin ? -1 : sc, zlo0, zlen0,
-                                         zlo1, zlen1, leave_room ? reserve_ : 0, tiles, sides);
+                                         zlo1, zlen1, leave_room ? kOverlapReserve : 0, tiles, sides);
     if (!ok) throw std::runtime_error("fused_runs: invalid z-runs");
     HIP_CHECK(hipGetLastError());
     return true;
@@ -256,13 +253,17 @@ class HipBackend final : public gs::Backend {
   // the tile grid of the inner launch it complements)
   // Process-wide cache of tuning results per launch shape: data-path tuning (and the golden
   // checks) build many engines over the same sub-domain shape; each would re-time the same
-  // candidates.  GS_AUTOTUNE_CACHE=0 disables it.
+  // candidates.  The key holds everything a launch's cost depends on: the local and global
+  // extents (edge tiles, the Philox counter width), the launch part and the workgroup slots
+  // left free beside it.
   struct TuneKey {
-    int tsize, nx, ny, nz, H, periodic, noise, n, fixed;
+    int tsize, nx, ny, nz, H, periodic, noise, n, fixed, q32, reserve;
+    int64_t Lx, Ly, Lz;
     Part pt;
     bool operator==(const TuneKey& o) const {
       return tsize == o.tsize && nx == o.nx && ny == o.ny && nz == o.nz && H == o.H &&
              periodic == o.periodic && noise == o.noise && n == o.n && fixed == o.fixed &&
+             q32 == o.q32 && reserve == o.reserve && Lx == o.Lx && Ly == o.Ly && Lz == o.Lz &&
              pt.zlo0 == o.pt.zlo0 && pt.zlen0 == o.pt.zlen0 && pt.zlo1 == o.pt.zlo1 &&
              pt.zlen1 == o.pt.zlen1 && pt.tiles == o.pt.tiles && pt.sides == o.pt.sides;
     }
@@ -278,19 +279,18 @@ class HipBackend final : public gs::Backend {
   bool autotune_part(int src, int dst, int n, int64_t t, const Part& pt, int* cfg, int* sched,
                      float* ms_best, int fixed_cfg = -1) {
     if (!autotune_enabled()) return false;
-    static const bool use_cache = !(getenv("GS_AUTOTUNE_CACHE") && atoi(getenv("GS_AUTOTUNE_CACHE")) == 0);
     const TuneKey key{(int)sizeof(T), g_.nx, g_.ny, g_.nz, g_.H, g_.periodic,
-                      p_.noise != 0.0 ? 1 : 0, n, fixed_cfg, pt};
-    if (use_cache)
-      for (const auto& kv : tune_cache())
-        if (kv.first == key) {
-          *cfg = kv.second.cfg;
-          *sched = kv.second.sched;
-          *ms_best = kv.second.ms;
-          return true;
-        }
+                      p_.noise != 0.0 ? 1 : 0, n, fixed_cfg, gsk::philox_q32(g_) ? 1 : 0,
+                      kOverlapReserve, g_.Lx, g_.Ly, g_.Lz, pt};
+    for (const auto& kv : tune_cache())
+      if (kv.first == key) {
+        *cfg = kv.second.cfg;
+        *sched = kv.second.sched;
+        *ms_best = kv.second.ms;
+        return true;
+      }
     if (!autotune_run(src, dst, n, t, pt, cfg, sched, ms_best, fixed_cfg)) return false;
-    if (use_cache) tune_cache().push_back({key, TuneVal{*cfg, *sched, *ms_best}});
+    tune_cache().push_back({key, TuneVal{*cfg, *sched, *ms_best}});
     return true;
   }
   bool autotune_run(int src, int dst, int n, int64_t t, const Part& pt, int* cfg, int* sched,
@@ -387,16 +387,19 @@ class HipBackend final : public gs::Backend {
   // ---------------------------------------------------------------------------------------
   // IPC peer-write transport (transport = "ipc").  Each rank exports a landing buffer (two
   // slots of its plan's receive layout) and a flag array, both uncached device memory, through
-  // hipIpcGetMemHandle; every rank maps its neighbours' (hipIpcOpenMemHandle).  Exchange n:
+  // hipIpcGetMemHandle, plus its device's PCI bus id; every rank maps its neighbours'
+  // (hipIpcOpenMemHandle) after checking that its device can reach theirs
+  // (hipDeviceCanAccessPeer).  Exchange n:
   //   pack:   one launch that stores every message straight into the receiving peer's
-  //           landing slot n&1 (over xGMI)
-  //   unpack: one single-wave launch: ready_P[me] = n for each send peer P, then wait for
-  //           ready[P] >= n for each receive peer P -> unpack from my slot n&1
-  // Slot reuse needs no flag of its own when the neighbour relation is symmetric (always, for
-  // a Cartesian grid): P's ready(n-1) follows P's unpack of exchange n-2 in P's stream order,
-  // and this rank waits for ready(n-1) (its unpack n-1) before its pack n, so P's slot n&1 is
-  // free by then.  Otherwise (asymmetric peer sets) the receiver also publishes
-  // freed_P[me] = n after its unpack and the sender waits for freed >= n-2 before packing.
+  //           landing slot n&1 (over xGMI), each wave ending with a system-scope release fence
+  //           (its stores are acknowledged before the wave retires)
+  //   unpack: one single-wave launch: ready_P[me] = n for each send peer P (system-scope
+  //           release), then wait for ready[P] >= n for each receive peer P (system-scope
+  //           acquire) -> unpack from my slot n&1
+  // Slot reuse needs no flag of its own because the neighbour relation is symmetric (send
+  // peers = receive peers, always so for a Cartesian grid; checked in ipc_connect): P's
+  // ready(n-1) follows P's unpack of exchange n-2 in P's stream order, and this rank waits for
+  // ready(n-1) (its unpack n-1) before its pack n, so P's slot n&1 is free by then.
   // All of it is stream-ordered device work on the halo stream (no host handshake), so the
   // scheduler's free-running passes and the comm/compute overlap work unchanged: the flags
   // are monotonic sequence numbers, which a consumer can wait on ahead of time, unlike
@@ -404,8 +407,8 @@ class HipBackend final : public gs::Backend {
   // (no stale L2 lines on either side).  Messages to this rank itself (periodic wrap) go
   // through the local send / receive buffers and self copies, unless loopback is on, in
   // which case they take the landing-buffer path too (single-GPU test of the protocol).
-  // Flags: flags_[r] = last exchange rank r has landed here; flags_[nranks + r] = last
-  // exchange whose landing slot rank r has consumed (i.e. its slot is free for reuse).
+  // A wait that times out sets a host-mapped word (the watchdog, wait_all, raises) and a
+  // device word that makes every later unpack write NaN ghosts instead of stale landing data.
   void ipc_export(const gs::HaloPlan& p, int nranks, int rank, char* out) {
     ipc_release();
     rank_ = rank;
@@ -413,9 +416,11 @@ class HipBackend final : public gs::Backend {
     landing_cells_ = std::max<int64_t>(p.recv_cells, 1);
     HIP_CHECK(hipExtMallocWithFlags((void**)&landing_, 2 * landing_cells_ * sizeof(V2),
                                     hipDeviceMallocUncached));
-    HIP_CHECK(hipExtMallocWithFlags((void**)&flags_, 2 * (size_t)nranks * sizeof(uint64_t),
+    HIP_CHECK(hipExtMallocWithFlags((void**)&flags_, (size_t)nranks * sizeof(uint64_t),
                                     hipDeviceMallocUncached));
-    HIP_CHECK(hipMemset(flags_, 0, 2 * (size_t)nranks * sizeof(uint64_t)));
+    HIP_CHECK(hipMemset(flags_, 0, (size_t)nranks * sizeof(uint64_t)));
+    HIP_CHECK(hipMalloc((void**)&ipc_dflag_, sizeof(int)));
+    HIP_CHECK(hipMemset(ipc_dflag_, 0, sizeof(int)));
     HIP_CHECK(hipDeviceSynchronize());
     HIP_CHECK(hipHostMalloc((void**)&ipc_err_, sizeof(int), hipHostMallocMapped));
     *ipc_err_ = 0;
@@ -423,7 +428,9 @@ class HipBackend final : public gs::Backend {
     hipIpcMemHandle_t h[2];
     HIP_CHECK(hipIpcGetMemHandle(&h[0], landing_));
     HIP_CHECK(hipIpcGetMemHandle(&h[1], flags_));
+    memset(out, 0, kIpcHandleBytes);
     memcpy(out, h, sizeof(h));
+    HIP_CHECK(hipDeviceGetPCIBusId(out + sizeof(h), kIpcPciBytes - 1, dev_));
     int khz = 0;
     HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev_));
     const double to = getenv("GS_COMM_TIMEOUT") ? atof(getenv("GS_COMM_TIMEOUT")) : 900.0;
@@ -442,13 +449,32 @@ class HipBackend final : public gs::Backend {
         if (peers_[i].rank == r) return (int)i;
       if (r < 0 || r >= ipc_nranks_) throw std::runtime_error("ipc: peer rank out of range");
       PeerMap pm{r, nullptr, nullptr, std::max<int64_t>(tabs[(int64_t)r * kIpcTabStride + 1], 1),
-                 false};
+                 false, dev_, 1};
       if (r == rank_) {
         pm.landing = landing_;
         pm.flags = flags_;
       } else {
+        const char* hr = handles + (size_t)r * kIpcHandleBytes;
+        char pci[kIpcPciBytes];
+        memcpy(pci, hr + 2 * sizeof(hipIpcMemHandle_t), kIpcPciBytes);
+        pci[kIpcPciBytes - 1] = 0;
+        // the peer's device as this process numbers it (all of the node's GPUs are visible
+        // to every rank); -1: not visible here, then the mapping itself is the check
+        int pdev = -1;
+        if (pci[0] && hipDeviceGetByPCIBusId(&pdev, pci) != hipSuccess) pdev = -1;
+        pm.device = pdev;
+        pm.p2p = pdev == dev_ ? 1 : -1;
+        if (pdev >= 0 && pdev != dev_) {
+          int can = 0;
+          HIP_CHECK(hipDeviceCanAccessPeer(&can, dev_, pdev));
+          if (!can)
+            throw std::runtime_error("ipc: device " + std::to_string(dev_) +
+                                     " cannot access peer device " + std::to_string(pdev) +
+                                     " (rank " + std::to_string(r) + ", " + pci + ")");
+          pm.p2p = 1;
+        }
         hipIpcMemHandle_t h[2];
-        memcpy(h, handles + (size_t)r * kIpcHandleBytes, sizeof(h));
+        memcpy(h, hr, sizeof(h));
         HIP_CHECK(hipIpcOpenMemHandle((void**)&pm.landing, h[0], hipIpcMemLazyEnablePeerAccess));
         HIP_CHECK(hipIpcOpenMemHandle((void**)&pm.flags, h[1], hipIpcMemLazyEnablePeerAccess));
         pm.opened = true;
@@ -496,28 +522,26 @@ class HipBackend final : public gs::Backend {
     std::vector<int> a = send_peers_, b = recv_peers_;
     std::sort(a.begin(), a.end());
     std::sort(b.begin(), b.end());
-    ipc_symmetric_ = a == b && !(getenv("GS_IPC_FREED") && atoi(getenv("GS_IPC_FREED")) != 0);
+    if (a != b)
+      throw std::runtime_error("ipc: the transport needs symmetric neighbours (send peers = "
+                               "receive peers), as every Cartesian decomposition has");
     ipc_ = true;
   }
 
   void ipc_pack(int b, const gs::HaloPlan& p) {
     ++xn_;
     const int64_t slot = (int64_t)(xn_ & 1);
-    if (!ipc_symmetric_ && xn_ > 2 && !send_peers_.empty()) {
-      gsk::IpcFlags w{};
-      for (int idx : send_peers_) {
-        w.f[w.n] = flags_ + ipc_nranks_ + peers_[idx].rank;
-        w.want[w.n++] = xn_ - 2;
-      }
-      gsk::k_ipc_wait<<<1, 64, 0, xs_>>>(w, ipc_ticks_, ipc_err_dev_);
-    }
     V2* ptrs[gs::kMaxMsgs];
+    bool remote = false;
     for (int i = 0; i < p.nsend; ++i) {
       const int idx = send_peer_[i];
       ptrs[i] = idx < 0 ? send_ + p.send[i].offset
                         : peers_[idx].landing + slot * peers_[idx].slot_cells + send_off_[i];
+      remote = remote || idx >= 0;
     }
-    gsk::launch_pack_ptrs<T, true>(buf_[b], ptrs, g_, p.send, p.nsend, xs_);
+    // stores that cross to a peer end with a system-scope release per wave
+    gsk::launch_pack_ptrs<T, true>(buf_[b], ptrs, g_, p.send, p.nsend, xs_,
+                                   remote && ipc_fence_, nullptr);
     HIP_CHECK(hipGetLastError());
   }
 
@@ -535,21 +559,27 @@ class HipBackend final : public gs::Backend {
         w.f[w.n] = flags_ + peers_[idx].rank;
         w.want[w.n++] = xn_;
       }
-      gsk::k_ipc_signal_wait<<<1, 64, 0, xs_>>>(s, w, ipc_ticks_, ipc_err_dev_, ipc_emulate_ticks_);
+      gsk::k_ipc_signal_wait<<<1, 64, 0, xs_>>>(s, w, ipc_ticks_, ipc_err_dev_, ipc_dflag_,
+                                                ipc_emulate_ticks_);
     }
     V2* ptrs[gs::kMaxMsgs];
     for (int i = 0; i < p.nrecv; ++i)
       ptrs[i] = (recv_peer_[i] < 0 ? recv_ : landing_ + slot * landing_cells_) + p.recv[i].offset;
-    gsk::launch_pack_ptrs<T, false>(buf_[b], ptrs, g_, p.recv, p.nrecv, xs_);
-    if (!ipc_symmetric_ && !recv_peers_.empty()) {
-      gsk::IpcFlags s{};
-      for (int idx : recv_peers_) {
-        s.f[s.n] = peers_[idx].flags + ipc_nranks_ + rank_;
-        s.want[s.n++] = xn_;
-      }
-      gsk::k_ipc_signal<<<1, 64, 0, xs_>>>(s);
-    }
+    gsk::launch_pack_ptrs<T, false>(buf_[b], ptrs, g_, p.recv, p.nrecv, xs_, false, ipc_dflag_);
     HIP_CHECK(hipGetLastError());
+  }
+
+  // {rank, device (-1: not visible here), peer access (1 yes, -1 unknown)} per mapped peer
+  int ipc_peers(int32_t* out, int cap) const {
+    int n = 0;
+    for (const PeerMap& pm : peers_)
+      if (pm.rank != rank_ && n < cap) {
+        out[3 * n] = pm.rank;
+        out[3 * n + 1] = pm.device;
+        out[3 * n + 2] = pm.p2p;
+        ++n;
+      }
+    return n;
   }
 
   void ipc_release() {
@@ -564,11 +594,23 @@ class HipBackend final : public gs::Backend {
     peers_.clear();
     if (landing_) (void)hipFree(landing_);
     if (flags_) (void)hipFree(flags_);
+    if (ipc_dflag_) (void)hipFree(ipc_dflag_);
     if (ipc_err_) (void)hipHostFree(ipc_err_);
     landing_ = nullptr;
     flags_ = nullptr;
+    ipc_dflag_ = nullptr;
     ipc_err_ = ipc_err_dev_ = nullptr;
     ipc_ = false;
+  }
+
+  // Forget the device transport after a failed trial (the "auto" fallback chain): abort the
+  // RCCL communicator -- it may be half broken -- and unmap the IPC peers, so the next
+  // transport in the chain is the only one this engine uses.
+  void drop_transport() override {
+    // no device sync first: an RCCL kernel waiting for a peer that failed would never end;
+    // ncclCommAbort is what releases it
+    if (comm_) abort_comm();
+    ipc_release();
   }
   bool ipc_active() const { return ipc_; }
   void self_copy(int64_t so, int64_t d, int64_t n) override {
@@ -641,6 +683,10 @@ class HipBackend final : public gs::Backend {
     gsk::launch_extract<T>(buf_[b], (T*)u, (T*)v, g_, stream_);
     HIP_CHECK(hipGetLastError());
   }
+  void randomize(int b, uint64_t seed, double lo, double hi) override {
+    gsk::launch_randomize<T>(buf_[b], g_, seed, lo, hi, stream_);
+    HIP_CHECK(hipGetLastError());
+  }
   void insert(int b, const void* u, const void* v) override {
     gsk::launch_insert<T>(buf_[b], (const T*)u, (const T*)v, g_, stream_);
     HIP_CHECK(hipGetLastError());
@@ -681,8 +727,7 @@ class HipBackend final : public gs::Backend {
 
   void init_comm(const ncclUniqueId& id, int nranks, int rank) {
     SharedComm& sc = shared_comm();
-    if (sc.comm && sc.nranks == nranks && sc.rank == rank &&
-        !(getenv("GS_RCCL_REUSE") && atoi(getenv("GS_RCCL_REUSE")) == 0)) {
+    if (sc.comm && sc.nranks == nranks && sc.rank == rank) {
       rank_ = rank;
       comm_ = sc.comm;
       return;
@@ -694,6 +739,10 @@ class HipBackend final : public gs::Backend {
 
  private:
   static constexpr int kStatBlocks = 1024;
+  // workgroup slots the inner part of an overlapped pass leaves free, so the communication
+  // kernels (RCCL's, pack / unpack) start beside it (0-16 equal within noise, 64 slower:
+  // profiles/r2_overlap_reserve.txt)
+  static constexpr int kOverlapReserve = 16;
   Geom g_;
   gs::Params p_;
   hipStream_t stream_;
@@ -706,8 +755,6 @@ class HipBackend final : public gs::Backend {
   hipEvent_t marks_[4] = {nullptr, nullptr, nullptr, nullptr};
   hipStream_t comm_stream_ = nullptr;
   hipStream_t xs_ = nullptr;  // stream for halo traffic (compute or comm stream)
-  // workgroup slots left free for RCCL while the inner-plane kernel runs (GS_OVERLAP_RESERVE)
-  int reserve_ = getenv("GS_OVERLAP_RESERVE") ? atoi(getenv("GS_OVERLAP_RESERVE")) : 16;
   bool inplace_off_ = getenv("GS_INPLACE_HALO") && atoi(getenv("GS_INPLACE_HALO")) == 0;
   int dev_ = 0;
   ncclComm_t comm_ = nullptr;
@@ -720,10 +767,18 @@ class HipBackend final : public gs::Backend {
     uint64_t* flags;  // the peer's flag array, mapped here
     int64_t slot_cells;
     bool opened;     // opened through IPC (not this rank's own buffers)
+    int device;      // the peer's device as numbered in this process (-1: not visible)
+    int p2p;         // 1: this device can access the peer's (checked), -1: unknown
   };
   bool ipc_ = false;
-  bool ipc_symmetric_ = false;  // send peers == receive peers: no 'freed' flags needed
+#ifdef GS_ABLATION
+  // timing experiment only: drop the packs' system-scope release (profiles/r3_ipc_fence.txt)
+  bool ipc_fence_ = !(getenv("GS_IPC_NOFENCE") && atoi(getenv("GS_IPC_NOFENCE")) != 0);
+#else
+  static constexpr bool ipc_fence_ = true;
+#endif
   int ipc_nranks_ = 0;
+  int* ipc_dflag_ = nullptr;  // device copy of the timeout word (unpacks write NaN once set)
   V2* landing_ = nullptr;
   uint64_t* flags_ = nullptr;
   int* ipc_err_ = nullptr;
@@ -758,6 +813,26 @@ gs::Backend* gs_make_backend(int32_t dtype, const gs::Geom& g, const gs::Params&
   throw std::runtime_error("unsupported dtype");
 }
 
+// The engine's backend as a HipBackend<T> for the dtype the caller names: a checked cast, so
+// a CPU engine or a dtype mismatch is an error, not undefined behaviour.
+template <typename T>
+HipBackend<T>* hip_backend_of(gs_engine* e) {
+  if (!e || !e->eng) throw std::runtime_error("null engine");
+  HipBackend<T>* b = dynamic_cast<HipBackend<T>*>(e->eng->backend());
+  if (!b)
+    throw std::runtime_error(std::string("engine is not a HIP ") +
+                             (sizeof(T) == 4 ? "fp32" : "fp64") + " engine");
+  return b;
+}
+
+// f(backend) on the engine's HipBackend of `dtype`
+template <class F>
+void with_hip_backend(gs_engine* e, int32_t dtype, F&& f) {
+  if (dtype == gs::kF32) f(hip_backend_of<float>(e));
+  else if (dtype == gs::kF64) f(hip_backend_of<double>(e));
+  else throw std::runtime_error("unsupported dtype");
+}
+
 extern "C" {
 
 int gs_rccl_unique_id(char* out, int32_t cap) {
@@ -776,9 +851,7 @@ int gs_rccl_unique_id(char* out, int32_t cap) {
 // {communicator size, rank in it, HIP device} of the engine's RCCL communicator (-1: none)
 int gs_rccl_info(gs_engine* e, int32_t dtype, int32_t* out3) {
   try {
-    gs::Backend* b = e->eng->backend();
-    if (dtype == gs::kF32) static_cast<HipBackend<float>*>(b)->comm_info(out3);
-    else static_cast<HipBackend<double>*>(b)->comm_info(out3);
+    with_hip_backend(e, dtype, [&](auto* b) { b->comm_info(out3); });
     return 0;
   } catch (const std::exception& ex) {
     g_gs_err = ex.what();
@@ -805,10 +878,7 @@ int gs_ipc_handle_bytes(void) { return kIpcHandleBytes; }
 int gs_ipc_tab_stride(void) { return kIpcTabStride; }
 int gs_ipc_export(gs_engine* e, int32_t dtype, int32_t nranks, int32_t rank, char* out) {
   try {
-    gs::Backend* b = e->eng->backend();
-    const gs::HaloPlan& p = e->eng->plan();
-    if (dtype == gs::kF32) static_cast<HipBackend<float>*>(b)->ipc_export(p, nranks, rank, out);
-    else static_cast<HipBackend<double>*>(b)->ipc_export(p, nranks, rank, out);
+    with_hip_backend(e, dtype, [&](auto* b) { b->ipc_export(e->eng->plan(), nranks, rank, out); });
     return kIpcHandleBytes;
   } catch (const std::exception& ex) {
     g_gs_err = ex.what();
@@ -817,11 +887,22 @@ int gs_ipc_export(gs_engine* e, int32_t dtype, int32_t nranks, int32_t rank, cha
 }
 int gs_ipc_connect(gs_engine* e, int32_t dtype, const char* handles, const int64_t* tabs) {
   try {
-    gs::Backend* b = e->eng->backend();
-    const gs::HaloPlan& p = e->eng->plan();
-    if (dtype == gs::kF32) static_cast<HipBackend<float>*>(b)->ipc_connect(p, handles, tabs);
-    else static_cast<HipBackend<double>*>(b)->ipc_connect(p, handles, tabs);
+    with_hip_backend(e, dtype, [&](auto* b) { b->ipc_connect(e->eng->plan(), handles, tabs); });
     return 0;
+  } catch (const std::exception& ex) {
+    g_gs_err = ex.what();
+    return -1;
+  }
+}
+
+// The IPC peers this engine mapped: out = cap x {rank, device (-1: not visible in this
+// process), peer access (1: hipDeviceCanAccessPeer said yes, -1: not checkable)}; returns the
+// count, or -1 on error.
+int gs_ipc_peers(gs_engine* e, int32_t dtype, int32_t* out, int32_t cap) {
+  try {
+    int n = 0;
+    with_hip_backend(e, dtype, [&](auto* b) { n = b->ipc_peers(out, cap); });
+    return n;
   } catch (const std::exception& ex) {
     g_gs_err = ex.what();
     return -1;
@@ -840,9 +921,7 @@ int gs_rccl_init(gs_engine* e, const char* uid, int32_t nranks, int32_t rank, in
   try {
     ncclUniqueId id;
     memcpy(&id, uid, sizeof(id));
-    gs::Backend* b = e->eng->backend();
-    if (dtype == gs::kF32) static_cast<HipBackend<float>*>(b)->init_comm(id, nranks, rank);
-    else static_cast<HipBackend<double>*>(b)->init_comm(id, nranks, rank);
+    with_hip_backend(e, dtype, [&](auto* b) { b->init_comm(id, nranks, rank); });
     return 0;
   } catch (const std::exception& ex) {
     g_gs_err = ex.what();
@@ -883,15 +962,18 @@ extern "C" {
 // Fused-kernel choice made by the autotuner for depth n: out = {cfg, sched}, ms = timing.
 int gs_fused_choice(gs_engine* e, int32_t n, int32_t dtype, int32_t* out2, float* ms) {
   if (n < 0 || n > 3) return -1;
-  gs::Backend* b = e->eng->backend();
-  int c = -1, s = -1;
-  float t = 0.f;
-  if (dtype == gs::kF32) static_cast<HipBackend<float>*>(b)->fused_choice(n, &c, &s, &t);
-  else static_cast<HipBackend<double>*>(b)->fused_choice(n, &c, &s, &t);
-  out2[0] = c;
-  out2[1] = s;
-  *ms = t;
-  return 0;
+  try {
+    int c = -1, s = -1;
+    float t = 0.f;
+    with_hip_backend(e, dtype, [&](auto* b) { b->fused_choice(n, &c, &s, &t); });
+    out2[0] = c;
+    out2[1] = s;
+    *ms = t;
+    return 0;
+  } catch (const std::exception& ex) {
+    g_gs_err = ex.what();
+    return -1;
+  }
 }
 
 }  // extern "C"

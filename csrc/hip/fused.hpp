@@ -767,9 +767,8 @@ struct FusedLaunch {
       int64_t bcost = INT64_MAX;
       // chunks of >= 2 planes: small sub-domains (one round) trade pipeline fill for
       // parallelism -- L=64 at T=2: 10.4 -> 6.8 us/step; large ones are set by the rounds
-      // (profiles/r1_tune_chunking.txt).  GS_FUSED_CHDIV overrides the divisor.
-      static const int chdiv = getenv("GS_FUSED_CHDIV") ? atoi(getenv("GS_FUSED_CHDIV")) : 2;
-      const int maxch = std::max(1, a.nzv / std::max(1, chdiv));
+      // (profiles/r1_tune_chunking.txt)
+      const int maxch = std::max(1, a.nzv / 2);
       for (int nch = 1; nch <= maxch; ++nch) {
         const int64_t per = ((int64_t)a.ntiles * nch + 7) / 8;
         const int64_t rounds = (per + M - 1) / M;

@@ -119,6 +119,12 @@ struct PackArgs {
   // per thread: the grid is sized by the messages' cells, not (largest message) x (count)
   int32_t b0[gs::kMaxMsgs + 1];
   int32_t n;
+  // PACK into peer memory (IPC): every wave ends with a system-scope release, so its stores
+  // to the peer's landing buffer are acknowledged before the ready flag can be published
+  int32_t fence;
+  // unpack from a landing buffer (IPC): a nonzero device word (a timed-out wait) makes the
+  // unpack write NaN ghosts instead of the stale landing data
+  const int* err;
 };
 
 constexpr int kPackItems = 4;
@@ -140,6 +146,9 @@ __global__ __launch_bounds__(256) void k_pack(typename Vec2<T>::type* __restrict
   const uint32_t n = (uint32_t)gs::box_cells(b);
   const uint32_t bnx = (uint32_t)b.nx, bny = (uint32_t)b.ny;
   const uint32_t base = (uint32_t)(blockIdx.x - a.b0[m]) * (256u * kPackItems) + threadIdx.x;
+  // a timed-out IPC wait: poison the ghosts (wave-uniform load of a device word)
+  const bool poison = !PACK && a.err && __hip_atomic_load(a.err, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT) != 0;
   // all loads first (kPackItems in flight per lane), then the stores
   typename Vec2<T>::type c[kPackItems];
   int64_t jj[kPackItems];
@@ -152,6 +161,7 @@ __global__ __launch_bounds__(256) void k_pack(typename Vec2<T>::type* __restrict
     const int y = (int)(r - z * bny);
     jj[k] = gs::lin(g, b.x0 + x, b.y0 + y, b.z0 + (int)z);
     if (i < n) c[k] = PACK ? f[jj[k]] : p[i];
+    if (!PACK && poison) c[k].x = c[k].y = __builtin_nan("");
   }
 #pragma unroll
   for (int k = 0; k < kPackItems; ++k) {
@@ -161,14 +171,18 @@ __global__ __launch_bounds__(256) void k_pack(typename Vec2<T>::type* __restrict
       else f[jj[k]] = c[k];
     }
   }
+  if (PACK && a.fence) __threadfence_system();
 }
 
 // msgs[i]'s packed cells live at ptrs[i] (any mix of local and peer-mapped buffers)
 template <typename T, bool PACK>
 void launch_pack_ptrs(typename Vec2<T>::type* f, typename Vec2<T>::type* const* ptrs,
-                      const Geom& g, const gs::HaloMsg* msgs, int n, hipStream_t st) {
+                      const Geom& g, const gs::HaloMsg* msgs, int n, hipStream_t st,
+                      bool fence = false, const int* err = nullptr) {
   PackArgs a;
   a.n = n;
+  a.fence = fence ? 1 : 0;
+  a.err = err;
   int32_t nb = 0;
   for (int i = 0; i < n; ++i) {
     a.box[i] = msgs[i].box;
@@ -193,12 +207,13 @@ void launch_pack(typename Vec2<T>::type* f, typename Vec2<T>::type* buf, const G
 
 // ------------------------------------------------------------------------------------------
 // IPC peer-write transport: sequence flags in uncached (fine-grained) memory shared between the
-// ranks of a node.  A wait kernel polls up to kMaxMsgs flags until each reaches its target
-// (system-scope acquire loads, one lane per flag) or until `ticks` of the 100 MHz wall clock
-// have passed -- then it reports through a host-mapped word and exits, so a dead peer never
-// leaves a wave spinning.  A signal kernel publishes one sequence number per flag with
-// system-scope release stores (vector stores; the writes of earlier kernels on the stream are
-// complete at the kernel boundary).
+// ranks of a node.  The signal-wait kernel publishes one sequence number per peer flag with
+// system-scope release stores (vector stores; the pack kernel before it on the stream ended
+// every wave with a system-scope release of its peer stores, k_pack `fence`), then polls up to
+// kMaxMsgs flags until each reaches its target (system-scope acquire loads, one lane per flag)
+// or until `ticks` of the 100 MHz wall clock have passed -- then it reports through a
+// host-mapped word (the watchdog) and a device word (the following unpack writes NaN) and
+// exits, so a dead peer never leaves a wave spinning.
 // ------------------------------------------------------------------------------------------
 struct IpcFlags {
   uint64_t* f[gs::kMaxMsgs];
@@ -207,11 +222,13 @@ struct IpcFlags {
 };
 
 // lane i < a.n polls flag i until it reaches its target or `ticks` have passed since t0
-__device__ __forceinline__ void ipc_poll(const IpcFlags& a, uint64_t t0, uint64_t ticks, int* err) {
+__device__ __forceinline__ void ipc_poll(const IpcFlags& a, uint64_t t0, uint64_t ticks, int* err,
+                                         int* dflag) {
   const int i = threadIdx.x;
   if (i >= a.n) return;
   while (__hip_atomic_load(a.f[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < a.want[i]) {
     if (wall_clock64() - t0 > ticks) {
+      __hip_atomic_store(dflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       return;
     }
@@ -219,27 +236,18 @@ __device__ __forceinline__ void ipc_poll(const IpcFlags& a, uint64_t t0, uint64_
   }
 }
 
-__global__ __launch_bounds__(64) void k_ipc_wait(IpcFlags a, uint64_t ticks, int* err) {
-  ipc_poll(a, wall_clock64(), ticks, err);
-}
-
-__global__ __launch_bounds__(64) void k_ipc_signal(IpcFlags a) {
-  const int i = threadIdx.x;
-  if (i < a.n) __hip_atomic_store(a.f[i], a.want[i], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 // signal, then wait, in one launch (the pack -> signal -> wait -> unpack chain of one exchange
 // has one launch fewer); signalling first keeps two ranks waiting on each other deadlock-free
 //   min_ticks > 0 (GS_IPC_EMULATE_US, modelling only): the launch also lasts at least that long,
 //   so a one-GPU loopback run can stand in for a slower inter-GPU link when timing overlap
 __global__ __launch_bounds__(64) void k_ipc_signal_wait(IpcFlags s, IpcFlags w, uint64_t ticks,
-                                                        int* err, uint64_t min_ticks) {
+                                                        int* err, int* dflag, uint64_t min_ticks) {
   const int i = threadIdx.x;
   const uint64_t t0 = wall_clock64();
   if (i < s.n) __hip_atomic_store(s.f[i], s.want[i], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   if (min_ticks && i == 0)
     while (wall_clock64() - t0 < min_ticks) __builtin_amdgcn_s_sleep(1);
-  ipc_poll(w, t0, ticks, err);
+  ipc_poll(w, t0, ticks, err, dflag);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -264,6 +272,29 @@ __global__ __launch_bounds__(256) void k_interior(typename Vec2<T>::type* __rest
     c.y = v[o];
     f[j] = c;
   }
+}
+
+// decomposition-invariant random interior (gs::random_init_cell), one thread per cell
+template <typename T>
+__global__ __launch_bounds__(256) void k_randomize(typename Vec2<T>::type* __restrict__ f, Geom g,
+                                                   uint64_t seed, double lo, double hi) {
+  const int x = blockIdx.x * 256 + threadIdx.x;
+  const int y = blockIdx.y;
+  const int z = blockIdx.z;
+  if (x >= g.nx) return;
+  double u, v;
+  gs::random_init_cell(g.ox + x, g.oy + y, g.oz + z, g.Lx, g.Ly, seed, lo, hi, &u, &v);
+  typename Vec2<T>::type c;
+  c.x = (T)u;
+  c.y = (T)v;
+  f[gs::lin(g, x, y, z)] = c;
+}
+
+template <typename T>
+void launch_randomize(typename Vec2<T>::type* f, const Geom& g, uint64_t seed, double lo,
+                      double hi, hipStream_t st) {
+  dim3 grid((g.nx + 255) / 256, g.ny, g.nz);
+  k_randomize<T><<<grid, 256, 0, st>>>(f, g, seed, lo, hi);
 }
 
 template <typename T>

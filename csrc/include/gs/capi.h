@@ -36,7 +36,10 @@ int gs_sync(gs_engine* e);
 int gs_extract(gs_engine* e, void* u, void* v);
 int gs_insert(gs_engine* e, const void* u, const void* v);
 int gs_stats(gs_engine* e, double* out6);
+// random interior u, v ~ U[lo, hi) keyed on the global cell (any decomposition: same state)
+int gs_randomize(gs_engine* e, uint64_t seed, double lo, double hi);
 int gs_set_transport(gs_engine* e, int (*fn)(void*), void* user);
+int gs_drop_transport(gs_engine* e);  // forget RCCL / IPC / callback transport (fallback)
 // halo plan introspection: counts and per-message (dir, peer, offset, cells)
 int gs_plan_info(gs_engine* e, int64_t* send_cells, int64_t* recv_cells, int32_t* nsend, int32_t* nrecv);
 int gs_plan_msg(gs_engine* e, int32_t which, int32_t i, int64_t* out4);

@@ -97,10 +97,14 @@ int gs_extract(gs_engine* e, void* u, void* v) {
 int gs_insert(gs_engine* e, const void* u, const void* v) {
   GS_TRY(e->eng->backend()->insert(e->eng->cur(), u, v))
 }
+int gs_randomize(gs_engine* e, uint64_t seed, double lo, double hi) {
+  GS_TRY(e->eng->randomize(seed, lo, hi))
+}
 int gs_stats(gs_engine* e, double* out6) { GS_TRY(e->eng->backend()->stats(e->eng->cur(), out6)) }
 int gs_set_transport(gs_engine* e, int (*fn)(void*), void* user) {
   GS_TRY(e->eng->set_transport(fn, user))
 }
+int gs_drop_transport(gs_engine* e) { GS_TRY(e->eng->drop_transport()) }
 
 int gs_plan_info(gs_engine* e, int64_t* sc, int64_t* rc, int32_t* ns, int32_t* nr) {
   const gs::HaloPlan& p = e->eng->plan();

@@ -14,6 +14,7 @@
 
 #include <stdint.h>
 #include <stddef.h>
+#include <math.h>
 
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
@@ -119,6 +120,20 @@ GS_HD U4 noise_block(int64_t gx, int64_t gy4, int64_t gz, int64_t Lx, int64_t Ly
   const uint64_t q = (uint64_t)gx + (uint64_t)Lx * ((uint64_t)gy4 + Ly4 * (uint64_t)gz);
   return philox4x32_10((uint32_t)q, (uint32_t)(q >> 32), (uint32_t)step,
                        (uint32_t)(step >> 32), seed);
+}
+
+// Random initial state (benchmarks: "random-init u/v", BASELINE.json), keyed on the global
+// cell id only, so every decomposition starts from the same global state:
+//   (w0, w1) = Philox4x32-10(counter = {q, q >> 32, ~0, ~0}, key = seed),
+//   q = gx + Lx * (gy + Ly * gz);  u = lo + (hi - lo) * (w0 >> 8) 2^-24, v likewise with w1.
+// Step ~0 (2^64 - 1) is never a noise step.  The 24-bit fractions are exact in fp32 and fp64.
+GS_HD void random_init_cell(int64_t gx, int64_t gy, int64_t gz, int64_t Lx, int64_t Ly,
+                            uint64_t seed, double lo, double hi, double* u, double* v) {
+  const uint64_t q = (uint64_t)gx + (uint64_t)Lx * ((uint64_t)gy + (uint64_t)Ly * (uint64_t)gz);
+  const U4 r = philox4x32_10((uint32_t)q, (uint32_t)(q >> 32), 0xFFFFFFFFu, 0xFFFFFFFFu, seed);
+  const double s = 5.9604644775390625e-08;  // 2^-24
+  *u = fma(hi - lo, (double)(r.x >> 8) * s, lo);
+  *v = fma(hi - lo, (double)(r.y >> 8) * s, lo);
 }
 
 GS_HD uint32_t u4_get(const U4& r, int i) {

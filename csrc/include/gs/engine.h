@@ -84,12 +84,16 @@ class Backend {
   virtual bool native_exchange(const HaloPlan& p) { (void)p; return false; }
   // loopback: messages to this rank also go through the native transport (tests)
   virtual void set_loopback(bool on) { (void)on; }
+  // forget the device transport (RCCL communicator, IPC mappings) after a failed trial
+  virtual void drop_transport() {}
   virtual void host_sync() {}
   // wait for all queued device work; a backend with a device transport turns a hang or an
   // asynchronous transport error into an exception after `timeout_s` seconds (watchdog)
   virtual void wait_all(double timeout_s) { (void)timeout_s; host_sync(); }
   virtual void extract(int b, void* u, void* v) = 0;
   virtual void insert(int b, const void* u, const void* v) = 0;
+  // random interior of buffer b, a function of the global cell only (gs::random_init_cell)
+  virtual void randomize(int b, uint64_t seed, double lo, double hi) = 0;
   // seed cube into buffer b
   virtual void seed(int b) = 0;
   // sum / min / max of u and v over the interior: out[6]
@@ -127,6 +131,12 @@ class Engine {
   int64_t step() const { return t_; }
   void set_step(int64_t t) { t_ = t; bc_parity_[0] = bc_parity_[1] = -1; }
   void set_transport(TransportFn fn, void* user) { tfn_ = fn; tuser_ = user; }
+  // back to "no transport" (the fallback chain tries the next one from a clean state)
+  void drop_transport() {
+    tfn_ = nullptr;
+    tuser_ = nullptr;
+    be_->drop_transport();
+  }
   // comm/compute overlap: -1 auto (on with a device transport and a comm stream),
   // 0 off, 1 on where possible
   void set_overlap(int mode) { overlap_ = mode; }
@@ -163,6 +173,9 @@ class Engine {
     bc_parity_[0] = 0;  // u ghosts = 1 -> even time
     bc_parity_[1] = 1;  // u_temp ghosts = 0 -> odd time
   }
+
+  // Random-init the current state's interior (u, v ~ U[lo, hi), decomposition-invariant).
+  void randomize(uint64_t seed, double lo, double hi) { be_->randomize(cur_, seed, lo, hi); }
 
   // Tune every fused depth this engine can use, without changing the state.
   void prepare() {

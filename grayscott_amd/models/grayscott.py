@@ -125,6 +125,12 @@ class GrayScott:
                 except Exception as ex:  # pragma: no cover - exercised on multi-GPU nodes
                     errors.append(f"{k}: {ex}")
                     ok = self.ctx.allreduce(0.0, "min") if self.ctx.is_distributed else 0.0
+                if ok <= 0:
+                    # a transport that set up but failed its trial (on any rank) must not stay
+                    # behind the next one: abort its communicator / unmap its peers first
+                    self.engine.drop_transport()
+                    self.transport = "none"
+                    self._torch_transport = None
                 if ok > 0:
                     if errors and self.ctx.rank == 0:
                         import warnings
@@ -183,6 +189,11 @@ class GrayScott:
             rc = self.engine.rccl_info()
             if rc is not None:
                 info["rccl_nranks"], info["rccl_rank"], info["rccl_device"] = rc
+            if self.transport == "ipc":
+                # which peers this rank maps, the device each runs on (as numbered here) and
+                # whether hipDeviceCanAccessPeer confirmed the path (-1: not checkable)
+                info["ipc_peers"] = [{"rank": r, "device": d, "peer_access": a}
+                                     for r, d, a in self.engine.ipc_peers()]
         return info
 
     @property
@@ -308,18 +319,11 @@ class GrayScott:
         self.engine.sync()
 
     def randomize_fields(self, seed: int = 0, lo: float = 0.0, hi: float = 1.0) -> None:
-        """Random-init the interior: u, v ~ U[lo, hi) drawn on the field device (benchmarks on
-        "random-init u/v fields", BASELINE.json).  Per-rank streams keyed by ``seed`` and rank."""
-        tdt = _TORCH_DTYPES[self.dtype]
-        gen = torch.Generator(device=self.device).manual_seed(int(seed) * 1000003 + self.domain.rank)
-        u = torch.rand(self.local_shape, generator=gen, device=self.device, dtype=tdt)
-        v = torch.rand(self.local_shape, generator=gen, device=self.device, dtype=tdt)
-        if (lo, hi) != (0.0, 1.0):
-            u.mul_(hi - lo).add_(lo)
-            v.mul_(hi - lo).add_(lo)
-        if self.backend == "hip":
-            torch.cuda.synchronize(self.device)
-        self.engine.insert(u.data_ptr(), v.data_ptr())
+        """Random-init the interior: u, v ~ U[lo, hi) (benchmarks on "random-init u/v fields",
+        BASELINE.json), drawn in place by the native engine from a counter-based Philox stream
+        keyed on the *global* cell id (gs::random_init_cell): every decomposition -- and the
+        golden model on any sub-box -- starts from the same global state."""
+        self.engine.randomize(seed, lo, hi)
         self.engine.sync()
 
     def full_state(self, which: Optional[int] = None) -> torch.Tensor:

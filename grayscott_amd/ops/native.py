@@ -85,6 +85,10 @@ def _declare(lib) -> None:
     lib.gs_insert.restype = c_int
     lib.gs_stats.argtypes = [c_void_p, POINTER(c_double)]
     lib.gs_stats.restype = c_int
+    lib.gs_randomize.argtypes = [c_void_p, c_uint64, c_double, c_double]
+    lib.gs_randomize.restype = c_int
+    lib.gs_drop_transport.argtypes = [c_void_p]
+    lib.gs_drop_transport.restype = c_int
     lib.gs_set_transport.argtypes = [c_void_p, TRANSPORT_FN, c_void_p]
     lib.gs_set_transport.restype = c_int
     lib.gs_plan_info.argtypes = [c_void_p, POINTER(c_int64), POINTER(c_int64), POINTER(c_int32),
@@ -123,6 +127,8 @@ def _declare(lib) -> None:
         lib.gs_ipc_export.restype = c_int
         lib.gs_ipc_connect.argtypes = [c_void_p, c_int32, ctypes.c_char_p, POINTER(c_int64)]
         lib.gs_ipc_connect.restype = c_int
+        lib.gs_ipc_peers.argtypes = [c_void_p, c_int32, POINTER(c_int32), c_int32]
+        lib.gs_ipc_peers.restype = c_int
     if hasattr(lib, "gs_fused_choice"):
         lib.gs_fused_choice.argtypes = [c_void_p, c_int32, c_int32, POINTER(c_int32),
                                         POINTER(ctypes.c_float)]
@@ -272,6 +278,16 @@ class Engine:
     def insert(self, u_ptr: int, v_ptr: int):
         self._chk(self.lib.gs_insert(self.h, c_void_p(u_ptr), c_void_p(v_ptr)), "insert")
 
+    def randomize(self, seed: int, lo: float = 0.0, hi: float = 1.0):
+        """Random interior, u, v ~ U[lo, hi): a function of the global cell and ``seed`` only
+        (the same global state for every decomposition)."""
+        self._chk(self.lib.gs_randomize(self.h, int(seed) & 0xFFFFFFFFFFFFFFFF, float(lo),
+                                        float(hi)), "randomize")
+
+    def drop_transport(self):
+        """Forget the halo transport (abort the RCCL communicator, unmap IPC peers)."""
+        self._chk(self.lib.gs_drop_transport(self.h), "drop_transport")
+
     def stats(self):
         out = (c_double * 6)()
         self._chk(self.lib.gs_stats(self.h, out), "stats")
@@ -337,6 +353,17 @@ class Engine:
                 tab[base + 2 + 3 * j:base + 5 + 3 * j] = [int(peer), int(off), int(cells)]
         self._chk(self.lib.gs_ipc_connect(self.h, DTYPE_CODES[self.dtype], b"".join(handles), tab),
                   "ipc_connect")
+
+    def ipc_peers(self):
+        """[(peer rank, device as numbered here or -1, peer access 1 / -1 unknown)] of the IPC
+        transport's mapped peers ([] without it)."""
+        if not hasattr(self.lib, "gs_ipc_peers"):
+            return []
+        out = (c_int32 * (3 * 26))()
+        n = self.lib.gs_ipc_peers(self.h, DTYPE_CODES[self.dtype], out, 26)
+        if n < 0:
+            raise RuntimeError(f"ipc_peers failed: {last_error(self.lib)}")
+        return [(int(out[3 * i]), int(out[3 * i + 1]), int(out[3 * i + 2])) for i in range(n)]
 
     def rccl_info(self):
         """(communicator size, rank in it, HIP device) of the RCCL transport, or None."""

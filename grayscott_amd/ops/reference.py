@@ -78,6 +78,26 @@ def init_fields(L: Sequence[int], offsets=(0, 0, 0), sizes=None, dtype=np.float6
     return u, v
 
 
+def random_fields(L: Sequence[int], offsets=(0, 0, 0), sizes=None, seed: int = 0,
+                  lo: float = 0.0, hi: float = 1.0, dtype=np.float64):
+    """The benchmarks' random initial interior (gs::random_init_cell): a function of the
+    global cell only.  (w0, w1) = Philox4x32-10({q, q >> 32, ~0, ~0}, seed) with
+    q = gx + Lx * (gy + Ly * gz); u = lo + (hi - lo) * (w0 >> 8) * 2^-24, v from w1."""
+    L = [int(v) for v in L]
+    sizes = list(sizes) if sizes is not None else list(L)
+    gx = np.arange(offsets[0], offsets[0] + sizes[0], dtype=np.uint64)
+    gy = np.arange(offsets[1], offsets[1] + sizes[1], dtype=np.uint64)
+    gz = np.arange(offsets[2], offsets[2] + sizes[2], dtype=np.uint64)
+    Z, Y, X = np.meshgrid(gz, gy, gx, indexing="ij")
+    q = X + np.uint64(L[0]) * (Y + np.uint64(L[1]) * Z)
+    full = np.full(q.shape, 0xFFFFFFFF, dtype=np.uint64)
+    w0, w1, _, _ = philox4x32_10(q & MASK32, q >> np.uint64(32), full, full, seed)
+    s = 2.0 ** -24
+    u = (hi - lo) * ((w0 >> np.uint32(8)).astype(np.float64) * s) + lo
+    v = (hi - lo) * ((w1 >> np.uint32(8)).astype(np.float64) * s) + lo
+    return u.astype(dtype), v.astype(dtype)
+
+
 def bc_u(t: int) -> float:
     return 0.0 if (t & 1) else 1.0
 
@@ -138,10 +158,15 @@ def _step_torch(u, v, t, F, k, dt, Du, Dv, noise_amp, seed, periodic, L):
 
 
 def run(L, nsteps: int, F=0.02, k=0.048, dt=1.0, Du=0.2, Dv=0.1, noise_amp=0.0, seed=0,
-        periodic=False, dtype=np.float64, backend="numpy"):
+        periodic=False, dtype=np.float64, backend="numpy", init_seed=None):
+    """``nsteps`` global steps from the reference init, or (``init_seed`` given) from the
+    benchmarks' random init (random_fields)."""
     if isinstance(L, int):
         L = (L, L, L)
-    u, v = init_fields(L, dtype=dtype)
+    if init_seed is None:
+        u, v = init_fields(L, dtype=dtype)
+    else:
+        u, v = random_fields(L, seed=init_seed, dtype=dtype)
     for t in range(nsteps):
         u, v = step(u, v, t, F, k, dt, Du, Dv, noise_amp, seed, periodic, backend)
     return u, v

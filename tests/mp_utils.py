@@ -42,11 +42,15 @@ def _worker(rank, world, port, outdir, cfg):
         sim = GrayScott(settings, dom, ctx, fuse=cfg.get("fuse"), transport=cfg.get("transport"),
                         use_fused=cfg.get("use_fused", True))
         sim.init_fields()
+        if cfg.get("random_init") is not None:
+            sim.randomize_fields(seed=cfg["random_init"])
         if cfg.get("poison"):
             sim.poison_ghosts()
         sim.iterate(cfg["steps"])
         u, v = sim.get_fields()
-        np.savez(os.path.join(outdir, f"rank{rank}.npz"), u=u, v=v,
+        import json
+        info = json.dumps(sim.device_info())
+        np.savez(os.path.join(outdir, f"rank{rank}.npz"), u=u, v=v, info=info,
                  offsets=np.array(dom.proc_offsets), sizes=np.array(dom.proc_sizes),
                  step=sim.step, transport=sim.transport, overlapped=sim.overlapped,
                  zplanes=sim.engine.plan()["zplanes"])
@@ -83,5 +87,6 @@ def run_ranks(world: int, cfg: dict, timeout: float = 240.0):
             u[sl] = d["u"]
             v[sl] = d["v"]
             meta.append({"step": int(d["step"]), "transport": str(d["transport"]),
-                         "overlapped": bool(d["overlapped"]), "zplanes": bool(d["zplanes"])})
+                         "overlapped": bool(d["overlapped"]), "zplanes": bool(d["zplanes"]),
+                         "info": __import__("json").loads(str(d["info"]))})
         return u, v, meta

@@ -51,10 +51,8 @@ def test_candidates_for_mi355x():
     # the reference's Dims_create grid first (always timed, reported as reference_grid), then
     # z slabs with and without overlap
     assert candidates(512, 8, "hip") == [([2, 2, 2], 0, "auto"), ([1, 1, 8], 0, "auto"),
-                                        ([1, 1, 8], 0, "off"), ([1, 1, 8], 2, "auto"),
-                                        ([2, 2, 2], 0, "off"), ([2, 2, 2], 2, "auto"),
+                                        ([1, 1, 8], 0, "off"), ([2, 2, 2], 0, "off"),
                                         ([1, 2, 4], 0, "auto"), ([1, 2, 4], 0, "off"),
-                                        ([1, 1, 8], 0, "auto", {"GS_OVERLAP_RESERVE": "64"}),
                                         ([1, 1, 8], 0, "auto", {}, "ipc"),
                                         ([1, 1, 8], 0, "off", {}, "ipc"),
                                         ([2, 2, 2], 0, "auto", {}, "ipc"),

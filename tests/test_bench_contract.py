@@ -38,7 +38,7 @@ def test_bench_torchrun_two_ranks(decomp):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "bench.py",
            "--gpus", "2", "--backend", "CPU", "--L", "32", "--steps", "6", "--warmup", "2",
-           "--decomposition", decomp]
+           "--decomposition", decomp, "--check", "golden", "--check-steps", "4"]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600,
                        env=dict(os.environ, OMP_NUM_THREADS="1"))
     assert r.returncode == 0, r.stderr[-3000:]
@@ -48,6 +48,10 @@ def test_bench_torchrun_two_ranks(decomp):
     tab = d["data_path_tuning"]
     assert len(tab) == 1 and tab[0]["ok"] and tab[0]["ms_per_step"] > 0
     assert d["config"]["dims"] == ([1, 1, 2] if decomp == "z" else [2, 1, 1])
+    # the timed multi-rank path against the golden model on each rank's grown block: the CPU
+    # backend runs the golden model's own kernel, so the blocks agree bit for bit
+    assert d["check"]["golden_ok"] and d["check"]["max_abs_err"] == 0.0
+    assert d["check"]["golden_steps"] == 4
 
 
 def test_bench_self_launch_two_ranks():

