@@ -69,6 +69,25 @@ class HipBackend final : public gs::Backend {
  public:
   using V2 = typename gsk::Vec2<T>::type;
 
+  struct Part {  // the launch being tuned: z-runs and store mask (whole interior: zlen0 < 0)
+    int zlo0, zlen0, zlo1, zlen1, mask;
+    bool operator==(const Part& o) const {
+      return zlo0 == o.zlo0 && zlen0 == o.zlen0 && zlo1 == o.zlo1 && zlen1 == o.zlen1 &&
+             mask == o.mask;
+    }
+  };
+  // tuned shapes of the overlapped passes' post-exchange parts (one entry per launch shape)
+  struct PartChoice {
+    int n;
+    Part pt;
+    int cfg, sched;
+  };
+  // the shell variant chosen per (depth, sides) (see shell())
+  struct ShellChoice {
+    int n, sides, variant;
+    float ms[2];
+  };
+
   HipBackend(const Geom& g, const gs::Params& p, void* b0, void* b1, void* send, void* recv,
              hipStream_t stream)
       : g_(g), p_(p), stream_(stream) {
@@ -143,45 +162,109 @@ class HipBackend final : public gs::Backend {
   bool fused_supported(int n) const override { return gsk::fused_supported(g_, n); }
 
   bool fused_runs(int src, int dst, int n, int64_t t, int zlo0, int zlen0, int zlo1,
-                  int zlen1, bool leave_room, int tiles, int sides) override {
+                  int zlen1, bool leave_room, int mask) override {
     if (!gsk::fused_supported(g_, n)) return false;
     if (!tuned_[n]) autotune(src, dst, n, t);
     const bool pin = fused_pinned();
-    // launched on the selected stream (comm_select): the ring tiles of a packed pass run on the
-    // comm stream next to the z end slabs on the compute stream.
-    // the post-exchange parts of an overlapped pass (z end slabs: kind 1, ring tiles: kind 2)
-    // are short, latency-bound launches: they get their own tuned tile shape / schedule
-    // (an inner-tiles launch always keeps the whole-domain shape its ring complements)
-    const int kind = (leave_room || tiles == 1) ? 0 : (tiles == 2 ? 2 : 1);
+    // launched on the selected stream (comm_select).  The z end slabs of an overlapped pass
+    // (no leave_room) are short, latency-bound launches: they get their own tuned tile shape /
+    // schedule; the inner part keeps the whole-domain choice.
     int c = cfg_[n], sc = sched_[n];
-    if (kind && !pin) {
-      const Part pt{zlo0, zlen0, zlo1, zlen1, tiles, sides};
-      PartChoice* pc = nullptr;
-      for (PartChoice& q : parts_)
-        if (q.n == n && q.pt.zlo0 == pt.zlo0 && q.pt.zlen0 == pt.zlen0 && q.pt.zlo1 == pt.zlo1 &&
-            q.pt.zlen1 == pt.zlen1 && q.pt.tiles == pt.tiles && q.pt.sides == pt.sides)
-          pc = &q;
-      if (!pc) {
-        parts_.push_back(PartChoice{n, pt, cfg_[n], sched_[n]});
-        pc = &parts_.back();
-        float ms = 0.f;
-        // the ring tiles are the complement of the inner launch's tile rectangle, which
-        // depends on the tile shape: keep the inner (whole-domain) shape, tune the schedule
-        const int fixed = kind == 2 ? std::max(cfg_[n], 0) : -1;
-        if (!autotune_part(src, dst, n, t, pt, &pc->cfg, &pc->sched, &ms, fixed)) {
-          pc->cfg = cfg_[n];
-          pc->sched = sched_[n];
-        }
-      }
-      c = pc->cfg;
-      sc = pc->sched;
+    if (!leave_room && !pin) {
+      const PartChoice& pc = part_choice(src, dst, n, t, Part{zlo0, zlen0, zlo1, zlen1, mask});
+      c = pc.cfg;
+      sc = pc.sched;
     }
     const bool ok = gsk::launch_fused<T>(buf_[src], buf_[dst], g_, p_, n, t, xs_,
                                          pin ? -1 : c, pin ? -1 : sc, zlo0, zlen0,
-                                         zlo1, zlen1, leave_room ? kOverlapReserve : 0, tiles, sides);
-    if (!ok) throw std::runtime_error("fused_runs: invalid z-runs");
+                                         zlo1, zlen1, leave_room ? kOverlapReserve : 0, mask);
+    if (!ok) throw std::runtime_error("fused_runs: invalid z-runs or mask");
     HIP_CHECK(hipGetLastError());
     return true;
+  }
+
+  // tuned {cfg, sched} of a z-run launch (first use times the candidates)
+  const PartChoice& part_choice(int src, int dst, int n, int64_t t, const Part& pt) {
+    for (const PartChoice& q : parts_)
+      if (q.n == n && q.pt == pt) return q;
+    parts_.push_back(PartChoice{n, pt, cfg_[n], sched_[n]});
+    PartChoice& pc = parts_.back();
+    float ms = 0.f;
+    if (!autotune_part(src, dst, n, t, pt, &pc.cfg, &pc.sched, &ms)) {
+      pc.cfg = cfg_[n];
+      pc.sched = sched_[n];
+    }
+    return pc;
+  }
+
+  // The shell of an overlapped pass (engine.h shell_run): the n-deep slabs at the faces in
+  // `sides`.  Two ways, timed against each other at first use per (n, sides) and the faster
+  // kept: (0) one k_slab launch for every face; (1) the z slabs as one two-run k_fused launch
+  // (its own tuned tile) and the x / y slabs as a k_slab launch after it.
+  bool shell(int src, int dst, int n, int64_t t, int sides, int variant) override {
+    if (!gsk::fused_supported(g_, n) || !sides) return sides == 0;
+    if (!tuned_[n]) autotune(src, dst, n, t);
+    if (variant >= 0) {
+      shell_variant(src, dst, n, t, sides, variant & 1);
+      return true;
+    }
+    ShellChoice* sc = nullptr;
+    for (ShellChoice& q : shells_)
+      if (q.n == n && q.sides == sides) sc = &q;
+    if (!sc) {
+      shells_.push_back(ShellChoice{n, sides, 0, {0.f, 0.f}});
+      sc = &shells_.back();
+      if (sides & 48) {
+        // warm both (the first k_fused z-run launch tunes its own shape), then best of 3
+        hipStream_t keep = xs_;
+        xs_ = stream_;
+        hipEvent_t e0, e1;
+        HIP_CHECK(hipEventCreate(&e0));
+        HIP_CHECK(hipEventCreate(&e1));
+        float best[2] = {1e30f, 1e30f};
+        for (int r = 0; r < 4; ++r)
+          for (int v = 0; v < 2; ++v) {
+            HIP_CHECK(hipEventRecord(e0, stream_));
+            shell_variant(src, dst, n, t, sides, v);
+            HIP_CHECK(hipEventRecord(e1, stream_));
+            HIP_CHECK(hipEventSynchronize(e1));
+            float ms = 0.f;
+            HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+            if (r > 0 && ms < best[v]) best[v] = ms;
+          }
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        xs_ = keep;
+        sc->variant = best[1] < best[0] ? 1 : 0;
+        sc->ms[0] = best[0];
+        sc->ms[1] = best[1];
+      }
+    }
+    shell_variant(src, dst, n, t, sides, sc->variant);
+    return true;
+  }
+
+  void shell_variant(int src, int dst, int n, int64_t t, int sides, int variant) {
+    int slab_sides = sides;
+    if (variant == 1 && (sides & 48)) {
+      const int la = (sides & 16) ? n : 0, lb = (sides & 32) ? n : 0;
+      if (la > 0) fused_runs(src, dst, n, t, 0, la, g_.nz - lb, lb, false, 0);
+      else fused_runs(src, dst, n, t, g_.nz - lb, lb, 0, 0, false, 0);
+      slab_sides = sides & 15;
+    }
+    if (slab_sides) {
+      if (!gsk::launch_shell<T>(buf_[src], buf_[dst], g_, p_, n, t, slab_sides, num_cus(), xs_))
+        throw std::runtime_error("shell: unsupported sub-domain (needs >= 2n cells per axis)");
+      HIP_CHECK(hipGetLastError());
+    }
+  }
+
+  int num_cus() const {
+    static int cus = 0;
+    if (!cus && (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev_) !=
+                     hipSuccess || cus < 1))
+      cus = 256;
+    return cus;
   }
 
   bool has_comm_stream() const override { return comm_stream_ != nullptr; }
@@ -240,9 +323,6 @@ class HipBackend final : public gs::Backend {
   // reads `src` and writes `dst`, so every candidate can be timed on the live buffers without
   // changing the simulation state, and all candidates produce bit-identical results.
   // Disabled by GS_AUTOTUNE=0 or by an explicit GS_FUSED_CFG / GS_FUSED_SCHED.
-  struct Part {  // the launch being tuned: z-runs and tile subset (whole interior: zlen0 < 0)
-    int zlo0, zlen0, zlo1, zlen1, tiles, sides;
-  };
   static bool autotune_enabled() {
     const char* e = getenv("GS_AUTOTUNE");
     return !((e && atoi(e) == 0) || getenv("GS_FUSED_CFG") || getenv("GS_FUSED_SCHED") ||
@@ -264,8 +344,7 @@ class HipBackend final : public gs::Backend {
       return tsize == o.tsize && nx == o.nx && ny == o.ny && nz == o.nz && H == o.H &&
              periodic == o.periodic && noise == o.noise && n == o.n && fixed == o.fixed &&
              q32 == o.q32 && reserve == o.reserve && Lx == o.Lx && Ly == o.Ly && Lz == o.Lz &&
-             pt.zlo0 == o.pt.zlo0 && pt.zlen0 == o.pt.zlen0 && pt.zlo1 == o.pt.zlo1 &&
-             pt.zlen1 == o.pt.zlen1 && pt.tiles == o.pt.tiles && pt.sides == o.pt.sides;
+             pt == o.pt;
     }
   };
   struct TuneVal {
@@ -317,7 +396,7 @@ class HipBackend final : public gs::Backend {
       for (int sc = 0; sc < nsched; ++sc) cands.push_back({c, sc});
     auto launch = [&](const Cand& c) {
       return gsk::launch_fused<T>(buf_[src], buf_[dst], g_, p_, n, t, stream_, c.cfg, c.sched,
-                                  pt.zlo0, pt.zlen0, pt.zlo1, pt.zlen1, 0, pt.tiles, pt.sides);
+                                  pt.zlo0, pt.zlen0, pt.zlo1, pt.zlen1, 0, pt.mask);
     };
     // interleaved rounds (box-to-box and launch-to-launch jitter is several %): first launch
     // of each candidate is a warm-up, then the best of kRounds timed launches decides
@@ -354,7 +433,7 @@ class HipBackend final : public gs::Backend {
 
   void autotune(int src, int dst, int n, int64_t t) {
     tuned_[n] = true;
-    const Part whole{0, -1, 0, 0, 0, 0};
+    const Part whole{0, -1, 0, 0, 0};
     float ms = 0.f;
     if (autotune_part(src, dst, n, t, whole, &cfg_[n], &sched_[n], &ms)) tuned_ms_[n] = ms;
   }
@@ -795,12 +874,7 @@ class HipBackend final : public gs::Backend {
   int cfg_[4] = {-1, -1, -1, -1};
   int sched_[4] = {-1, -1, -1, -1};
   float tuned_ms_[4] = {0.f, 0.f, 0.f, 0.f};
-  // tuned shapes of the overlapped passes' post-exchange parts (one entry per launch shape)
-  struct PartChoice {
-    int n;
-    Part pt;
-    int cfg, sched;
-  };
+  std::vector<ShellChoice> shells_;
   std::vector<PartChoice> parts_;
 };
 

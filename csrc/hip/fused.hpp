@@ -42,12 +42,13 @@ struct FusedArgs {
   int64_t units;
   int32_t sched;   // 0: units split evenly; 1: XCD-grouped z-chunks; 2: persistent XCD rounds
   int32_t nchunk;  // sched 1/2: z-chunks per tile
-  int32_t ntiles;  // tiles enumerated (ntx * nty, or the inner / ring subset)
-  // tile subset (comm/compute overlap of packed halos): 0 all tiles, 1 the inner rectangle
-  // [itx0, itx1) x [ity0, ity1) (no input cell within reach of a fresh halo), 2 its ring
-  int32_t tmode;
-  int32_t sides;  // bit0/1/2/3: neighbour at -x/+x/-y/+y (whose halo is in flight)
-  int32_t itx0, itx1, ity0, ity1;
+  int32_t ntiles;  // tiles enumerated (ntx * nty)
+  // output store mask [mx0, mx1) x [my0, my1) (local x / y; the whole interior by default).
+  // The inner part of an overlapped pass clips its outputs to the cells at least T from every
+  // x / y face whose halo is in flight: those depend on interior cells only, so the tiles may
+  // read ghost cells that are being written meanwhile (the values never reach a stored cell);
+  // the k-deep face slabs are computed by k_slab once the halos have landed (slab.hpp).
+  int32_t mx0, mx1, my0, my1;
   int32_t grpM;    // sched 1/2: workgroups per XCD group (grid = 8 * grpM)
   int32_t cfg;     // tile/prefetch configuration index (fused_cfg_names)
   int64_t t;
@@ -506,37 +507,6 @@ __device__ __forceinline__ bool fused_period(FusedState<C>& S,
   }
 }
 
-// Enumerated tile index -> (tx, ty) of the full ntx x nty tile grid for the tile subset.
-__device__ __forceinline__ void map_tile(const FusedArgs& a, int t, int& tx, int& ty) {
-  if (a.tmode == 0) {
-    tx = t % a.ntx;
-    ty = t / a.ntx;
-  } else if (a.tmode == 1) {
-    const int w = a.itx1 - a.itx0;
-    tx = a.itx0 + t % w;
-    ty = a.ity0 + t / w;
-  } else {
-    // ring: full rows below ity0, the left / right parts of rows [ity0, ity1), full rows above
-    const int n0 = a.ity0 * a.ntx;
-    if (t < n0) {
-      tx = t % a.ntx;
-      ty = t / a.ntx;
-      return;
-    }
-    t -= n0;
-    const int mid = a.ntx - (a.itx1 - a.itx0), h = a.ity1 - a.ity0;
-    if (t < h * mid) {
-      ty = a.ity0 + t / mid;
-      const int r = t % mid;
-      tx = r < a.itx0 ? r : a.itx1 + (r - a.itx0);
-      return;
-    }
-    t -= h * mid;
-    tx = t % a.ntx;
-    ty = a.ity1 + t / a.ntx;
-  }
-}
-
 template <class C, typename T>
 __global__ __launch_bounds__(64 * C::WAVES, C::WPEU) void k_fused(const typename C::V2* __restrict__ s,
                                                             typename C::V2* __restrict__ d,
@@ -636,8 +606,7 @@ __global__ __launch_bounds__(64 * C::WAVES, C::WPEU) void k_fused(const typename
       const int z0 = a.zlo[run] + (zv - rv0);
       const int z1 = z0 + (zv1 - zv);
       u += zv1 - zv;
-      int tx, ty;
-      map_tile(a, tile, tx, ty);
+      const int tx = tile % a.ntx, ty = tile / a.ntx;
       const int X0 = tx * a.xstep - TL;
       const int Y0 = a.ybase + ty * a.ystep - TL;
       const int x = X0 + sg.lane;
@@ -648,9 +617,9 @@ __global__ __launch_bounds__(64 * C::WAVES, C::WPEU) void k_fused(const typename
       sg.gx = gwrap<C>(sg.gxu, g.Lx);
       sg.gy0 = g.oy + ylo;
       sg.gx32 = (uint32_t)sg.gx;
-      const int ox1 = min(X0 + TL + a.xstep, g.nx);
-      const int oy0 = max(Y0 + TL, 0), oy1 = min(Y0 + TL + a.ystep, g.ny);
-      const bool xin = x >= max(X0 + TL, 0) && x < ox1;
+      const int ox1 = min(X0 + TL + a.xstep, a.mx1);
+      const int oy0 = max(Y0 + TL, a.my0), oy1 = min(Y0 + TL + a.ystep, a.my1);
+      const bool xin = x >= max(X0 + TL, a.mx0) && x < ox1;
       sg.svoff = xin ? sg.voff : (int)0x80000000;  // masked lanes store out of range
       sg.srow0 = max(oy0 - ylo, 0);
       sg.srow1 = min(oy1 - ylo, ROWS);
@@ -719,22 +688,6 @@ struct FusedLaunch {
     a.ntx = (a.g.nx + a.xstep - 1) / a.xstep;
     a.nty = (a.g.ny - a.ybase + a.ystep - 1) / a.ystep;
     a.ntiles = a.ntx * a.nty;
-    if (a.tmode != 0) {
-      // inner rectangle: tiles whose level-0 input box [X0, X0 + 64) x [Y0, Y0 + rows) stays
-      // inside the interior on every side whose halo is in flight
-      const int rows = C::RT;
-      int x0 = 0, x1 = a.ntx, y0 = 0, y1 = a.nty;
-      if (a.sides & 1) while (x0 < a.ntx && x0 * a.xstep - C::TL < 0) ++x0;
-      if (a.sides & 2) while (x1 > x0 && (x1 - 1) * a.xstep - C::TL + 64 > a.g.nx) --x1;
-      if (a.sides & 4) while (y0 < a.nty && a.ybase + y0 * a.ystep - C::TL < 0) ++y0;
-      if (a.sides & 8)
-        while (y1 > y0 && a.ybase + (y1 - 1) * a.ystep - C::TL + rows > a.g.ny) --y1;
-      if (x1 <= x0 || y1 <= y0) x0 = x1 = y0 = y1 = 0;  // no inner tile: the ring is all
-      a.itx0 = x0; a.itx1 = x1; a.ity0 = y0; a.ity1 = y1;
-      const int inner = (x1 - x0) * (y1 - y0);
-      a.ntiles = a.tmode == 1 ? inner : a.ntiles - inner;
-      if (a.ntiles == 0) return;
-    }
     a.units = (int64_t)a.ntiles * a.nzv;
     static int cus = 0;
     if (!cus) {
@@ -959,7 +912,7 @@ template <typename T>
 bool launch_fused(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, const Geom& g,
                   const gs::Params& p, int n, int64_t t, hipStream_t st, int cfg = -1,
                   int sched = -1, int zlo0 = 0, int zlen0 = -1, int zlo1 = 0, int zlen1 = 0,
-                  int reserve = 0, int tmode = 0, int sides = 0) {
+                  int reserve = 0, int mask = 0) {
   if (!fused_supported(g, n)) return false;
   FusedArgs a{};
   if (zlen0 < 0) zlen0 = g.nz;
@@ -972,8 +925,12 @@ bool launch_fused(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, co
   a.zlo[1] = zlo1; a.zlen[1] = zlen1;
   a.nzv = zlen0 + zlen1;
   a.reserve = reserve > 0 ? reserve : 0;
-  a.tmode = tmode;
-  a.sides = sides;
+  // mask bit0/1/2/3: leave the n cells next to the -x/+x/-y/+y face unwritten (overlap)
+  a.mx0 = (mask & 1) ? n : 0;
+  a.mx1 = (mask & 2) ? g.nx - n : g.nx;
+  a.my0 = (mask & 4) ? n : 0;
+  a.my1 = (mask & 8) ? g.ny - n : g.ny;
+  if (a.mx1 <= a.mx0 || a.my1 <= a.my0) return false;
   a.g = g;
   a.t = t;
   // GS_PHILOX_GENERIC=1 forces the 64-bit-counter Philox path (tests: both paths agree bitwise)

@@ -106,6 +106,7 @@ void launch_seed(typename Vec2<T>::type* f, const Geom& g, hipStream_t s) {
 }
 
 #include "stencil.hpp"
+#include "slab.hpp"
 
 // ------------------------------------------------------------------------------------------
 // halo pack / unpack: all messages in one launch (blockIdx.y = message)

@@ -26,7 +26,9 @@ int gs_set_loopback(gs_engine* e, int32_t on);  // self messages via the device 
 int gs_overlapped(gs_engine* e, int32_t k);      // 1 if a k-step pass overlaps its exchange
 int gs_plan_zplanes(gs_engine* e);               // 1 if halos are whole contiguous z planes
 int gs_fused_runs_raw(gs_engine* e, int32_t k, int32_t zlo0, int32_t zlen0, int32_t zlo1,
-                      int32_t zlen1, int32_t tiles, int32_t sides);  // timing (state unchanged)
+                      int32_t zlen1, int32_t mask, int32_t leave_room);  // timing (state unchanged)
+// variant: -1 the tuned choice, 0 all faces through k_slab, 1 z faces through k_fused
+int gs_shell_raw(gs_engine* e, int32_t k, int32_t sides, int32_t variant);
 int gs_advance(gs_engine* e, int64_t nsteps);
 int gs_exchange(gs_engine* e);
 int64_t gs_get_step(gs_engine* e);

@@ -69,15 +69,23 @@ int gs_set_overlap(gs_engine* e, int32_t mode) { GS_TRY(e->eng->set_overlap(mode
 int gs_set_loopback(gs_engine* e, int32_t on) { GS_TRY(e->eng->set_loopback(on != 0)) }
 int gs_overlapped(gs_engine* e, int32_t k) { return e->eng->overlapped(k) ? 1 : 0; }
 int gs_plan_zplanes(gs_engine* e) { return e->eng->plan().zplanes; }
-// Timing primitive: one fused k-step update of the given z-runs from the current buffer into
-// the other one (interior planes only, so the next pass overwrites it; state unchanged).
+// Timing primitives: one fused k-step update of the given z-runs (store mask: engine.h
+// fused_runs) / of the shell slabs at `sides`, from the current buffer into the other one
+// (interior cells only, so the next pass overwrites them; the state is unchanged).
 int gs_fused_runs_raw(gs_engine* e, int32_t k, int32_t zlo0, int32_t zlen0, int32_t zlo1,
-                      int32_t zlen1, int32_t tiles, int32_t sides) {
+                      int32_t zlen1, int32_t mask, int32_t leave_room) {
   GS_TRY({
     gs::Engine& g = *e->eng;
     if (!g.backend()->fused_runs(g.cur(), 1 - g.cur(), k, g.step(), zlo0, zlen0, zlo1, zlen1,
-                                 false, tiles, sides))
+                                 leave_room != 0, mask))
       throw std::runtime_error("fused runs unsupported for this k / backend");
+  })
+}
+int gs_shell_raw(gs_engine* e, int32_t k, int32_t sides, int32_t variant) {
+  GS_TRY({
+    gs::Engine& g = *e->eng;
+    if (!g.backend()->shell(g.cur(), 1 - g.cur(), k, g.step(), sides, variant))
+      throw std::runtime_error("shell unsupported for this k / backend");
   })
 }
 int gs_advance(gs_engine* e, int64_t n) { GS_TRY(e->eng->advance(n)) }

@@ -49,12 +49,19 @@ class Backend {
   virtual bool fused_supported(int n) const { (void)n; return false; }
   // leave_room: launch fewer workgroups than the device holds so concurrently running
   // communication kernels (RCCL) find free slots instead of waiting for this kernel to end.
-  // tiles: 0 all x-y tiles; 1 only the inner tiles, whose inputs stay clear of the x / y
-  // halos flagged in `sides` (bit0 -x, bit1 +x, bit2 -y, bit3 +y); 2 the remaining ring.
+  // mask (bit0 -x, bit1 +x, bit2 -y, bit3 +y): outputs within n of those faces are not
+  // written -- the inner part of an overlapped pass, whose tiles may read in-flight halos.
   virtual bool fused_runs(int src, int dst, int n, int64_t t, int zlo0, int zlen0, int zlo1,
-                          int zlen1, bool leave_room = false, int tiles = 0, int sides = 0) {
+                          int zlen1, bool leave_room = false, int mask = 0) {
     (void)src; (void)dst; (void)n; (void)t; (void)zlo0; (void)zlen0; (void)zlo1; (void)zlen1;
-    (void)leave_room; (void)tiles; (void)sides;
+    (void)leave_room; (void)mask;
+    return false;
+  }
+  // the shell of an overlapped n-step pass: the n cells next to every face flagged in `sides`
+  // (bit0 -x, bit1 +x, bit2 -y, bit3 +y, bit4 -z, bit5 +z), src at time t -> dst.  Supported
+  // exactly when fused_supported(n).  variant >= 0 forces one implementation (tests).
+  virtual bool shell(int src, int dst, int n, int64_t t, int sides, int variant = -1) {
+    (void)src; (void)dst; (void)n; (void)t; (void)sides; (void)variant;
     return false;
   }
   // in-place transport of a zplanes plan straight from / into field buffer b (no pack)
@@ -151,12 +158,13 @@ class Engine {
       if (d != 13 && cfg_.nbr[d] >= 0 && (on || cfg_.nbr[d] != cfg_.rank)) has_remote_ = true;
   }
   // whether a pass of k steps runs with the halo exchange overlapped with the inner update:
-  // z-slab plans (in-place planes) split z only; packed plans split z and the x-y tile grid
-  // ("auto" only with a device transport: a host callback transport serialises anyway)
+  // the inner box (cells >= k from every face with a neighbour) while the halos fly, then the
+  // k-deep face slabs ("auto" only with a device transport: a host callback serialises anyway)
   bool overlapped(int k) const {
+    const Geom& g = cfg_.g;
     return (overlap_ == 1 || (overlap_ == -1 && tfn_ == nullptr)) && cfg_.use_fused && k > 1 &&
-           has_remote_ && be_->has_comm_stream() &&
-           be_->fused_supported(k) && cfg_.g.nz >= 2 * k + 1;
+           has_remote_ && be_->has_comm_stream() && be_->fused_supported(k) &&
+           g.nz >= 2 * k + 1 && g.nx >= 2 * k + 1 && g.ny >= 2 * k + 1;
   }
   double comm_calls() const { return (double)ncomm_; }
 
@@ -184,7 +192,11 @@ class Engine {
       be_->prepare_fused(cur_, 1 - cur_, n, t_);
       // tune the overlapped passes' post-exchange launches now too (their first call times
       // the candidates), so no tuning lands inside a timed region; all on the compute stream
-      if (overlapped(n)) shell_runs(cur_, 1 - cur_, n, t_, overlap_split(n), false);
+      if (overlapped(n)) {
+        const Split sp = overlap_split(n);
+        inner_run(cur_, 1 - cur_, n, t_, sp);
+        shell_run(cur_, 1 - cur_, n, t_, sp);
+      }
     }
     // the timing runs scribbled over the other buffer: restore the reference's zeroed
     // u_temp/v_temp (ghosts included) so the ghost-parity bookkeeping stays exact
@@ -306,10 +318,9 @@ class Engine {
         be_->comm_select(false);
         be_->wait_mark(3, false);
         const Split sp = overlap_split(k);
-        if (sp.z1 > sp.z0) {
+        {
           TraceRange tr("gs.fused_inner");
-          be_->fused_runs(cur_, oth, k, t_, sp.z0, sp.z1 - sp.z0, 0, 0, true,
-                          sp.sides ? 1 : 0, sp.sides);
+          inner_run(cur_, oth, k, t_, sp);
         }
         be_->comm_select(true);
         exchange_finish(true);
@@ -317,7 +328,7 @@ class Engine {
         be_->comm_join();  // the compute stream sees the landed halos
         {
           TraceRange tr("gs.fused_shell");
-          shell_runs(cur_, oth, k, t_, sp, true);
+          shell_run(cur_, oth, k, t_, sp);
         }
         cur_ = oth;
         t_ += k;
@@ -381,17 +392,16 @@ class Engine {
       exchange_finish(true);  // (packed plans) unpack
       be_->comm_select(false);
       if (p > 0) be_->wait_mark(2, false);
-      if (sp.z1 > sp.z0) {
+      {
         TraceRange tr("gs.fused_inner");
-        be_->fused_runs(cur_, oth, k, t_, sp.z0, sp.z1 - sp.z0, 0, 0, true, sp.sides ? 1 : 0,
-                        sp.sides);
+        inner_run(cur_, oth, k, t_, sp);
       }
       be_->mark((int)(p & 1), false);
       if (p > 0) be_->wait_mark((int)((p - 1) & 1), true);
       {
         TraceRange tr("gs.fused_shell");
         be_->comm_select(true);
-        shell_runs(cur_, oth, k, t_, sp, false);
+        shell_run(cur_, oth, k, t_, sp);
         be_->comm_select(false);
       }
       be_->mark(2, true);
@@ -401,10 +411,11 @@ class Engine {
     be_->comm_join();
   }
 
-  // Split of an overlapped k-step pass.  The inner box [z0, z1) x (inner tiles) is clear of
-  // every face with a neighbour -- z by planes, x / y by whole tiles (z-slab plans split z
-  // only); a face without a neighbour (global boundary) needs no halo, so its end slab joins
-  // the inner part.
+  // Cell-granular split of an overlapped k-step pass.  The inner box -- planes [z0, z1), and
+  // along x / y every cell at least k from a face flagged in `sides` -- is clear of every face
+  // with a neighbour; a face without one (global boundary) needs no halo, so its cells join
+  // the inner part.  The shell is the k-deep slab at each flagged face (bit0 -x, bit1 +x,
+  // bit2 -y, bit3 +y, bit4 -z, bit5 +z).
   struct Split {
     int z0, z1, sides;
   };
@@ -414,27 +425,20 @@ class Engine {
     Split sp;
     sp.z0 = nb[dir_index(0, 0, -1)] >= 0 ? k : 0;
     sp.z1 = nb[dir_index(0, 0, 1)] >= 0 ? nz - k : nz;
-    sp.sides = plan_.zplanes ? 0
-        : (nb[dir_index(-1, 0, 0)] >= 0 ? 1 : 0) | (nb[dir_index(1, 0, 0)] >= 0 ? 2 : 0) |
-          (nb[dir_index(0, -1, 0)] >= 0 ? 4 : 0) | (nb[dir_index(0, 1, 0)] >= 0 ? 8 : 0);
+    sp.sides = (nb[dir_index(-1, 0, 0)] >= 0 ? 1 : 0) | (nb[dir_index(1, 0, 0)] >= 0 ? 2 : 0) |
+               (nb[dir_index(0, -1, 0)] >= 0 ? 4 : 0) | (nb[dir_index(0, 1, 0)] >= 0 ? 8 : 0) |
+               (sp.z0 > 0 ? 16 : 0) | (sp.z1 < nz ? 32 : 0);
     return sp;
   }
-  // The post-exchange launches of an overlapped pass: the z end slabs over all tiles and
-  // (packed plans) the ring tiles of the inner planes.  ring_on_comm: the ring runs on the comm
-  // stream in parallel with the end slabs on the compute stream -- two short, latency-bound
-  // launches side by side instead of back to back -- and the compute stream joins it.
-  void shell_runs(int src, int dst, int k, int64_t t, const Split& sp, bool ring_on_comm) {
-    const int nz = cfg_.g.nz;
-    const bool ring = sp.sides && sp.z1 > sp.z0;
-    const int la = sp.z0, lb = nz - (sp.z1 > sp.z0 ? sp.z1 : sp.z0);
-    if (ring) {
-      if (ring_on_comm) be_->comm_select(true);
-      be_->fused_runs(src, dst, k, t, sp.z0, sp.z1 - sp.z0, 0, 0, false, 2, sp.sides);
-      if (ring_on_comm) be_->comm_select(false);
-    }
-    if (la > 0) be_->fused_runs(src, dst, k, t, 0, la, nz - lb, lb);
-    else if (lb > 0) be_->fused_runs(src, dst, k, t, nz - lb, lb, 0, 0);
-    if (ring && ring_on_comm) be_->comm_join();
+  // the inner box: all x-y tiles over planes [z0, z1), outputs clipped by the x / y mask,
+  // leaving workgroup slots free for the communication kernels that run beside it
+  void inner_run(int src, int dst, int k, int64_t t, const Split& sp) {
+    if (sp.z1 > sp.z0) be_->fused_runs(src, dst, k, t, sp.z0, sp.z1 - sp.z0, 0, 0, true, sp.sides & 15);
+  }
+  // the shell: the k-deep face slabs, after the halos have landed
+  void shell_run(int src, int dst, int k, int64_t t, const Split& sp) {
+    if (sp.sides && !be_->shell(src, dst, k, t, sp.sides))
+      throw std::runtime_error("overlapped pass: the backend has no shell kernel for this depth");
   }
 
   EngineConfig cfg_;

@@ -1,16 +1,20 @@
 #!/usr/bin/env python3
 """Kernel-side cost of the comm/compute-overlap split on ONE MI355X (no communication).
 
-For a z-slab sub-domain (what one rank of an N-GPU 1x1xN run owns) it times, per k-step pass:
-  full   -- one fused launch over all nz planes (the non-overlapped pass),
-  inner  -- the launch over planes [k, nz-k) (runs while the halos are in flight),
-  shell  -- the launch over the two k-plane boundary slabs (runs after they land).
+For a sub-domain (what one rank of an N-GPU run owns) it times, per k-step pass:
+  full   -- one fused launch over the whole interior (the non-overlapped pass),
+  inner  -- the launch that runs while the halos are in flight: all x-y tiles over the planes
+            at least k from a z face with a neighbour, outputs clipped to at least k from every
+            x / y face with one (cell-granular store mask), workgroup slots left free,
+  shell  -- the k-deep face slabs after the halos land (engine.h shell_run: k_slab, or the
+            z slabs through k_fused -- the faster of the two, chosen at first use).
 The overlapped pass costs shell + max(inner, exchange); the plain one full + exchange.
-With --packed the sub-domain is one rank of the balanced grid (neighbours on every side):
-inner = the inner x-y tiles x planes [k, nz-k), shell = the z end slabs + the ring tiles.
+Default: a z slab (neighbours at -z and +z).  --packed: one rank of the balanced grid with
+neighbours on every side; --one-sided: neighbours only at +x, +y, +z (BASELINE config 3's
+2x2x2 ranks all look like this).
 
   python scripts/bench_overlap_split.py --nz 64 128 256 --k 2 3
-  python scripts/bench_overlap_split.py --packed --L 256 --nz 256 --k 2 3
+  python scripts/bench_overlap_split.py --packed --one-sided --L 256 --nz 256 --k 3
 """
 import argparse
 import json
@@ -47,36 +51,40 @@ def main():
             sim.init_fields()
             lib, h = sim.engine.lib, sim.engine.h
 
-            sides = 2 | 8 if a.one_sided else 15
+            if a.packed and a.one_sided:
+                sides = 2 | 8 | 32
+            elif a.packed:
+                sides = 63
+            else:
+                sides = 16 | 32
+            z0 = k if sides & 16 else 0
+            z1 = nz - k if sides & 32 else nz
 
-            def run(z0, n0, z1, n1, tiles=0):
-                native.check(lib, lib.gs_fused_runs_raw(h, k, z0, n0, z1, n1, tiles,
-                                                        sides if tiles else 0), "fused_runs")
+            def run(kind):
+                if kind == "full":
+                    rc = lib.gs_fused_runs_raw(h, k, 0, nz, 0, 0, 0, 0)
+                elif kind == "inner":
+                    rc = lib.gs_fused_runs_raw(h, k, z0, z1 - z0, 0, 0, sides & 15, 1)
+                else:
+                    rc = lib.gs_shell_raw(h, k, sides, -1)
+                native.check(lib, rc, kind)
 
             def timed(*runs):
                 for _ in range(3):
                     for r in runs:
-                        run(*r)
+                        run(r)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 torch.cuda.synchronize()
                 e0.record()
                 for _ in range(a.reps):
                     for r in runs:
-                        run(*r)
+                        run(r)
                 e1.record()
                 torch.cuda.synchronize()
                 return e0.elapsed_time(e1) / a.reps * 1e3  # us
 
-            full = timed((0, nz, 0, 0))
-            if a.packed and a.one_sided:
-                ins = [(0, nz - k, 0, 0, 1)]
-                shs = [(nz - k, k, 0, 0), (0, nz - k, 0, 0, 2)]
-            elif a.packed:
-                ins = [(k, nz - 2 * k, 0, 0, 1)]
-                shs = [(0, k, nz - k, k), (k, nz - 2 * k, 0, 0, 2)]
-            else:
-                ins = [(k, nz - 2 * k, 0, 0)]
-                shs = [(0, k, nz - k, k)]
+            full = timed("full")
+            ins, shs = ["inner"], ["shell"]
             inner = timed(*ins)
             shell = timed(*shs)
             both = timed(*(ins + shs))
@@ -85,7 +93,7 @@ def main():
                    "inner_us": round(inner, 1), "shell_us": round(shell, 1),
                    "inner_plus_shell_us": round(both, 1),
                    "full_mlups": round(a.L * a.L * nz * k / full, 0),
-                   "tile": sim.fused_choice().get(k)}
+                   "sides": sides, "tile": sim.fused_choice().get(k)}
             rows.append(row)
             print(json.dumps(row), flush=True)
             sim.close()
