@@ -69,11 +69,13 @@ class HipBackend final : public gs::Backend {
  public:
   using V2 = typename gsk::Vec2<T>::type;
 
-  struct Part {  // the launch being tuned: z-runs and store mask (whole interior: zlen0 < 0)
-    int zlo0, zlen0, zlo1, zlen1, mask;
+  // the launch being tuned: z-runs, store mask and the workgroup slots it leaves free
+  // (whole interior: zlen0 < 0)
+  struct Part {
+    int zlo0, zlen0, zlo1, zlen1, mask, reserve;
     bool operator==(const Part& o) const {
       return zlo0 == o.zlo0 && zlen0 == o.zlen0 && zlo1 == o.zlo1 && zlen1 == o.zlen1 &&
-             mask == o.mask;
+             mask == o.mask && reserve == o.reserve;
     }
   };
   // tuned shapes of the overlapped passes' post-exchange parts (one entry per launch shape)
@@ -166,18 +168,21 @@ class HipBackend final : public gs::Backend {
     if (!gsk::fused_supported(g_, n)) return false;
     if (!tuned_[n]) autotune(src, dst, n, t);
     const bool pin = fused_pinned();
-    // launched on the selected stream (comm_select).  The z end slabs of an overlapped pass
-    // (no leave_room) are short, latency-bound launches: they get their own tuned tile shape /
-    // schedule; the inner part keeps the whole-domain choice.
+    // launched on the selected stream (comm_select).  Every part of an overlapped pass -- the
+    // inner box (slots left free), the z end slabs (short, latency-bound) -- gets its own tuned
+    // tile shape / schedule; the whole interior keeps the choice made for it.
     int c = cfg_[n], sc = sched_[n];
-    if (!leave_room && !pin) {
-      const PartChoice& pc = part_choice(src, dst, n, t, Part{zlo0, zlen0, zlo1, zlen1, mask});
+    const int reserve = leave_room ? kOverlapReserve : 0;
+    const bool whole = zlo0 == 0 && zlen0 == g_.nz && zlen1 <= 0 && mask == 0 && reserve == 0;
+    if (!whole && !pin) {
+      const PartChoice& pc =
+          part_choice(src, dst, n, t, Part{zlo0, zlen0, zlo1, zlen1, mask, reserve});
       c = pc.cfg;
       sc = pc.sched;
     }
     const bool ok = gsk::launch_fused<T>(buf_[src], buf_[dst], g_, p_, n, t, xs_,
                                          pin ? -1 : c, pin ? -1 : sc, zlo0, zlen0,
-                                         zlo1, zlen1, leave_room ? kOverlapReserve : 0, mask);
+                                         zlo1, zlen1, reserve, mask);
     if (!ok) throw std::runtime_error("fused_runs: invalid z-runs or mask");
     HIP_CHECK(hipGetLastError());
     return true;
@@ -360,7 +365,7 @@ class HipBackend final : public gs::Backend {
     if (!autotune_enabled()) return false;
     const TuneKey key{(int)sizeof(T), g_.nx, g_.ny, g_.nz, g_.H, g_.periodic,
                       p_.noise != 0.0 ? 1 : 0, n, fixed_cfg, gsk::philox_q32(g_) ? 1 : 0,
-                      kOverlapReserve, g_.Lx, g_.Ly, g_.Lz, pt};
+                      pt.reserve, g_.Lx, g_.Ly, g_.Lz, pt};
     for (const auto& kv : tune_cache())
       if (kv.first == key) {
         *cfg = kv.second.cfg;
@@ -396,7 +401,7 @@ class HipBackend final : public gs::Backend {
       for (int sc = 0; sc < nsched; ++sc) cands.push_back({c, sc});
     auto launch = [&](const Cand& c) {
       return gsk::launch_fused<T>(buf_[src], buf_[dst], g_, p_, n, t, stream_, c.cfg, c.sched,
-                                  pt.zlo0, pt.zlen0, pt.zlo1, pt.zlen1, 0, pt.mask);
+                                  pt.zlo0, pt.zlen0, pt.zlo1, pt.zlen1, pt.reserve, pt.mask);
     };
     // interleaved rounds (box-to-box and launch-to-launch jitter is several %): first launch
     // of each candidate is a warm-up, then the best of kRounds timed launches decides
@@ -433,7 +438,7 @@ class HipBackend final : public gs::Backend {
 
   void autotune(int src, int dst, int n, int64_t t) {
     tuned_[n] = true;
-    const Part whole{0, -1, 0, 0, 0};
+    const Part whole{0, -1, 0, 0, 0, 0};
     float ms = 0.f;
     if (autotune_part(src, dst, n, t, whole, &cfg_[n], &sched_[n], &ms)) tuned_ms_[n] = ms;
   }

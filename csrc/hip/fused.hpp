@@ -707,6 +707,14 @@ struct FusedLaunch {
       // one unit per workgroup: never more units than resident slots (a second, partial
       // round of workgroups would double the time)
       int nch = (int)(slots / a.ntiles);
+      // the reserved slots cost a chunk per tile only when they must: if the whole device's
+      // chunking already leaves >= 8 slots over, keep it (256^3 rank: 7 chunks x 35 tiles of 256
+      // slots, 11 left -- a 16-slot reserve would drop to 6 chunks, +15 % per workgroup)
+      if (a.reserve > 0) {
+        const int64_t all = (int64_t)occupancy() * cus;
+        const int n0 = (int)(all / a.ntiles);
+        if (all - (int64_t)n0 * a.ntiles >= std::min(a.reserve, 8)) nch = n0;
+      }
       nch = std::max(1, std::min(nch, a.nzv / (4 * C::TL + 4) > 0 ? a.nzv / (4 * C::TL + 4) : 1));
       a.nchunk = nch;
       const int64_t nunits = (int64_t)a.ntiles * nch;

@@ -18,6 +18,13 @@
 //   M  the march axis: one plane per iteration; level L of plane p - L is computed from level
 //      L-1's planes p-L-1 .. p-L+1 (three-plane register rings: no LDS, no barriers)
 // orientation 0: x face (A=y, N=x, M=z); 1: y face (A=x, N=y, M=z); 2: z face (A=x, N=z, M=y).
+// The Philox block of a cell serves the four cells of its y-quad, and each orientation shares
+// it along its own y: across a quad of lanes (0: quad_transpose), between a lane's cells (1),
+// across four march steps (2: a per-cell block cache).
+// A face slab is small, so the launch is latency-bound: the level-0 planes are prefetched
+// three iterations ahead, every access goes through a per-unit buffer descriptor (uniform
+// offsets on the SALU, no 64-bit address VALU), and a unit's march chunk balances the
+// outputs' cone fill against SIMD occupancy (launch_slabs_tl).
 // Every wave is an independent unit (face, lane tile, march chunk).
 //
 // Bit-exactness: the overlapped pass must equal the one-rank run (k_fused everywhere) bit for
@@ -33,7 +40,9 @@ struct SlabFace {
   int32_t n0;               // first output cell along N: outputs [n0, n0 + k)
   int32_t a0, a1;           // outputs along A
   int32_t m0, m1;           // outputs along M
-  int32_t ntile, nchunk;    // lane tiles (64 - 2k outputs each) x march chunks
+  int32_t ntile, nchunk;    // lane tiles x march chunks
+  int32_t abase, astep;     // tile t: lanes at A = abase + t * astep + lane, owning the
+                            // outputs [a0 + t * astep, + astep)
   int32_t chunk;            // output planes per chunk
   int32_t u0;               // first unit (wave) of this face
 };
@@ -70,52 +79,96 @@ template <typename T, int TL_, bool PER_, bool NOISE_, bool Q32_, int OR_>
 struct SCfg {
   using V2 = typename PairT<T>::type;
   static constexpr int TL = TL_, OR = OR_, NC = 3 * TL_;
+  static constexpr int PF = 3;  // level-0 prefetch distance (planes)
   static constexpr bool PER = PER_, NOISE = NOISE_, Q32 = Q32_;
   using AX = SlabAxes<OR_>;
 };
 
 // per-unit constants
 struct SlabUnit {
-  int64_t base;          // element index of (A = lane, N = first level-0 cell, M = 0)
-  int64_t sN, sM;        // element strides along N and M
+  __amdgpu_buffer_rsrc_t src, dst;  // descriptors based at (A = -H, N = nb, M = pstart)
+  int voff, svoff;       // this lane's byte offset (its A coordinate); for its stores (out of
+                         // range on lanes that own no output)
+  int sNb, sMb;          // byte strides along N and M
+  int pstart;            // first level-0 plane
   int64_t gA, gN0, gM0;  // global coordinate of this lane, of level-0 cell 0, of M = 0
   int mc0, mc1;          // output planes along M
-  bool edge, aout, store;
+  int qr;                // lane & 3 (orientation 0: the lane's place in its y-quad)
+  uint32_t qm1, qm2;     // all-ones where bit 0 / bit 1 of qr is set (branch-free selects)
+  bool edge, aout;
 };
 
-template <class C, typename T>
-__device__ __forceinline__ uint32_t slab_word(const SlabUnit& u, const Geom& g, int j, int64_t gM,
-                                              int64_t step, uint64_t seed, gs::U4& blk,
-                                              bool refresh) {
-  using AX = typename C::AX;
-  int64_t gc[3];
-  gc[AX::A] = u.gA;
-  gc[AX::N] = u.gN0 + j;
-  gc[AX::M] = gM;
-  const int64_t gx = gwrap_t<C::PER>(gc[0], g.Lx), gy = gwrap_t<C::PER>(gc[1], g.Ly),
-                gz = gwrap_t<C::PER>(gc[2], g.Lz);
-  if (refresh) {
-    if constexpr (C::Q32) {
-      const uint32_t Ly4 = (uint32_t)((g.Ly + 3) >> 2);
-      blk = philox_dev<true>((uint32_t)gx + (uint32_t)g.Lx * ((uint32_t)(gy >> 2) +
-                                                               Ly4 * (uint32_t)gz),
-                             0u, (uint64_t)step, seed);
-    } else {
-      blk = gs::noise_block(gx, gy >> 2, gz, g.Lx, g.Ly, (uint64_t)step, seed);
-    }
-  }
-  const int wi = (int)(gy & 3);
-  return wi == 0 ? blk.x : (wi == 1 ? blk.y : (wi == 2 ? blk.z : blk.w));
+// m ? b : a bit by bit (one v_bfi_b32); a lane-varying ?: may compile to exec-mask branches
+__device__ __forceinline__ uint32_t bsel(uint32_t m, uint32_t a, uint32_t b) {
+  return (a & ~m) | (b & m);
+}
+// a[r] for the lane-varying index r = (m2 ? 2 : 0) + (m1 ? 1 : 0): three v_bfi_b32
+__device__ __forceinline__ uint32_t sel4(uint32_t m1, uint32_t m2, uint32_t a0, uint32_t a1,
+                                         uint32_t a2, uint32_t a3) {
+  return bsel(m2, bsel(m1, a0, a1), bsel(m1, a2, a3));
 }
 
+// lane s of each quad receives v of lane (s - M) & 3 (DPP quad_perm rotation)
+template <int M>
+__device__ __forceinline__ uint32_t quad_rot(uint32_t v) {
+  if constexpr (M == 0) return v;
+  constexpr int ctrl = M == 1 ? 0x93 : (M == 2 ? 0x4E : 0x39);
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, ctrl, 0xf, 0xf, false);
+}
+
+// Orientation 0 (lanes along y, y-quads aligned with lane quads): the four lanes of a quad
+// each draw the Philox block of a different cell c0 + r and exchange words, so that lane s
+// ends with word s (its y & 3) of each of the four cells' blocks -- one draw per four cells
+// instead of four.  W: this lane's block; returns X[c] = word (lane & 3) of cell c0 + c.
+//   Y[m] = W[(r + m) & 3] (per-lane rotation); Z[m] = Y[m] of lane (s - m) & 3 (DPP);
+//   X[c] = Z[(s - c) & 3].  24 selects + 3 DPP moves.
+__device__ __forceinline__ void quad_transpose(uint32_t m1, uint32_t m2, const gs::U4& W,
+                                               uint32_t (&X)[4]) {
+  const uint32_t w[4] = {W.x, W.y, W.z, W.w};
+  uint32_t Z[4];
+  Z[0] = sel4(m1, m2, w[0], w[1], w[2], w[3]);
+  Z[1] = quad_rot<1>(sel4(m1, m2, w[1], w[2], w[3], w[0]));
+  Z[2] = quad_rot<2>(sel4(m1, m2, w[2], w[3], w[0], w[1]));
+  Z[3] = quad_rot<3>(sel4(m1, m2, w[3], w[0], w[1], w[2]));
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+    X[c] = sel4(m1, m2, Z[(4 - c) & 3], Z[(5 - c) & 3], Z[(6 - c) & 3], Z[(7 - c) & 3]);
+}
+
+// The Philox block of global cell (gx, gy, gz) at `step` (gs::noise_block's stream); the round
+// keys of rounds 4-10 come from VGPRs filled once per unit (kv), not rebuilt per call
+template <class C>
+__device__ __forceinline__ gs::U4 slab_block(const Geom& g, int64_t gx, int64_t gy, int64_t gz,
+                                             int64_t step, uint64_t seed, const uint32_t* kv) {
+  if constexpr (C::Q32) {
+    const uint32_t Ly4 = (uint32_t)((g.Ly + 3) >> 2);
+    return philox_dev<true, true>((uint32_t)gx + (uint32_t)g.Lx * ((uint32_t)(gy >> 2) +
+                                                                   Ly4 * (uint32_t)gz),
+                                  0u, (uint64_t)step, seed, kv);
+  } else {
+    return gs::noise_block(gx, gy >> 2, gz, g.Lx, g.Ly, (uint64_t)step, seed);
+  }
+}
+
+__device__ __forceinline__ uint32_t word_of(const gs::U4& b, int i) {
+  return i == 0 ? b.x : (i == 1 ? b.y : (i == 2 ? b.z : b.w));
+}
+
+// registers of one unit
+template <class C>
+struct SlabRegs {
+  using V2 = typename C::V2;
+  V2 R[C::TL][3][C::NC];   // level L, ring slot (plane mod 3), cell j in [L, NC - L)
+  V2 NX[C::PF][C::NC];     // level-0 planes in flight
+  gs::U4 PC[C::OR == 2 && C::NOISE ? C::TL + 1 : 1][C::NC];  // orientation 2: block cache
+  uint32_t kv[14];         // Philox round keys of rounds 4-10
+};
+
 // Level L (1..TL) of plane q from level L-1's ring slots IM (plane q-1), IC (q), IP (q+1).
-// R[L][slot][j]: level L, cells j in [L, NC - L) (the unused entries are never touched, so
-// they take no registers).  Level TL is stored.
+// The unused entries of R are never touched, so they take no registers.  Level TL is stored.
 template <class C, typename T, int L, int IM, int IC, int IP>
-__device__ __forceinline__ void slab_level(typename C::V2 (&R)[C::TL][3][C::NC],
-                                           typename C::V2* __restrict__ d, const SlabArgs& a,
-                                           const SlabUnit& u, int q, const FoldCoef<T>& f,
-                                           T ar31, uint64_t seed) {
+__device__ __forceinline__ void slab_level(SlabRegs<C>& S, const SlabArgs& a, const SlabUnit& u,
+                                           int q, const FoldCoef<T>& f, T ar31, uint64_t seed) {
   using V2 = typename C::V2;
   using AX = typename C::AX;
   constexpr int TL = C::TL, NC = C::NC, OR = C::OR;
@@ -125,13 +178,51 @@ __device__ __forceinline__ void slab_level(typename C::V2 (&R)[C::TL][3][C::NC],
   const bool mout = u.edge && (gM < 0 || gM >= Lg[AX::M]);
   const T bu = (T)gs::bc_u(a.t + L);
   const int64_t step = a.t + (L - 1);
-  gs::U4 blk{0, 0, 0, 0};
+  // noise words of this level's cells
+  uint32_t wq[C::NOISE ? NC : 1];
+  if constexpr (C::NOISE) {
+    if constexpr (OR == 0) {
+      // y along the lanes: one draw per four cells, exchanged across the lane quad
+      const int64_t gy = gwrap_t<C::PER>(u.gA, g.Ly), gz = gwrap_t<C::PER>(gM, g.Lz);
+#pragma unroll
+      for (int j0 = L; j0 < NC - L; j0 += 4) {
+        const int jr = min(j0 + u.qr, NC - L - 1);  // this lane's cell of the group
+        const gs::U4 W = slab_block<C>(g, gwrap_t<C::PER>(u.gN0 + jr, g.Lx), gy, gz, step, seed, S.kv);
+        uint32_t X[4];
+        quad_transpose(u.qm1, u.qm2, W, X);
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (j0 + c < NC - L) wq[j0 + c] = X[c];
+      }
+    } else if constexpr (OR == 1) {
+      // y along N: the cells of one y-quad share a block (wave-uniform refresh)
+      const int64_t gx = gwrap_t<C::PER>(u.gA, g.Lx), gz = gwrap_t<C::PER>(gM, g.Lz);
+      gs::U4 blk{0, 0, 0, 0};
+#pragma unroll
+      for (int j = L; j < NC - L; ++j) {
+        const int64_t gy = gwrap_t<C::PER>(u.gN0 + j, g.Ly);
+        if (j == L || (gy & 3) == 0) blk = slab_block<C>(g, gx, gy, gz, step, seed, S.kv);
+        wq[j] = word_of(blk, (int)(gy & 3));
+      }
+    } else {
+      // y along the march: a cell's block serves four consecutive planes; refreshed at the
+      // level's first plane and at every y-quad start (wave-uniform)
+      const int64_t gx = gwrap_t<C::PER>(u.gA, g.Lx), gy = gwrap_t<C::PER>(gM, g.Ly);
+      const bool refresh = (gy & 3) == 0 || q == u.mc0 - (TL - L);
+      const int wi = (int)(gy & 3);
+#pragma unroll
+      for (int j = L; j < NC - L; ++j) {
+        if (refresh) S.PC[L][j] = slab_block<C>(g, gx, gy, gwrap_t<C::PER>(u.gN0 + j, g.Lz), step, seed, S.kv);
+        wq[j] = word_of(S.PC[L][j], wi);
+      }
+    }
+  }
 #pragma unroll
   for (int j = L; j < NC - L; ++j) {
-    const V2 c = R[L - 1][IC][j];
-    const V2 nm = R[L - 1][IC][j - 1], np = R[L - 1][IC][j + 1];  // N neighbours
-    const V2 mm = R[L - 1][IM][j], mp = R[L - 1][IP][j];          // M neighbours
-    const V2 lm = V2{lane_from_left(c.x), lane_from_left(c.y)};    // A neighbours
+    const V2 c = S.R[L - 1][IC][j];
+    const V2 nm = S.R[L - 1][IC][j - 1], np = S.R[L - 1][IC][j + 1];  // N neighbours
+    const V2 mm = S.R[L - 1][IM][j], mp = S.R[L - 1][IP][j];          // M neighbours
+    const V2 lm = V2{lane_from_left(c.x), lane_from_left(c.y)};      // A neighbours
     const V2 lp = V2{lane_from_right(c.x), lane_from_right(c.y)};
     V2 sum;
     if constexpr (OR == 0) sum = slab_sum<T>(nm, np, lm, lp, mm, mp);       // X=N Y=A Z=M
@@ -142,63 +233,58 @@ __device__ __forceinline__ void slab_level(typename C::V2 (&R)[C::TL][3][C::NC],
     V2 P = __builtin_elementwise_fma(f.kd, uvv, f.kc);
     P = __builtin_elementwise_fma(f.ks, sum, P);
     P = __builtin_elementwise_fma(f.kcc, c, P);
-    if constexpr (C::NOISE) {
-      // orientation 1 runs y along N: the cells of one y-quad share a Philox block (the
-      // refresh test is wave-uniform); elsewhere each cell draws its own block
-      bool refresh = true;
-      if constexpr (OR == 1) {
-        const int64_t gy = gwrap_t<C::PER>(u.gN0 + j, g.Ly);
-        refresh = j == L || (gy & 3) == 0;
-      }
-      const uint32_t w = slab_word<C, T>(u, g, j, gM, step, seed, blk, refresh);
-      P.x = fma(ar31, (T)(int32_t)w, P.x);
-    }
+    if constexpr (C::NOISE) P.x = fma(ar31, (T)(int32_t)wq[j], P.x);
     if constexpr (L < TL) {
-      if (u.edge) {
-        const int64_t gN = u.gN0 + j;
-        if (u.aout || mout || gN < 0 || gN >= Lg[AX::N]) P = V2{bu, (T)0};
-      }
-      R[L][IC][j] = P;
+      // outside the global domain: the boundary value of this time level (a select; the
+      // cell / plane tests are wave-uniform)
+      const int64_t gN = u.gN0 + j;
+      const bool out = mout || gN < 0 || gN >= Lg[AX::N];
+      const bool rst = u.edge && (out || u.aout);
+      S.R[L][IC][j] = rst ? V2{bu, (T)0} : P;
     } else {
-      // outputs: cells [TL, 2TL) of planes [mc0, mc1), lanes of the tile's output range
-      if (j >= TL && j < 2 * TL && q >= u.mc0 && q < u.mc1 && u.store)
-        d[u.base + (int64_t)j * u.sN + (int64_t)q * u.sM] = P;
+      // outputs: cells [TL, 2TL) of planes [mc0, mc1); lanes outside the tile's outputs
+      // store to an out-of-range offset (dropped)
+      const int off = (q >= u.mc0 && q < u.mc1) ? u.svoff : (int)0x80000000;
+      bstore(u.dst, off + (j * u.sNb + (q - u.pstart) * u.sMb), P);
     }
   }
 }
 
 // one march iteration p (ring index I = (p - pstart) mod 3): level 0 of plane p from the
-// prefetch, the prefetch of plane p + 1, then levels 1..TL bottom-up
+// prefetch queue, the prefetch of plane p + PF, then levels 1..TL bottom-up
 template <class C, typename T, int I, int L = 1>
-__device__ __forceinline__ void slab_levels(typename C::V2 (&R)[C::TL][3][C::NC],
-                                            typename C::V2* __restrict__ d, const SlabArgs& a,
-                                            const SlabUnit& u, int p, const FoldCoef<T>& f,
-                                            T ar31, uint64_t seed) {
+__device__ __forceinline__ void slab_levels(SlabRegs<C>& S, const SlabArgs& a, const SlabUnit& u,
+                                            int p, const FoldCoef<T>& f, T ar31, uint64_t seed) {
   if constexpr (L <= C::TL) {
     const int q = p - L;
     // level L is needed on planes [mc0 - (TL - L), mc1 + (TL - L)) (the outputs' cone)
     if (q >= u.mc0 - (C::TL - L) && q < u.mc1 + (C::TL - L))
-      slab_level<C, T, L, (I - L + 5) % 3, (I - L + 6) % 3, (I - L + 7) % 3>(R, d, a, u, q, f,
+      slab_level<C, T, L, (I - L + 5) % 3, (I - L + 6) % 3, (I - L + 7) % 3>(S, a, u, q, f,
                                                                                ar31, seed);
-    slab_levels<C, T, I, L + 1>(R, d, a, u, p, f, ar31, seed);
+    slab_levels<C, T, I, L + 1>(S, a, u, p, f, ar31, seed);
   }
 }
 
+template <class C>
+__device__ __forceinline__ void slab_load(SlabRegs<C>& S, const SlabUnit& u, int slot, int p,
+                                          int pend) {
+  // planes past the unit's range read through an empty offset (keeps the VMEM count fixed)
+  const int sp = p < pend ? (p - u.pstart) * u.sMb : 0;
+  const int vo = p < pend ? u.voff : (int)0x80000000;
+#pragma unroll
+  for (int j = 0; j < C::NC; ++j)
+    S.NX[slot][j] = bload(u.src, vo + (j * u.sNb + sp), (typename C::V2*)nullptr);
+}
+
 template <class C, typename T, int I>
-__device__ __forceinline__ bool slab_iter(typename C::V2 (&R)[C::TL][3][C::NC],
-                                          typename C::V2 (&NX)[C::NC],
-                                          const typename C::V2* __restrict__ s,
-                                          typename C::V2* __restrict__ d, const SlabArgs& a,
-                                          const SlabUnit& u, int& p, int pend,
-                                          const FoldCoef<T>& f, T ar31, uint64_t seed) {
+__device__ __forceinline__ bool slab_iter(SlabRegs<C>& S, const SlabArgs& a, const SlabUnit& u,
+                                          int& p, int pend, const FoldCoef<T>& f, T ar31,
+                                          uint64_t seed) {
   if (p >= pend) return false;
 #pragma unroll
-  for (int j = 0; j < C::NC; ++j) R[0][I][j] = NX[j];
-  if (p + 1 < pend) {
-#pragma unroll
-    for (int j = 0; j < C::NC; ++j) NX[j] = s[u.base + (int64_t)j * u.sN + (int64_t)(p + 1) * u.sM];
-  }
-  slab_levels<C, T, I>(R, d, a, u, p, f, ar31, seed);
+  for (int j = 0; j < C::NC; ++j) S.R[0][I][j] = S.NX[I][j];
+  slab_load<C>(S, u, I, p + C::PF, pend);
+  slab_levels<C, T, I>(S, a, u, p, f, ar31, seed);
   ++p;
   return true;
 }
@@ -211,6 +297,7 @@ __device__ __forceinline__ void slab_unit(const typename C::V2* __restrict__ s,
   using V2 = typename C::V2;
   using AX = typename C::AX;
   constexpr int TL = C::TL, NC = C::NC;
+  static_assert(C::PF == 3, "the prefetch queue is indexed by the ring slot");
   const Geom& g = a.g;
   const int lane = threadIdx.x & 63;
   const int tile = unit / F.nchunk, chunk = unit % F.nchunk;
@@ -222,21 +309,34 @@ __device__ __forceinline__ void slab_unit(const typename C::V2* __restrict__ s,
   const int64_t org[3] = {g.ox, g.oy, g.oz};
   const int64_t Lg[3] = {g.Lx, g.Ly, g.Lz};
   const int64_t str[3] = {1, g.px, (int64_t)g.px * g.py};
-  // this lane's A coordinate; outputs: lanes [TL, 64 - TL) of the tile, clipped to [a0, a1)
-  const int A0 = F.a0 - TL + tile * (64 - 2 * TL);
+  // this lane's A coordinate; the tile owns outputs [o, o + astep) (within lanes [TL, 64-TL))
+  const int A0 = F.abase + tile * F.astep;
   const int ca = A0 + lane;
-  u.store = lane >= TL && lane < 64 - TL && ca >= F.a0 && ca < F.a1;
+  const int o = F.a0 + tile * F.astep;
+  const bool store = ca >= o && ca < o + F.astep && ca < F.a1;
+  u.qr = lane & 3;
+  u.qm1 = (lane & 1) ? 0xFFFFFFFFu : 0u;
+  u.qm2 = (lane & 2) ? 0xFFFFFFFFu : 0u;
   const int cac = clampi(ca, -g.H, ext[AX::A] + g.H - 1);  // loads stay inside the allocation
   const int nb = F.n0 - TL;  // N coordinate of level-0 cell 0
+  u.pstart = u.mc0 - TL;
+  // descriptors based at (A = -H, N = nb, M = pstart); lane / cell / plane offsets in bytes
+  int64_t e0;
   {
     int c[3];
-    c[AX::A] = cac;
+    c[AX::A] = -g.H;
     c[AX::N] = nb;
-    c[AX::M] = 0;
-    u.base = gs::lin(g, c[0], c[1], c[2]);
+    c[AX::M] = u.pstart;
+    e0 = gs::lin(g, c[0], c[1], c[2]);
   }
-  u.sN = str[AX::N];
-  u.sM = str[AX::M];
+  const int64_t left = (gs::total_elems(g) - e0) * (int64_t)sizeof(V2);
+  const int range = (int)(left < 0x7ffffff0LL ? left : 0x7ffffff0LL);
+  u.src = plane_rsrc((const char*)(s + e0), range);
+  u.dst = plane_rsrc((const char*)(d + e0), range);
+  u.voff = (int)((int64_t)(cac + g.H) * str[AX::A] * (int64_t)sizeof(V2));
+  u.svoff = store ? u.voff : (int)0x80000000;
+  u.sNb = (int)(str[AX::N] * (int64_t)sizeof(V2));
+  u.sMb = (int)(str[AX::M] * (int64_t)sizeof(V2));
   u.gA = org[AX::A] + ca;
   u.gN0 = org[AX::N] + nb;
   u.gM0 = org[AX::M];
@@ -245,16 +345,23 @@ __device__ __forceinline__ void slab_unit(const typename C::V2* __restrict__ s,
                        u.gN0 < 0 || u.gN0 + NC > Lg[AX::N] ||
                        u.gM0 + u.mc0 - TL < 0 || u.gM0 + u.mc1 + TL > Lg[AX::M]);
   u.aout = u.edge && (u.gA < 0 || u.gA >= Lg[AX::A]);
-  // a wave-uniform copy of the noise coefficient in a VGPR (as k_fused)
-  V2 R[TL][3][NC];
-  V2 NX[NC];
-  int p = u.mc0 - TL;
+  SlabRegs<C> S;
+  if constexpr (C::NOISE && C::Q32) {
+#pragma unroll
+    for (int r = 3; r < 10; ++r) {
+      const uint32_t k0 = (uint32_t)seed + (uint32_t)r * kPhW0;
+      const uint32_t k1 = (uint32_t)(seed >> 32) + (uint32_t)r * kPhW1;
+      asm volatile("v_mov_b32 %0, %1" : "=v"(S.kv[2 * (r - 3)]) : "s"(k0));
+      asm volatile("v_mov_b32 %0, %1" : "=v"(S.kv[2 * (r - 3) + 1]) : "s"(k1));
+    }
+  }
+  int p = u.pstart;
   const int pend = u.mc1 + TL;
 #pragma unroll
-  for (int j = 0; j < NC; ++j) NX[j] = s[u.base + (int64_t)j * u.sN + (int64_t)p * u.sM];
-  while (slab_iter<C, T, 0>(R, NX, s, d, a, u, p, pend, f, ar31, seed) &&
-         slab_iter<C, T, 1>(R, NX, s, d, a, u, p, pend, f, ar31, seed) &&
-         slab_iter<C, T, 2>(R, NX, s, d, a, u, p, pend, f, ar31, seed)) {
+  for (int k = 0; k < C::PF; ++k) slab_load<C>(S, u, k, p + k, pend);
+  while (slab_iter<C, T, 0>(S, a, u, p, pend, f, ar31, seed) &&
+         slab_iter<C, T, 1>(S, a, u, p, pend, f, ar31, seed) &&
+         slab_iter<C, T, 2>(S, a, u, p, pend, f, ar31, seed)) {
   }
 }
 
@@ -319,7 +426,12 @@ void launch_slabs_tl(const void* s, void* d, const Geom& g, const gs::Params& p,
                       : (per ? slab_occupancy<T, TL, true, true, false>()
                              : slab_occupancy<T, TL, false, true, false>());
   const int64_t slots = (int64_t)occ * 4 * cus;  // resident waves
-  // march chunk: minimise rounds x (chunk + 2 TL pipeline fill) over the resident wave slots
+  // March chunk c.  A wave's work is W(c) = sum_L (c + 2 (TL - L)) (3 TL - 2 L) cell updates
+  // (its outputs' cone: the fill costs 2 (TL - L) extra planes per level); waves are VALU-bound,
+  // so co-resident waves share their SIMD: the time is ~ ceil(waves / SIMDs) x W(c).  Short
+  // chunks drown in fill work, long ones leave SIMDs idle (one-sided 256^3, T=3: c = 4).
+  (void)slots;
+  const int64_t simds = 4LL * cus;
   int chunk = 1;
   int64_t best = INT64_MAX;
   for (int c = 1; c <= 64; ++c) {
@@ -327,10 +439,12 @@ void launch_slabs_tl(const void* s, void* d, const Geom& g, const gs::Params& p,
     for (int i = 0; i < nspec; ++i) {
       const int m = spec[i].m1 - spec[i].m0, an = spec[i].a1 - spec[i].a0;
       if (m <= 0 || an <= 0) continue;
-      waves += (int64_t)((an + (64 - 2 * TL) - 1) / (64 - 2 * TL)) * ((m + c - 1) / c);
+      const int astep = spec[i].orient == 0 ? 52 : 64 - 2 * TL;
+      waves += (int64_t)((an + astep - 1) / astep) * ((m + c - 1) / c);
     }
-    const int64_t rounds = (waves + slots - 1) / slots;
-    const int64_t cost = rounds * (c + 2 * TL);
+    int64_t w = 0;
+    for (int L = 1; L <= TL; ++L) w += (int64_t)(c + 2 * (TL - L)) * (3 * TL - 2 * L);
+    const int64_t cost = ((waves + simds - 1) / simds) * w;
     if (cost < best) { best = cost; chunk = c; }
   }
   int u0 = 0;
@@ -342,7 +456,16 @@ void launch_slabs_tl(const void* s, void* d, const Geom& g, const gs::Params& p,
     F.n0 = spec[i].n0;
     F.a0 = spec[i].a0; F.a1 = spec[i].a1;
     F.m0 = spec[i].m0; F.m1 = spec[i].m1;
-    F.ntile = (an + (64 - 2 * TL) - 1) / (64 - 2 * TL);
+    if (F.orient == 0) {
+      // lanes along y: tiles start on a global y-quad (the noise draw shares one block per
+      // quad across lanes) and step by 52, so the owned outputs stay in lanes [TL, 64 - TL)
+      F.abase = (F.a0 - TL) - mod4(g.oy + F.a0 - TL);
+      F.astep = 52;
+    } else {
+      F.abase = F.a0 - TL;
+      F.astep = 64 - 2 * TL;
+    }
+    F.ntile = (an + F.astep - 1) / F.astep;
     F.chunk = chunk;
     F.nchunk = (m + chunk - 1) / chunk;
     F.u0 = u0;
