@@ -475,8 +475,8 @@ class HipBackend final : public gs::Backend {
   // (hipIpcOpenMemHandle) after checking that its device can reach theirs
   // (hipDeviceCanAccessPeer).  Exchange n:
   //   pack:   one launch that stores every message straight into the receiving peer's
-  //           landing slot n&1 (over xGMI), each wave ending with a system-scope release fence
-  //           (its stores are acknowledged before the wave retires)
+  //           landing slot n&1 (over xGMI); each wave waits for its stores to be acknowledged
+  //           before it retires (the landing buffer is uncached: no L2 line holds them)
   //   unpack: one single-wave launch: ready_P[me] = n for each send peer P (system-scope
   //           release), then wait for ready[P] >= n for each receive peer P (system-scope
   //           acquire) -> unpack from my slot n&1
@@ -855,12 +855,7 @@ class HipBackend final : public gs::Backend {
     int p2p;         // 1: this device can access the peer's (checked), -1: unknown
   };
   bool ipc_ = false;
-#ifdef GS_ABLATION
-  // timing experiment only: drop the packs' system-scope release (profiles/r3_ipc_fence.txt)
-  bool ipc_fence_ = !(getenv("GS_IPC_NOFENCE") && atoi(getenv("GS_IPC_NOFENCE")) != 0);
-#else
   static constexpr bool ipc_fence_ = true;
-#endif
   int ipc_nranks_ = 0;
   int* ipc_dflag_ = nullptr;  // device copy of the timeout word (unpacks write NaN once set)
   V2* landing_ = nullptr;

@@ -120,8 +120,12 @@ struct PackArgs {
   // per thread: the grid is sized by the messages' cells, not (largest message) x (count)
   int32_t b0[gs::kMaxMsgs + 1];
   int32_t n;
-  // PACK into peer memory (IPC): every wave ends with a system-scope release, so its stores
-  // to the peer's landing buffer are acknowledged before the ready flag can be published
+  // PACK into peer memory (IPC): every wave waits for its stores to the peer's landing buffer
+  // to be acknowledged before it ends (s_waitcnt 0), so they are complete before the ready flag
+  // can be published.  Not a system-scope fence: the landing buffer is uncached, so no L2
+  // line holds them, while __threadfence_system() writes back every XCD's dirty L2 lines --
+  // the fused kernel's output -- once per wave (+80 us per exchange on the loopback,
+  // profiles/r3_ipc_fence.txt)
   int32_t fence;
   // unpack from a landing buffer (IPC): a nonzero device word (a timed-out wait) makes the
   // unpack write NaN ghosts instead of the stale landing data
@@ -172,7 +176,7 @@ __global__ __launch_bounds__(256) void k_pack(typename Vec2<T>::type* __restrict
       else f[jj[k]] = c[k];
     }
   }
-  if (PACK && a.fence) __threadfence_system();
+  if (PACK && a.fence) __builtin_amdgcn_s_waitcnt(0);
 }
 
 // msgs[i]'s packed cells live at ptrs[i] (any mix of local and peer-mapped buffers)
@@ -209,8 +213,8 @@ void launch_pack(typename Vec2<T>::type* f, typename Vec2<T>::type* buf, const G
 // ------------------------------------------------------------------------------------------
 // IPC peer-write transport: sequence flags in uncached (fine-grained) memory shared between the
 // ranks of a node.  The signal-wait kernel publishes one sequence number per peer flag with
-// system-scope release stores (vector stores; the pack kernel before it on the stream ended
-// every wave with a system-scope release of its peer stores, k_pack `fence`), then polls up to
+// system-scope release stores (vector stores; every wave of the pack kernel before it on the
+// stream waited for its uncached peer stores to be acknowledged, k_pack `fence`), then polls up to
 // kMaxMsgs flags until each reaches its target (system-scope acquire loads, one lane per flag)
 // or until `ticks` of the 100 MHz wall clock have passed -- then it reports through a
 // host-mapped word (the watchdog) and a device word (the following unpack writes NaN) and

@@ -97,14 +97,16 @@ def candidates(L: int, nprocs: int, backend: str) -> List[Tuple]:
     # the reference's Dims_create grid first: it is always timed (bench.py reports it as
     # ``reference_grid``), then the z slabs (overlapped and not: the overlap's split launches
     # cost more than they hide unless the exchange is slow), then the variants.  Fuse depth 2
-    # never won a row at L=512 (profiles/r3_rehearsal_pre.txt, round-2 tables): the default
-    # depth only.
+    # never won a z-slab row at L=512 (profiles/r3_rehearsal_pre.txt, round-2 tables); on the
+    # balanced grid it halves the overlapped pass's face-slab shell (11 vs 28 us per pass for a
+    # 256^3 rank, profiles/r3_overlap_split.txt), so it is timed there.
     add(bal, 0)
     if backend == "hip" and L // nprocs >= 8:
         add(z, 0)
         add(z, 0, "off")
     if backend == "hip":
         add(bal, 0, "off")
+        add(bal, 2)
         # z slabs split once along y: half the z-plane bytes per link of the plain slabs, full
         # 64-lane x tiles, and only one face slab (y) outside the overlap
         if nprocs >= 4 and nprocs % 2 == 0 and L // (nprocs // 2) >= 8:
@@ -117,6 +119,7 @@ def candidates(L: int, nprocs: int, backend: str) -> List[Tuple]:
                 out.append((list(z), 0, "off", {}, "ipc"))
             out.append((list(bal), 0, "auto", {}, "ipc"))
             out.append((list(bal), 0, "off", {}, "ipc"))
+            out.append((list(bal), 2, "auto", {}, "ipc"))
     return out
 
 

@@ -65,9 +65,11 @@ def main():
                     rc = lib.gs_fused_runs_raw(h, k, 0, nz, 0, 0, 0, 0)
                 elif kind == "inner":
                     rc = lib.gs_fused_runs_raw(h, k, z0, z1 - z0, 0, 0, sides & 15, 1)
-                else:
+                elif kind == "shell":
                     rc = lib.gs_shell_raw(h, k, sides, -1)
-                native.check(lib, rc, kind)
+                else:  # ("faces", subset of sides, variant)
+                    rc = lib.gs_shell_raw(h, k, kind[1], kind[2])
+                native.check(lib, rc, str(kind))
 
             def timed(*runs):
                 for _ in range(3):
@@ -88,7 +90,13 @@ def main():
             inner = timed(*ins)
             shell = timed(*shs)
             both = timed(*(ins + shs))
-            row = {"local": [a.L, a.L, nz], "k": k, "packed": a.packed,
+            # per face group: z slabs through k_slab (v0) or k_fused (v1), x and y slabs
+            faces = {}
+            for name, bits in (("z", sides & 48), ("x", sides & 3), ("y", sides & 12)):
+                if bits:
+                    for v in ((0, 1) if name == "z" else (0,)):
+                        faces[f"{name}_v{v}_us"] = round(timed(("faces", bits, v)), 1)
+            row = {"local": [a.L, a.L, nz], "k": k, "packed": a.packed, "faces": faces,
                    "one_sided": a.one_sided, "full_us": round(full, 1),
                    "inner_us": round(inner, 1), "shell_us": round(shell, 1),
                    "inner_plus_shell_us": round(both, 1),

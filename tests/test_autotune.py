@@ -52,11 +52,13 @@ def test_candidates_for_mi355x():
     # z slabs with and without overlap
     assert candidates(512, 8, "hip") == [([2, 2, 2], 0, "auto"), ([1, 1, 8], 0, "auto"),
                                         ([1, 1, 8], 0, "off"), ([2, 2, 2], 0, "off"),
+                                        ([2, 2, 2], 2, "auto"),
                                         ([1, 2, 4], 0, "auto"), ([1, 2, 4], 0, "off"),
                                         ([1, 1, 8], 0, "auto", {}, "ipc"),
                                         ([1, 1, 8], 0, "off", {}, "ipc"),
                                         ([2, 2, 2], 0, "auto", {}, "ipc"),
-                                        ([2, 2, 2], 0, "off", {}, "ipc")]
+                                        ([2, 2, 2], 0, "off", {}, "ipc"),
+                                        ([2, 2, 2], 2, "auto", {}, "ipc")]
     assert candidates(512, 1, "hip") == [([1, 1, 1], 0, "auto")]
 
 
