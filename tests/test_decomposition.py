@@ -148,3 +148,23 @@ def test_halo_poisoning(world, L, fuse, periodic, decomp):
     assert np.isfinite(un).all() and np.isfinite(vn).all()
     np.testing.assert_array_equal(un, u1)
     np.testing.assert_array_equal(vn, v1)
+
+
+@pytest.mark.parametrize("world,L", [(4, 20), (3, 17)])
+def test_random_init_is_decomposition_invariant(world, L):
+    """The benchmarks' random init is a function of the global cell (gs::random_init_cell):
+    N ranks start from -- and, 6 steps later, end at -- the same global state as one rank."""
+    from grayscott_amd.ops import reference as ref
+    cfg1 = _cfg(L, 0, 1, False)
+    cfg1["random_init"] = 99
+    u0, v0, _ = run_ranks(world, cfg1)
+    ru, rv = ref.random_fields((L, L, L), seed=99, dtype=np.float32)
+    np.testing.assert_array_equal(u0, ru)
+    np.testing.assert_array_equal(v0, rv)
+    cfg1["steps"] = 6
+    cfgn = _cfg(L, 6, 1, False)
+    cfgn["random_init"] = 99
+    u1, v1, _ = run_ranks(1, cfg1)
+    un, vn, _ = run_ranks(world, cfgn)
+    np.testing.assert_array_equal(un, u1)
+    np.testing.assert_array_equal(vn, v1)
