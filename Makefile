@@ -20,7 +20,11 @@ HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-parame
 
 CORE_SRC := csrc/cpu/backend_cpu.cpp csrc/io/bp4.cpp
 HIP_SRC  := csrc/hip/backend_hip.hip
+# the heavy template instantiations (fused kernel per precision, overlap shell) in their own
+# translation units, compiled in parallel (make -j)
+HIP_INST := $(wildcard csrc/hip/inst/*.hip)
 HDRS     := $(wildcard csrc/include/gs/*.h) $(wildcard csrc/hip/*.hpp)
+HIP_OBJ  := $(patsubst csrc/hip/%.hip,build/obj/%.o,$(HIP_SRC) $(HIP_INST))
 
 all: $(OUT)/libgs_core.so $(OUT)/libgs_hip.so
 
@@ -28,13 +32,17 @@ $(OUT)/libgs_core.so: $(CORE_SRC) $(HDRS)
 	@mkdir -p $(OUT)
 	$(CXX) $(CXXFLAGS) -fopenmp $(INC) -shared -o $@ $(CORE_SRC)
 
-$(OUT)/libgs_hip.so: $(HIP_SRC) $(HDRS)
-	@mkdir -p $(OUT)
-	$(HIPCC) $(HIPFLAGS) $(INC) -shared -o $@ $(HIP_SRC) -L$(ROCM)/lib -lrccl -Wl,-rpath,$(ROCM)/lib
+build/obj/%.o: csrc/hip/%.hip $(HDRS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) $(INC) -c -o $@ $<
 
-$(OUT)/libgs_hip_abl.so: $(HIP_SRC) $(HDRS)
+$(OUT)/libgs_hip.so: $(HIP_OBJ)
 	@mkdir -p $(OUT)
-	$(HIPCC) $(HIPFLAGS) -DGS_ABLATION $(INC) -shared -o $@ $(HIP_SRC) -L$(ROCM)/lib -lrccl -Wl,-rpath,$(ROCM)/lib
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(HIP_OBJ) -L$(ROCM)/lib -lrccl -Wl,-rpath,$(ROCM)/lib
+
+$(OUT)/libgs_hip_abl.so: $(HIP_SRC) $(HIP_INST) $(HDRS)
+	@mkdir -p $(OUT)
+	$(HIPCC) $(HIPFLAGS) -DGS_ABLATION $(INC) -shared -o $@ $(HIP_SRC) $(HIP_INST) -L$(ROCM)/lib -lrccl -Wl,-rpath,$(ROCM)/lib
 
 ablation: $(OUT)/libgs_hip_abl.so
 

@@ -20,6 +20,21 @@
 #include "gs/capi_impl.h"
 #include "kernels.hpp"
 
+// The fused kernel and the shell kernels are instantiated in their own translation units
+// (csrc/hip/inst/*.hip), compiled in parallel.
+namespace gsk {
+extern template bool launch_fused<float>(const Vec2<float>::type*, Vec2<float>::type*, const Geom&,
+                                         const gs::Params&, int, int64_t, hipStream_t, int, int,
+                                         int, int, int, int, int, int);
+extern template bool launch_fused<double>(const Vec2<double>::type*, Vec2<double>::type*,
+                                          const Geom&, const gs::Params&, int, int64_t,
+                                          hipStream_t, int, int, int, int, int, int, int, int);
+extern template bool launch_shell<float>(const void*, void*, const Geom&, const gs::Params&, int,
+                                         int64_t, int, int, hipStream_t);
+extern template bool launch_shell<double>(const void*, void*, const Geom&, const gs::Params&, int,
+                                          int64_t, int, int, hipStream_t);
+}  // namespace gsk
+
 #define HIP_CHECK(expr)                                                                   \
   do {                                                                                    \
     hipError_t _e = (expr);                                                               \

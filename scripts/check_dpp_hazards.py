@@ -25,23 +25,30 @@ import subprocess
 import sys
 import tempfile
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from fatbin import LLVM, code_objects  # noqa: E402
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LLVM = "/opt/rocm/lib/llvm/bin"
-TARGET = "hipv4-amdgcn-amd-amdhsa--gfx950"
 
 _INSN = re.compile(r"^\s+([a-z_0-9]+)\s*(.*?)\s*//\s*([0-9A-F]{12}):")
 _BRANCH = re.compile(r"^s_(c?branch\w*|call\w*)$")
 _VREG = re.compile(r"^v(\d+)$|^v\[(\d+):(\d+)\]$")
 
 
-def disassemble(lib: str) -> str:
+def disassemble(lib: str) -> list[str]:
+    """One disassembly per code object (addresses restart in each, so they are checked apart)."""
     with tempfile.TemporaryDirectory() as d:
-        fat, co = os.path.join(d, "fatbin"), os.path.join(d, "gfx950.co")
-        subprocess.run(["objcopy", f"--dump-section=.hip_fatbin={fat}", lib], check=True)
-        subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o",
-                        f"--input={fat}", f"--targets={TARGET}", f"--output={co}"], check=True)
-        return subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--mcpu=gfx950", co], check=True,
-                              capture_output=True, text=True).stdout
+        return [subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--mcpu=gfx950", co], check=True,
+                               capture_output=True, text=True).stdout
+                for co in code_objects(lib, d)]
+
+
+def check_all(texts: list[str]):
+    checked, problems = 0, []
+    for t in texts:
+        n, p = check(t)
+        checked, problems = checked + n, problems + p
+    return checked, problems
 
 
 def vregs(op: str):
@@ -125,7 +132,7 @@ def check(text: str):
 
 def main(argv):
     lib = argv[1] if len(argv) > 1 else os.path.join(ROOT, "grayscott_amd", "_lib", "libgs_hip.so")
-    checked, problems = check(disassemble(lib))
+    checked, problems = check_all(disassemble(lib))
     for p in problems[:50]:
         print("HAZARD", p)
     print(f"{os.path.basename(lib)}: {checked} DPP instructions checked, {len(problems)} hazard(s)")

@@ -15,19 +15,17 @@ import subprocess
 import sys
 import tempfile
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from fatbin import LLVM, code_objects  # noqa: E402
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LLVM = "/opt/rocm/lib/llvm/bin"
-TARGET = "hipv4-amdgcn-amd-amdhsa--gfx950"
 
 
 def notes(lib: str) -> str:
     with tempfile.TemporaryDirectory() as d:
-        fat, co = os.path.join(d, "fatbin"), os.path.join(d, "gfx950.co")
-        subprocess.run(["objcopy", f"--dump-section=.hip_fatbin={fat}", lib], check=True)
-        subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o",
-                        f"--input={fat}", f"--targets={TARGET}", f"--output={co}"], check=True)
-        return subprocess.run([f"{LLVM}/llvm-readelf", "--notes", co], check=True,
-                              capture_output=True, text=True).stdout
+        return "".join(subprocess.run([f"{LLVM}/llvm-readelf", "--notes", co], check=True,
+                                      capture_output=True, text=True).stdout
+                       for co in code_objects(lib, d))
 
 
 def kernels(text: str, everything: bool = False):

@@ -47,6 +47,6 @@ def test_built_library_has_no_dpp_hazard():
     lib = os.path.join(ROOT, "grayscott_amd", "_lib", "libgs_hip.so")
     if not os.path.exists(lib):
         pytest.skip("libgs_hip.so not built")
-    n, problems = chk.check(chk.disassemble(lib))
+    n, problems = chk.check_all(chk.disassemble(lib))
     assert n > 1000, n
     assert not problems, problems[:5]
