@@ -139,21 +139,19 @@ constexpr int kPackItems = 4;
 // consecutive cells per pass so a row's cells go to neighbouring lanes.  Sizing the grid by
 // the total cell count matters: one workgroup row per message at the largest message's size
 // launched ~20k mostly empty workgroups for a 256^3 rank and took ~10 us per pack / unpack.
+// one workgroup's kPackItems x 256 cells: workgroup `blk` of the prefix table
 template <typename T, bool PACK>
-__global__ __launch_bounds__(256) void k_pack(typename Vec2<T>::type* __restrict__ f,
-                                              Geom g, PackArgs a) {
+__device__ __forceinline__ void pack_block(typename Vec2<T>::type* __restrict__ f, const Geom& g,
+                                           const PackArgs& a, int blk, bool poison) {
   int m = 0;
-  while (m + 1 < a.n && (int)blockIdx.x >= a.b0[m + 1]) ++m;
+  while (m + 1 < a.n && blk >= a.b0[m + 1]) ++m;
   const Box b = a.box[m];
   typename Vec2<T>::type* __restrict__ p = (typename Vec2<T>::type*)a.ptr[m];
   // a message box holds < 2^31 cells (halo slabs of one sub-domain): 32-bit index math
   // (the 64-bit divisions dominated this kernel)
   const uint32_t n = (uint32_t)gs::box_cells(b);
   const uint32_t bnx = (uint32_t)b.nx, bny = (uint32_t)b.ny;
-  const uint32_t base = (uint32_t)(blockIdx.x - a.b0[m]) * (256u * kPackItems) + threadIdx.x;
-  // a timed-out IPC wait: poison the ghosts (wave-uniform load of a device word)
-  const bool poison = !PACK && a.err && __hip_atomic_load(a.err, __ATOMIC_RELAXED,
-                                                          __HIP_MEMORY_SCOPE_AGENT) != 0;
+  const uint32_t base = (uint32_t)(blk - a.b0[m]) * (256u * kPackItems) + threadIdx.x;
   // all loads first (kPackItems in flight per lane), then the stores
   typename Vec2<T>::type c[kPackItems];
   int64_t jj[kPackItems];
@@ -176,6 +174,15 @@ __global__ __launch_bounds__(256) void k_pack(typename Vec2<T>::type* __restrict
       else f[jj[k]] = c[k];
     }
   }
+}
+
+template <typename T, bool PACK>
+__global__ __launch_bounds__(256) void k_pack(typename Vec2<T>::type* __restrict__ f,
+                                              Geom g, PackArgs a) {
+  // a timed-out IPC wait: poison the ghosts (wave-uniform load of a device word)
+  const bool poison = !PACK && a.err && __hip_atomic_load(a.err, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT) != 0;
+  pack_block<T, PACK>(f, g, a, (int)blockIdx.x, poison);
   if (PACK && a.fence) __builtin_amdgcn_s_waitcnt(0);
 }
 
@@ -245,8 +252,8 @@ __device__ __forceinline__ void ipc_poll(const IpcFlags& a, uint64_t t0, uint64_
 // has one launch fewer); signalling first keeps two ranks waiting on each other deadlock-free
 //   min_ticks > 0 (GS_IPC_EMULATE_US, modelling only): the launch also lasts at least that long,
 //   so a one-GPU loopback run can stand in for a slower inter-GPU link when timing overlap
-[[maybe_unused]] static __global__ __launch_bounds__(64) void k_ipc_signal_wait(IpcFlags s, IpcFlags w, uint64_t ticks,
-                                                        int* err, int* dflag, uint64_t min_ticks) {
+[[maybe_unused]] static __global__ __launch_bounds__(64) void k_ipc_signal_wait(
+    IpcFlags s, IpcFlags w, uint64_t ticks, int* err, int* dflag, uint64_t min_ticks) {
   const int i = threadIdx.x;
   const uint64_t t0 = wall_clock64();
   if (i < s.n) __hip_atomic_store(s.f[i], s.want[i], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -60,7 +60,8 @@ def summarise(root):
             rows += list(csv.DictReader(fh))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     last = [r for r in rows if "k_fused" in r["Kernel_Name"] or "ccl" in r["Kernel_Name"].lower()
-            or "k_pack" in r["Kernel_Name"] or "k_ipc" in r["Kernel_Name"]][-24:]
+            or "k_pack" in r["Kernel_Name"] or "k_ipc" in r["Kernel_Name"]
+            or "k_slab" in r["Kernel_Name"]][-24:]
     t0 = int(last[0]["Start_Timestamp"])
     print(f"{'start_us':>9} {'end_us':>9} {'dur_us':>7} queue  kernel")
     for r in last:
