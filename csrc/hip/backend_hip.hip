@@ -407,13 +407,25 @@ class HipBackend final : public gs::Backend {
       int nt = 0;
       const gsk::FusedCfgEntry* tab = gsk::fused_cfg_table(&nt);
       const int dflt = sizeof(T) == 4 ? gsk::fused_cfg_lookup("4x12:2s") : gsk::fused_cfg_lookup("4x8:1s");
+      // the small-grid block kernel (k_block) serves whole-interior launches it supports only
+      gsk::FusedArgs fa{};
+      fa.g = g_;
+      fa.q32 = gsk::philox_q32(g_) ? 1 : 0;
+      fa.zlen[0] = pt.zlen0 < 0 ? g_.nz : pt.zlen0;
+      fa.zlo[0] = pt.zlo0;
+      fa.zlen[1] = pt.zlen1;
+      fa.mx1 = g_.nx;
+      fa.my1 = g_.ny;
+      fa.reserve = pt.reserve;
+      const bool blk_ok = pt.mask == 0 && gsk::block_supported(fa);
       for (int i = 0; i < nt; ++i)
-        if ((sizeof(T) == 4 ? tab[i].f32 : tab[i].f64) && i != dflt && !strstr(tab[i].name, "-abl"))
+        if ((sizeof(T) == 4 ? tab[i].f32 : tab[i].f64) && i != dflt && !strstr(tab[i].name, "-abl") &&
+            (blk_ok || !gsk::fused_cfg_is_block(i)))
           cfgs.push_back(i);
     }
     const int nsched = pt.zlen1 > 0 ? 1 : 3;  // two z-runs always use schedule 0
-    for (int c : cfgs)
-      for (int sc = 0; sc < nsched; ++sc) cands.push_back({c, sc});
+    for (int c : cfgs)  // (k_block has no work schedule)
+      for (int sc = 0; sc < (gsk::fused_cfg_is_block(c) ? 1 : nsched); ++sc) cands.push_back({c, sc});
     auto launch = [&](const Cand& c) {
       return gsk::launch_fused<T>(buf_[src], buf_[dst], g_, p_, n, t, stream_, c.cfg, c.sched,
                                   pt.zlo0, pt.zlen0, pt.zlo1, pt.zlen1, pt.reserve, pt.mask);
@@ -1041,6 +1053,17 @@ int gs_fused_sched(int32_t sched) {
   if (sched < 0 || sched > 2) return -1;
   gsk::fused_sched_slot() = sched;
   fused_pinned() = true;
+  return 0;
+}
+
+// Back to the autotuned choice (engines created afterwards tune again; tests that pinned a
+// configuration call this so later engines in the process are not affected).
+int gs_fused_unpin(void) {
+  gsk::fused_cfg_slot() = -1;
+  (void)gsk::fused_cfg_env();
+  gsk::fused_sched_slot() = -1;
+  (void)gsk::fused_sched_slot();
+  fused_pinned() = false;
   return 0;
 }
 

@@ -1,0 +1,188 @@
+// SPDX-License-Identifier: MIT
+// k_block: the fused T-step pass for SMALL grids, every time level of a block held in LDS.
+// Included inside namespace gsk by kernels.hpp, after fused.hpp (it shares fused.hpp's cell
+// update order, Philox stream and DPP sums, so its results are bit-identical to k_fused's and it
+// is simply one more candidate of the fused kernel's autotuner: fused_cfg_table "blk*").
+//
+// Why a second kernel: k_fused marches each tile along z through a 3T-1 iteration pipeline fill.
+// On the reference's example grid (L = 64, examples/settings-files.toml) a workgroup's chunk is
+// 1-2 planes, so a pass is that fill chain's latency (~1.3 us per iteration, profiles/
+// r3_small_grid.txt: 9.5 us per T=2 pass, 55k MLUPS) while the chip's VALU work is ~0.6 us.
+// Here a workgroup owns an output block of whole x rows x BY rows x BZ planes, loads the block's
+// level-0 input (BY+10 rows x BZ+2T planes, independent loads: one memory latency) into LDS,
+// computes the T levels from LDS into LDS (ping-pong buffers, one barrier per level; each wave
+// takes whole 4-row noise quads, so one Philox draw serves 4 cells as in k_fused), and writes
+// the last level straight to HBM.  The intermediate levels are recomputed on the block's halo
+// (the dependency cone), which costs 2-4x the useful cell updates -- cheap at this size, where
+// the chip is otherwise idle.
+//
+// Scope: x rows fit one wave (nx <= 64) and both x faces are the global (non-periodic)
+// boundary, so no x halo is computed: a level's x ghost is the boundary value of its time level
+// (engine.h ensure_bc for level 0, the k_fused reset rule for the others) and enters the
+// x-neighbour sum of lane 0 / lane 63 as an exact correction (below).  y / z faces may have
+// neighbours (their halos are H >= T deep, as for k_fused).
+//
+// The update computed is the reference's calculate! (Simulation_CPU.jl:92-112), T steps per pass.
+#pragma once
+
+struct BlockArgs {
+  Geom g;
+  int64_t t;
+  int32_t yb;   // local y of block row 0 (<= 0; (oy + yb) % 4 == 0: whole noise quads)
+  int32_t nby;  // blocks along y (grid = nby * ceil(nz / BZ))
+  int32_t gr;   // nx == 64: no lane holds the +x ghost; lane 63 adds it explicitly
+};
+
+template <typename T_, int TL_, int BY_, int BZ_, int NW_, bool NOISE_>
+struct BCfg {
+  using T = T_;
+  using V2 = typename PairT<T>::type;
+  static constexpr int TL = TL_, BY = BY_, BZ = BZ_, NW = NW_;
+  static constexpr bool NOISE = NOISE_;
+  // LDS rows: local y0-5 .. y0+BY+4 (intermediate levels compute the quads [y0-4, y0+BY+4) and
+  // read one row beyond); LDS planes z0-T .. z0+BZ+T-1
+  static constexpr int R0 = 5;
+  static constexpr int NR = BY + 10;
+  static constexpr int NP = BZ + 2 * TL;
+  static constexpr int LDS_BYTES = 2 * NP * NR * 64 * (int)sizeof(V2);
+  static_assert(BY % 4 == 0, "blocks hold whole noise quads");
+  static_assert(LDS_BYTES <= 160 * 1024, "two level buffers must fit the CU's LDS");
+};
+
+template <class C>
+__global__ __launch_bounds__(64 * C::NW, 1) void k_block(const typename C::V2* __restrict__ s,
+                                                       typename C::V2* __restrict__ d,
+                                                       BlockArgs a, FoldCoef<typename C::T> f,
+                                                       uint64_t seed) {
+  using T = typename C::T;
+  using V2 = typename C::V2;
+  constexpr int TL = C::TL, BY = C::BY, BZ = C::BZ, NW = C::NW, NR = C::NR, NP = C::NP;
+  __shared__ V2 buf[2][NP][NR][64];  // [level parity][plane][row][lane]
+  const Geom& g = a.g;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int by = blockIdx.x % a.nby, bz = blockIdx.x / a.nby;
+  const int y0 = a.yb + by * BY, z0 = bz * BZ;
+
+  // level 0.  Rows / planes outside the storage (beyond the H-deep ghosts) and lanes past the
+  // row's last ghost read 0: they only feed cells outside every stored output's cone.
+  for (int i = wave; i < NP * NR; i += NW) {
+    const int pz = i / NR, ry = i - pz * NR;
+    const int z = z0 - TL + pz, y = y0 - C::R0 + ry;
+    V2 v{(T)0, (T)0};
+    if (z >= -g.H && z < g.nz + g.H && y >= -g.H && y < g.ny + g.H && lane < g.nx + g.H)
+      v = s[gs::lin(g, lane, y, z)];
+    buf[0][pz][ry][lane] = v;
+  }
+  // the first and last rows of the level-1 buffer are read (quad halo rows) but never computed
+  for (int pz = wave; pz < NP; pz += NW) {
+    buf[1][pz][0][lane] = V2{(T)0, (T)0};
+    buf[1][pz][NR - 1][lane] = V2{(T)0, (T)0};
+  }
+  V2 kc;
+  {
+    const T k0 = f.kc.x, k1 = f.kc.y;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(kc.x) : "s"(k0));
+    asm volatile("v_mov_b32 %0, %1" : "=v"(kc.y) : "s"(k1));
+  }
+  const T ar31 = f.ar * (T)4.656612873077392578125e-10;
+  const uint32_t Ly4 = (uint32_t)((g.Ly + 3) >> 2);
+  __syncthreads();
+
+#pragma unroll
+  for (int l = 0; l < TL; ++l) {
+    const V2(*in)[NR][64] = buf[l & 1];
+    V2(*out)[NR][64] = buf[(l + 1) & 1];
+    const bool last = l + 1 == TL;
+    const int mq = last ? 0 : 1;          // intermediate levels: one quad of halo each side
+    const int nq = BY / 4 + 2 * mq;
+    const int dz = TL - 1 - l;            // planes of halo this level still needs
+    const int npl = BZ + 2 * dz;
+    const uint64_t tstep = (uint64_t)(a.t + l);
+    // x ghosts of level l (the input): its boundary value.  Lane 0's left neighbour is added
+    // last in the sum (in[x-1] + (in[x+1] + yz)), so adding it after the DPP sum (where the
+    // missing lane read 0) is exact; lane 63's right neighbour is added first, so it goes into
+    // yz before the DPP sum.  Other lanes add +0.
+    const T bin = (T)gs::bc_u(a.t + l);
+    const V2 gl = lane == 0 ? V2{bin, (T)0} : V2{(T)0, (T)0};
+    const V2 gr = (a.gr && lane == 63) ? V2{bin, (T)0} : V2{(T)0, (T)0};
+    const T bout = (T)gs::bc_u(a.t + l + 1);
+    for (int it = wave; it < nq * npl; it += NW) {
+      const int zi = it / nq, qi = it - zi * nq;
+      const int qy = y0 - 4 * mq + 4 * qi;  // local y of the quad's first row
+      const int z = z0 - dz + zi;
+      const int pz = z - (z0 - TL);
+      const int ry = qy - y0 + C::R0;
+      V2 row[6], pm[4], pp[4];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) row[k] = lds_load2(&in[pz][ry - 1 + k][lane]);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        pm[k] = lds_load2(&in[pz - 1][ry + k][lane]);
+        pp[k] = lds_load2(&in[pz + 1][ry + k][lane]);
+      }
+      const int64_t gz = g.oz + z;
+      gs::U4 blk{0, 0, 0, 0};
+      if constexpr (C::NOISE) {
+        // k_fused's counter: gx + Lx * (gy4 + Ly4 * gz) (fits 32 bits: host check)
+        const uint32_t gy4 = (uint32_t)((g.oy + qy) >> 2);
+        const uint32_t qu = (uint32_t)g.Lx * (gy4 + Ly4 * (uint32_t)gz);
+        blk = philox_dev<true>(qu + (uint32_t)(g.ox + lane), 0u, tstep, seed);
+      }
+      const bool zout = gz < 0 || gz >= g.Lz;
+      const bool xout = g.ox + lane >= g.Lx;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const V2 c = row[k + 1];
+        V2 yz = (row[k] + row[k + 2]) + pm[k];
+        if (a.gr) yz = yz + gr;
+        V2 A{lane_pair_sum_add<false>(c.x, yz.x), lane_pair_sum_add<false>(c.y, yz.y)};
+        A = A + gl;
+        const V2 sum = A + pp[k];
+        const V2 tt = c * c.yy;
+        const V2 uvv = tt.xx * c.yy;
+        V2 P = __builtin_elementwise_fma(f.kd, uvv, kc);
+        P = __builtin_elementwise_fma(f.ks, sum, P);
+        P = __builtin_elementwise_fma(f.kcc, c, P);
+        if constexpr (C::NOISE) {
+          const uint32_t w = k == 0 ? blk.x : (k == 1 ? blk.y : (k == 2 ? blk.z : blk.w));
+          P.x = fma(ar31, (T)(int32_t)w, P.x);
+        }
+        const int y = qy + k;
+        if (!last) {
+          const int64_t gy = g.oy + y;
+          if (zout || xout || gy < 0 || gy >= g.Ly) P = V2{bout, (T)0};
+          out[pz][ry + k][lane] = P;
+        } else if (lane < g.nx && y >= 0 && y < g.ny && z < g.nz) {
+          d[gs::lin(g, lane, y, z)] = P;
+        }
+      }
+    }
+    if (!last) __syncthreads();
+  }
+}
+
+template <class C>
+bool run_block(const void* s, void* d, const FusedArgs& a0, const gs::Params& p, hipStream_t st) {
+  const Geom& g = a0.g;
+  BlockArgs a{};
+  a.g = g;
+  a.t = a0.t;
+  a.yb = -mod4(g.oy);
+  a.nby = (g.ny - a.yb + C::BY - 1) / C::BY;
+  a.gr = g.nx == 64 ? 1 : 0;
+  const int nbz = (g.nz + C::BZ - 1) / C::BZ;
+  const FoldCoef<typename C::T> f = make_fold<typename C::T>(p);
+  k_block<C><<<(unsigned)(a.nby * nbz), 64 * C::NW, 0, st>>>(
+      (const typename C::V2*)s, (typename C::V2*)d, a, f, p.seed);
+  return true;
+}
+
+// whether k_block can run this launch: the whole interior (no z-runs / store mask / reserve),
+// whole non-periodic x rows of at most 64 cells, a 32-bit Philox counter
+inline bool block_supported(const FusedArgs& a) {
+  const Geom& g = a.g;
+  return !g.periodic && g.nx <= 64 && g.ox == 0 && g.nx == g.Lx && a.q32 && a.zlo[0] == 0 &&
+         a.zlen[0] == g.nz && a.zlen[1] == 0 && a.mx0 == 0 && a.mx1 == g.nx && a.my0 == 0 &&
+         a.my1 == g.ny && a.reserve == 0;
+}

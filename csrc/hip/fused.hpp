@@ -746,6 +746,8 @@ struct FusedLaunch {
   }
 };
 
+#include "block.hpp"
+
 // Work-schedule override: GS_FUSED_SCHED at load time or gs_fused_sched() at run time.
 inline int& fused_sched_slot() {
   static int v = -1;
@@ -787,21 +789,34 @@ inline const FusedCfgEntry* fused_cfg_table(int* n) {
       {"4x4:2", false, true},    // 17
       {"4x16:1", true, false},   // 18
       {"4x16:1s", true, false},  // 19  64-row tile, 4 waves per SIMD (fits 128 VGPRs)
+      // small grids (block.hpp): k_block, output blocks of whole x rows x BY rows x BZ planes,
+      // NW waves; timed only on launches it supports (block_supported), else the default shape
+      {"blk8x2w8", true, false},  // 20
+      {"blk4x2w4", true, false},  // 21
+      {"blk8x1w8", true, false},  // 22
+      {"blk4x4w8", true, false},  // 23
+      {"blk4x1w4", true, false},  // 24
 #ifdef GS_ABLATION
-      {"4x12:2s-abl1", true, false},  // 20  no barriers
-      {"4x12:2s-abl2", true, false},  // 21  L2-resident loads
-      {"4x12:1s-abl4", true, false},  // 22  Philox keys in VGPRs (exact)
-      {"4x12:2s-abl4", true, false},  // 23  Philox keys in VGPRs (exact)
-      {"4x12:1s-abl8", true, false},  // 24  DPP sums with the s_nop (exact)
-      {"4x12:1s-abl12", true, false}, // 25  abl4 + abl8 (exact)
-      {"4x12:1s-abl16", true, false}, // 26  pipeline fill computes every level (exact)
-      {"4x8:1s-abl16", true, true},   // 27  pipeline fill computes every level (exact)
-      {"4x6:2s-abl16", true, true},   // 28  pipeline fill computes every level (exact)
-      {"4x12:1s-abl32", true, false}, // 29  Philox only on lanes in the x cone (exact)
+      {"4x12:2s-abl1", true, false},  // 25  no barriers
+      {"4x12:2s-abl2", true, false},  // 26  L2-resident loads
+      {"4x12:1s-abl4", true, false},  // 27  Philox keys in VGPRs (exact)
+      {"4x12:2s-abl4", true, false},  // 28  Philox keys in VGPRs (exact)
+      {"4x12:1s-abl8", true, false},  // 29  DPP sums with the s_nop (exact)
+      {"4x12:1s-abl12", true, false}, // 30  abl4 + abl8 (exact)
+      {"4x12:1s-abl16", true, false}, // 31  pipeline fill computes every level (exact)
+      {"4x8:1s-abl16", true, true},   // 32  pipeline fill computes every level (exact)
+      {"4x6:2s-abl16", true, true},   // 33  pipeline fill computes every level (exact)
+      {"4x12:1s-abl32", true, false}, // 34  Philox only on lanes in the x cone (exact)
 #endif
   };
   *n = (int)(sizeof(t) / sizeof(t[0]));
   return t;
+}
+
+inline bool fused_cfg_is_block(int i) {
+  int n = 0;
+  const FusedCfgEntry* t = fused_cfg_table(&n);
+  return i > 0 && i < n && !strncmp(t[i].name, "blk", 3);
 }
 
 inline int& fused_cfg_slot() {
@@ -841,8 +856,8 @@ void run_fused_cfg(const void* s, void* d, const FusedArgs& a, const gs::Params&
       case 16: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
       case 17: FusedLaunch<FCfg<T, TL, 4, 4, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
 #ifdef GS_ABLATION
-      case 27: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
-      case 28: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 32: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 33: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
 #endif
       default: break;
     }
@@ -865,17 +880,22 @@ void run_fused_cfg(const void* s, void* d, const FusedArgs& a, const gs::Params&
       case 15: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true>, T>::run(s, d, a, p, st); return;
       case 18: FusedLaunch<FCfg<T, TL, 4, 16, 1, PER, NZ>, T>::run(s, d, a, p, st); return;
       case 19: FusedLaunch<FCfg<T, TL, 4, 16, 1, PER, NZ, true>, T>::run(s, d, a, p, st); return;
+      case 20: if (block_supported(a)) { run_block<BCfg<T, TL, 8, 2, 8, NZ>>(s, d, a, p, st); return; } break;
+      case 21: if (block_supported(a)) { run_block<BCfg<T, TL, 4, 2, 4, NZ>>(s, d, a, p, st); return; } break;
+      case 22: if (block_supported(a)) { run_block<BCfg<T, TL, 8, 1, 8, NZ>>(s, d, a, p, st); return; } break;
+      case 23: if (block_supported(a)) { run_block<BCfg<T, TL, 4, 4, 8, NZ>>(s, d, a, p, st); return; } break;
+      case 24: if (block_supported(a)) { run_block<BCfg<T, TL, 4, 1, 4, NZ>>(s, d, a, p, st); return; } break;
 #ifdef GS_ABLATION
-      case 20: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 1>, T>::run(s, d, a, p, st); return;
-      case 21: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 2>, T>::run(s, d, a, p, st); return;
-      case 22: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;
-      case 23: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;
-      case 24: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 8>, T>::run(s, d, a, p, st); return;
-      case 25: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 12>, T>::run(s, d, a, p, st); return;
-      case 26: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
-      case 27: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
-      case 28: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
-      case 29: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 32>, T>::run(s, d, a, p, st); return;
+      case 25: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 1>, T>::run(s, d, a, p, st); return;
+      case 26: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 2>, T>::run(s, d, a, p, st); return;
+      case 27: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;
+      case 28: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;
+      case 29: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 8>, T>::run(s, d, a, p, st); return;
+      case 30: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 12>, T>::run(s, d, a, p, st); return;
+      case 31: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 32: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 33: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 34: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 32>, T>::run(s, d, a, p, st); return;
 #endif
       default: break;  // 0 and 14: the default shape below
     }

@@ -417,6 +417,14 @@ def fused_sched(sched: int) -> None:
         raise ValueError(f"unknown schedule {sched}")
 
 
+def fused_unpin() -> None:
+    """Undo fused_select / fused_sched: engines created afterwards use the autotuner again."""
+    lib = load("hip")
+    lib.gs_fused_unpin.argtypes = []
+    lib.gs_fused_unpin.restype = c_int
+    lib.gs_fused_unpin()
+
+
 def fused_cfg_lookup(name: str) -> int:
     """Index of fused-kernel configuration ``name`` in the loaded HIP library, -1 if this build
     does not have it (the ablation variants exist only in ``make ablation`` builds)."""

@@ -1,0 +1,100 @@
+"""The small-grid block kernel (csrc/hip/block.hpp, k_block) vs the z-marching fused kernel.
+
+k_block is one more candidate of the fused kernel's autotuner, so it must reproduce k_fused bit
+for bit: same neighbour-sum order, Philox stream, boundary resets.  Checked from the benchmarks'
+random init (rough data, every cell's noise draw matters) on grids where the x rows fill the
+wave exactly (L = 64, the +x ghost added on lane 63), partly (L = 36, 42: the ghost is a lane)
+and with rows that are not a multiple of the 4-row noise quads (L = 42), at both fuse depths; and
+against the CPU golden backend (the reference's update, Simulation_CPU.jl:92-112).
+"""
+import numpy as np
+import pytest
+import torch
+
+from grayscott_amd.models.grayscott import GrayScott
+from grayscott_amd.parallel.decomp import init_domain
+from grayscott_amd.utils.config import Settings
+
+pytestmark = pytest.mark.gpu
+
+BLOCKS = ["blk8x2w8", "blk4x2w4", "blk8x1w8", "blk4x4w8", "blk4x1w4"]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from grayscott_amd.ops import native
+    native.load("hip")
+    yield
+    native.fused_unpin()
+
+
+def _run(L, fuse, steps, cfg=None, backend="AMDGPU", random=True):
+    from grayscott_amd.ops import native
+    if backend == "AMDGPU":
+        if cfg is None:
+            native.fused_unpin()
+        else:
+            native.fused_select(cfg)
+    s = Settings(L=L, precision="Float32", F=0.02, k=0.048, dt=1.0, Du=0.2, Dv=0.1, noise=0.1,
+                 backend=backend, seed=19)
+    sim = GrayScott(s, init_domain(L, 1, 0), fuse=fuse)
+    try:
+        sim.init_fields()
+        if random:
+            sim.randomize_fields(seed=3)
+        sim.iterate(steps)
+        return sim.get_fields()
+    finally:
+        sim.close()
+
+
+@pytest.mark.parametrize("L", [64, 42, 36])
+@pytest.mark.parametrize("fuse", [2, 3])
+def test_block_kernel_bitwise_vs_fused(L, fuse):
+    steps = 4 * fuse + 1  # whole passes plus a remainder step
+    ref = _run(L, fuse, steps, cfg="4x8:1s")
+    for name in BLOCKS:
+        u, v = _run(L, fuse, steps, cfg=name)
+        np.testing.assert_array_equal(u, ref[0], err_msg=f"{name} u")
+        np.testing.assert_array_equal(v, ref[1], err_msg=f"{name} v")
+
+
+@pytest.mark.parametrize("fuse", [2, 3])
+def test_block_kernel_vs_cpu_golden(fuse):
+    g = _run(64, fuse, 30, cfg="blk8x2w8")
+    c = _run(64, 1, 30, backend="CPU")
+    assert np.abs(g[0] - c[0]).max() < 2e-5
+    assert np.abs(g[1] - c[1]).max() < 2e-5
+
+
+def test_block_kernel_from_seed_state():
+    # the reference's own initial state (u = 1, v = 0, 13^3 seed cube): smooth data, boundary
+    # values switching with the time parity
+    ref = _run(64, 3, 20, cfg="4x8:1s", random=False)
+    u, v = _run(64, 3, 20, cfg="blk4x4w8", random=False)
+    np.testing.assert_array_equal(u, ref[0])
+    np.testing.assert_array_equal(v, ref[1])
+
+
+def test_autotuner_times_block_kernel_at_l64():
+    """At L = 64 the tuner's candidate list includes the block kernels; whatever it picks must
+    reproduce the pinned k_fused result."""
+    from grayscott_amd.ops import native
+    native.fused_unpin()
+    s = Settings(L=64, precision="Float32", F=0.02, k=0.048, dt=1.0, Du=0.2, Dv=0.1, noise=0.1,
+                 backend="AMDGPU", seed=19)
+    sim = GrayScott(s, init_domain(64, 1, 0), fuse=2)
+    try:
+        sim.init_fields()
+        sim.randomize_fields(seed=3)
+        choice = sim.fused_choice()
+        sim.iterate(9)
+        got = sim.get_fields()
+    finally:
+        sim.close()
+    print("L=64 tuned choice:", choice)
+    ref = _run(64, 2, 9, cfg="4x8:1s")
+    np.testing.assert_array_equal(got[0], ref[0])
+    np.testing.assert_array_equal(got[1], ref[1])
