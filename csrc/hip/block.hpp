@@ -64,20 +64,25 @@ __global__ __launch_bounds__(64 * C::NW, 1) void k_block(const typename C::V2* _
   const int by = blockIdx.x % a.nby, bz = blockIdx.x / a.nby;
   const int y0 = a.yb + by * BY, z0 = bz * BZ;
 
-  // level 0.  Rows / planes outside the storage (beyond the H-deep ghosts) and lanes past the
-  // row's last ghost read 0: they only feed cells outside every stored output's cone.
-  for (int i = wave; i < NP * NR; i += NW) {
-    const int pz = i / NR, ry = i - pz * NR;
+  // level 0: the outputs' dependency cone, rows y0-T .. y0+BY+T-1 of every plane.  Rows /
+  // planes outside the storage (beyond the H-deep ghosts) and lanes past the row's last ghost
+  // read 0: they only feed cells outside every stored output's cone.
+  constexpr int NL = BY + 2 * TL;
+  for (int i = wave; i < NP * NL; i += NW) {
+    const int pz = i / NL, ry = C::R0 - TL + (i - pz * NL);
     const int z = z0 - TL + pz, y = y0 - C::R0 + ry;
     V2 v{(T)0, (T)0};
     if (z >= -g.H && z < g.nz + g.H && y >= -g.H && y < g.ny + g.H && lane < g.nx + g.H)
       v = s[gs::lin(g, lane, y, z)];
     buf[0][pz][ry][lane] = v;
   }
-  // the first and last rows of the level-1 buffer are read (quad halo rows) but never computed
-  for (int pz = wave; pz < NP; pz += NW) {
-    buf[1][pz][0][lane] = V2{(T)0, (T)0};
-    buf[1][pz][NR - 1][lane] = V2{(T)0, (T)0};
+  // rows the quads read beyond the cone (level 0: R0-5 .. R0-T-1 and R0+BY+T .. NR-1; the
+  // level-1 buffer's first and last rows are never computed): defined zeros
+  constexpr int NZR = C::R0 - TL;  // zero rows per side of level 0
+  for (int i = wave; i < NP * (2 * NZR + 2); i += NW) {
+    const int pz = i / (2 * NZR + 2), j = i - pz * (2 * NZR + 2);
+    if (j < 2 * NZR) buf[0][pz][j < NZR ? j : NR - 2 * NZR + j][lane] = V2{(T)0, (T)0};
+    else buf[1][pz][j == 2 * NZR ? 0 : NR - 1][lane] = V2{(T)0, (T)0};
   }
   V2 kc;
   {
