@@ -268,7 +268,7 @@ def run(args) -> int:
                                 if sim.overlapped else f"spatial-3d {dstr}"),
                 "dims": dom.dims,
                 "local_extent": dom.proc_sizes,
-                "fuse_steps": sim.fuse,
+                "fuse_steps": sim.depth, "ghost_width": sim.H,
                 "fused_kernel": {str(n): {"tile": c[0] or "default", "sched": c[1]}
                                  for n, c in sim.fused_choice().items()},
                 "transport": sim.transport,

@@ -470,6 +470,8 @@ class HipBackend final : public gs::Backend {
     if (autotune_part(src, dst, n, t, whole, &cfg_[n], &sched_[n], &ms)) tuned_ms_[n] = ms;
   }
 
+  double fused_ms(int n) const override { return n >= 2 && n <= 3 ? tuned_ms_[n] : 0.0; }
+
   void fused_choice(int n, int* cfg, int* sched, float* ms) const {
     *cfg = cfg_[n];
     *sched = sched_[n];

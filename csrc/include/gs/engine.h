@@ -44,6 +44,9 @@ class Backend {
   // optional one-time preparation (autotuning) of the fused kernel for depth n; must not
   // change the state held in buffer src
   virtual void prepare_fused(int src, int dst, int n, int64_t t) { (void)src; (void)dst; (void)n; (void)t; }
+  // milliseconds of one whole-interior fused pass of depth n as timed by prepare_fused (0 if
+  // not timed: tuning disabled or a configuration pinned)
+  virtual double fused_ms(int n) const { (void)n; return 0.0; }
   // fused() restricted to the output z-runs [zlo0, +zlen0) and [zlo1, +zlen1) (zlen1 may be 0).
   // Supported exactly when fused_supported(n); reads level-0 planes zlo-n .. zend+n-1 only.
   virtual bool fused_supported(int n) const { (void)n; return false; }
@@ -198,6 +201,24 @@ class Engine {
         shell_run(cur_, 1 - cur_, n, t_, sp);
       }
     }
+    // Without a halo exchange to amortise, the depth is a pure kernel-cost choice: use the one
+    // with the lowest tuned time per step (small grids: T=2 tiles waste less on the 2T halo,
+    // large ones: T=3 saves HBM traffic; profiles/r2_fuse_small.txt, r3_small_grid.txt).
+    if (auto_depth_ && !has_remote_ && cfg_.fuse >= 3) {
+      double best = 0.0;
+      for (int n = 2; n <= cfg_.fuse; ++n) {
+        const double ms = be_->fused_ms(n);
+        if (ms <= 0.0) {
+          best = 0.0;
+          break;
+        }
+        if (best == 0.0 || ms / n < best) {
+          best = ms / n;
+          depth_ = n;
+        }
+      }
+      if (best == 0.0) depth_ = 0;
+    }
     // the timing runs scribbled over the other buffer: restore the reference's zeroed
     // u_temp/v_temp (ghosts included) so the ghost-parity bookkeeping stays exact
     const Geom& g = cfg_.g;
@@ -294,9 +315,18 @@ class Engine {
            (be_->can_exchange_inplace(plan_) || be_->has_native_transport());
   }
 
+  // steps per pass: the fuse depth, or the measured cheaper one (prepare, single rank, when
+  // the depth was left to the engine: set_auto_depth)
+  int depth() const { return depth_ > 0 ? depth_ : cfg_.fuse; }
+  void set_auto_depth(bool on) {
+    auto_depth_ = on;
+    if (!on) depth_ = 0;
+  }
+
   void advance(int64_t nsteps) {
+    const int kmax = depth();
     while (nsteps > 0) {
-      const int k = (int)(nsteps < cfg_.fuse ? nsteps : cfg_.fuse);
+      const int k = (int)(nsteps < kmax ? nsteps : kmax);
       const int oth = 1 - cur_;
       if (nsteps >= 2 * (int64_t)k && chained(k)) {
         const int64_t npass = nsteps / k;
@@ -447,6 +477,8 @@ class Engine {
   bool has_nbr_ = false;
   bool has_remote_ = false;
   int overlap_ = -1;
+  int depth_ = 0;  // measured steps per pass (0: cfg_.fuse)
+  bool auto_depth_ = false;
   bool loopback_ = false;
   // GS_OVERLAP_CHAIN=0: run in-place overlapped passes one by one (A/B of advance_chained)
   bool chain_ = !(getenv("GS_OVERLAP_CHAIN") && atoi(getenv("GS_OVERLAP_CHAIN")) == 0);

@@ -173,7 +173,7 @@ def run(settings: Settings, out=sys.stdout) -> dict:
         stream.close()
     result = {"steps": step, "loop_s": loop_s, "compute_s": compute_s,
               "mlups_compute": cells * (step - first_step) / max(compute_s, 1e-12) / 1e6,
-              "timers": timer.summary(), "ranks": ctx.world_size, "fuse": sim.fuse,
+              "timers": timer.summary(), "ranks": ctx.world_size, "fuse": sim.depth,
               "transport": sim.transport}
     perf.write(summary=result)
     perf.close()

@@ -43,6 +43,11 @@ def default_fuse(backend: str, domain: CartDomain, dtype: str = "float32") -> in
     # T=2 on smaller planes (L=128: 224-227k vs 191-192k, L=64: 54k vs 42k), where the
     # 2T-cell tile halo costs more than the saved traffic.
     nx, ny, nz = domain.proc_sizes
+    if not any(r >= 0 and r != domain.rank for i, r in enumerate(domain.nbr27) if i != 13):
+        # no halo exchange to amortise: H = 3 ghost layers, and prepare() runs the depth (2 or
+        # 3) with the lower measured kernel time per step (engine.h depth()) -- the block
+        # kernel (csrc/hip/block.hpp) moved the small-grid crossover
+        return max(1, min(3, nx, ny, nz))
     t = 2 if min(nx, ny) < 160 else 3
     return max(1, min(t, nx, ny, nz))
 
@@ -64,6 +69,7 @@ class GrayScott:
             self.device = torch.device("cuda", torch.cuda.current_device())
         else:
             self.device = torch.device("cpu")
+        auto_depth = (fuse is None or fuse <= 0) and settings.fuse_steps <= 0
         if fuse is None or fuse <= 0:
             fuse = (settings.fuse_steps if settings.fuse_steps > 0
                     else default_fuse(self.backend, domain, parse_precision(settings.precision)))
@@ -91,6 +97,9 @@ class GrayScott:
                                     domain.rank, fuse, use_fused, self.buffers[0].data_ptr(),
                                     self.buffers[1].data_ptr(), self.sendbuf.data_ptr(),
                                     self.recvbuf.data_ptr(), stream)
+        # a depth left to the engine: prepare() may run fewer steps per pass when they are
+        # cheaper per step (single rank; an explicit fuse is kept as given)
+        self.engine.set_auto_depth(auto_depth)
         ov = str(getattr(settings, "overlap", "auto")).lower()
         if ov not in ("auto", "on", "off", "true", "false", "1", "0"):
             raise ValueError(f"overlap must be auto | on | off, not {ov!r}")
@@ -200,6 +209,12 @@ class GrayScott:
     def overlapped(self) -> bool:
         """Whether full-depth passes overlap their halo exchange with the inner planes."""
         return self.engine.overlapped(self.fuse)
+
+    @property
+    def depth(self) -> int:
+        """Steps per pass (per halo exchange): ``fuse``, or -- single rank, after
+        init_fields -- the depth <= fuse with the lowest measured kernel time per step."""
+        return self.engine.depth()
 
     # ------------------------------------------------------------------------------------
     def init_fields(self) -> None:

@@ -75,6 +75,10 @@ def _declare(lib) -> None:
     lib.gs_set_loopback.restype = c_int
     lib.gs_overlapped.argtypes = [c_void_p, c_int32]
     lib.gs_overlapped.restype = c_int
+    lib.gs_depth.argtypes = [c_void_p]
+    lib.gs_depth.restype = c_int
+    lib.gs_set_auto_depth.argtypes = [c_void_p, c_int32]
+    lib.gs_set_auto_depth.restype = c_int
     lib.gs_get_step.argtypes = [c_void_p]
     lib.gs_get_step.restype = c_int64
     lib.gs_set_step.argtypes = [c_void_p, c_int64]
@@ -250,6 +254,13 @@ class Engine:
 
     def overlapped(self, k: int) -> bool:
         return bool(self.lib.gs_overlapped(self.h, int(k)))
+
+    def set_auto_depth(self, on: bool):
+        self._chk(self.lib.gs_set_auto_depth(self.h, 1 if on else 0), "set_auto_depth")
+
+    def depth(self) -> int:
+        """Steps per pass: the fuse depth, or the cheaper one measured by prepare()."""
+        return int(self.lib.gs_depth(self.h))
 
     def advance(self, n: int):
         self._chk(self.lib.gs_advance(self.h, int(n)), "advance")

@@ -98,3 +98,27 @@ def test_autotuner_times_block_kernel_at_l64():
     ref = _run(64, 2, 9, cfg="4x8:1s")
     np.testing.assert_array_equal(got[0], ref[0])
     np.testing.assert_array_equal(got[1], ref[1])
+
+
+def test_auto_depth_is_measured_single_rank():
+    """fuse left to the engine (single rank): H = 3 ghosts, prepare() runs the depth with the
+    lower tuned time per step (engine.h depth()); the result stays within the golden tolerance."""
+    from grayscott_amd.ops import native
+    native.fused_unpin()
+    s = Settings(L=64, precision="Float32", F=0.02, k=0.048, dt=1.0, Du=0.2, Dv=0.1, noise=0.1,
+                 backend="AMDGPU", seed=19)
+    sim = GrayScott(s, init_domain(64, 1, 0))
+    try:
+        sim.init_fields()
+        assert sim.fuse == 3 and sim.depth in (2, 3)
+        choice = sim.fused_choice()
+        print("L=64 auto depth:", sim.depth, choice)
+        per_step = {n: c[2] / n for n, c in choice.items()}
+        assert sim.depth == min(per_step, key=per_step.get)
+        sim.iterate(24)
+        g = sim.get_fields()
+    finally:
+        sim.close()
+    c = _run(64, 1, 24, backend="CPU", random=False)
+    assert np.abs(g[0] - c[0]).max() < 2e-5
+    assert np.abs(g[1] - c[1]).max() < 2e-5
