@@ -67,14 +67,33 @@ __global__ __launch_bounds__(64 * C::NW, 1) void k_block(const typename C::V2* _
   // level 0: the outputs' dependency cone, rows y0-T .. y0+BY+T-1 of every plane.  Rows /
   // planes outside the storage (beyond the H-deep ghosts) and lanes past the row's last ghost
   // read 0: they only feed cells outside every stored output's cone.
+  // Every load of a wave is issued before the first LDS write (one memory latency, not one per
+  // row): a fully unrolled loop into registers, through plane buffer descriptors whose
+  // out-of-range accesses return 0 (no branches).
   constexpr int NL = BY + 2 * TL;
-  for (int i = wave; i < NP * NL; i += NW) {
-    const int pz = i / NL, ry = C::R0 - TL + (i - pz * NL);
-    const int z = z0 - TL + pz, y = y0 - C::R0 + ry;
-    V2 v{(T)0, (T)0};
-    if (z >= -g.H && z < g.nz + g.H && y >= -g.H && y < g.ny + g.H && lane < g.nx + g.H)
-      v = s[gs::lin(g, lane, y, z)];
-    buf[0][pz][ry][lane] = v;
+  constexpr int NLD = NP * NL;
+  constexpr int JL = (NLD + NW - 1) / NW;
+  {
+    const int pzb = (int)(gs::plane_elems(g) * (int64_t)sizeof(V2));
+    V2 lv[JL];
+#pragma unroll
+    for (int j = 0; j < JL; ++j) {
+      const int i = wave + j * NW;
+      const int pz = i / NL, ry = C::R0 - TL + (i - pz * NL);
+      const int z = z0 - TL + pz, y = y0 - C::R0 + ry;
+      const bool ok = i < NLD && z >= -g.H && z < g.nz + g.H && y >= -g.H && y < g.ny + g.H;
+      const __amdgpu_buffer_rsrc_t r =
+          plane_rsrc((const char*)s + (int64_t)(ok ? z + g.H : 0) * pzb, ok ? pzb : 0);
+      const int off = lane < g.nx + g.H ? ((y + g.H) * g.px + lane + g.xo) * (int)sizeof(V2)
+                                        : (int)0x80000000;
+      lv[j] = bload(r, off, (V2*)nullptr);
+    }
+#pragma unroll
+    for (int j = 0; j < JL; ++j) {
+      const int i = wave + j * NW;
+      const int pz = i / NL, ry = C::R0 - TL + (i - pz * NL);
+      if (i < NLD) buf[0][pz][ry][lane] = lv[j];
+    }
   }
   // rows the quads read beyond the cone (level 0: R0-5 .. R0-T-1 and R0+BY+T .. NR-1; the
   // level-1 buffer's first and last rows are never computed): defined zeros
