@@ -1,0 +1,17 @@
+# Round 3: the small-grid block kernel, short run (tests, small-grid benches, A/B, L=64 trace).
+# bitwise tests, small-grid benches (the autotuner sees the blk* candidates, the engine picks the
+# depth), an in-process A/B of every candidate, a kernel trace at L=64, then the whole GPU suite,
+# the driver's N=1 bench command and smoke().
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/${GS_OUT:-blk3c}
+mkdir -p $O
+cd $R
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests/test_gpu_block.py -x -v -s --timeout 120 --timeout-method thread > $O/blocktests.log 2>&1 &&
+timeout -k 10 300 python -u -m pytest tests/test_gpu_block.py -x -v -s --timeout 120 --timeout-method thread > $O/blocktests.log 2>&1 &&
+timeout -k 10 120 python bench.py --L 64 --steps 2000 --warmup 200 > $O/l64.json 2> $O/l64.err &&
+timeout -k 10 120 python bench.py --L 128 --steps 1000 --warmup 100 > $O/l128.json 2> $O/l128.err &&
+timeout -k 10 300 python scripts/tune_inproc.py --L 64 48 --fuse 2 3 --cfg 4x6:2s 4x8:1s blk8x2w8 blk4x2w4 blk8x1w8 blk4x4w8 blk4x1w4 --sched 2 --init random --rounds 3 --steps 400 > $O/ab.txt 2>&1 &&
+timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $O/prof64 -o run -- python bench.py --L 64 --steps 400 --warmup 40 > $O/prof64.log 2>&1
+echo "exit $?"
