@@ -45,8 +45,16 @@ struct BCfg {
   static constexpr int NR = BY + 10;
   static constexpr int NP = BZ + 2 * TL;
   static constexpr int LDS_BYTES = 2 * NP * NR * 64 * (int)sizeof(V2);
+  // whether the two level buffers fit the CU's LDS (run_block falls back to k_fused if not)
+  static constexpr bool FITS = LDS_BYTES <= 160 * 1024;
   static_assert(BY % 4 == 0, "blocks hold whole noise quads");
-  static_assert(LDS_BYTES <= 160 * 1024, "two level buffers must fit the CU's LDS");
+  // level l+1's work items (noise quad, plane): intermediate levels one quad of halo on each
+  // side in y and TL-1-l planes in z; each wave takes items wave, wave + NW, ...
+  static constexpr int nq(int l) { return BY / 4 + (l + 1 < TL ? 2 : 0); }
+  static constexpr int npl(int l) { return BZ + 2 * (TL - 1 - l); }
+  static constexpr int items(int l) { return nq(l) * npl(l); }
+  static constexpr int per_wave(int l) { return (items(l) + NW - 1) / NW; }
+  static constexpr int JMAX = per_wave(0);
 };
 
 template <class C>
@@ -63,6 +71,16 @@ __global__ __launch_bounds__(64 * C::NW, 1) void k_block(const typename C::V2* _
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int by = blockIdx.x % a.nby, bz = blockIdx.x / a.nby;
   const int y0 = a.yb + by * BY, z0 = bz * BZ;
+
+  V2 kc;
+  {
+    const T k0 = f.kc.x, k1 = f.kc.y;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(kc.x) : "s"(k0));
+    asm volatile("v_mov_b32 %0, %1" : "=v"(kc.y) : "s"(k1));
+  }
+  const T ar31 = f.ar * (T)4.656612873077392578125e-10;
+  const uint32_t Ly4 = (uint32_t)((g.Ly + 3) >> 2);
+  gs::U4 W[TL][C::JMAX];  // noise words per (level, item of this wave)
 
   // level 0: the outputs' dependency cone, rows y0-T .. y0+BY+T-1 of every plane.  Rows /
   // planes outside the storage (beyond the H-deep ghosts) and lanes past the row's last ghost
@@ -88,6 +106,25 @@ __global__ __launch_bounds__(64 * C::NW, 1) void k_block(const typename C::V2* _
                                         : (int)0x80000000;
       lv[j] = bload(r, off, (V2*)nullptr);
     }
+    // the noise words of every item this wave will compute, at every level, while the loads
+    // are in flight (they depend on the cell and the step only)
+    if constexpr (C::NOISE) {
+#pragma unroll
+      for (int l = 0; l < TL; ++l) {
+#pragma unroll
+        for (int j = 0; j < C::per_wave(l); ++j) {
+          const int it = wave + j * NW;
+          if (it < C::items(l)) {
+            const int zi = it / C::nq(l), qi = it - zi * C::nq(l);
+            const int qy = y0 - (l + 1 < TL ? 4 : 0) + 4 * qi;
+            const int z = z0 - (TL - 1 - l) + zi;
+            const uint32_t gy4 = (uint32_t)((g.oy + qy) >> 2);
+            const uint32_t qu = (uint32_t)g.Lx * (gy4 + Ly4 * (uint32_t)(g.oz + z));
+            W[l][j] = philox_dev<true>(qu + (uint32_t)(g.ox + lane), 0u, (uint64_t)(a.t + l), seed);
+          }
+        }
+      }
+    }
 #pragma unroll
     for (int j = 0; j < JL; ++j) {
       const int i = wave + j * NW;
@@ -103,14 +140,6 @@ __global__ __launch_bounds__(64 * C::NW, 1) void k_block(const typename C::V2* _
     if (j < 2 * NZR) buf[0][pz][j < NZR ? j : NR - 2 * NZR + j][lane] = V2{(T)0, (T)0};
     else buf[1][pz][j == 2 * NZR ? 0 : NR - 1][lane] = V2{(T)0, (T)0};
   }
-  V2 kc;
-  {
-    const T k0 = f.kc.x, k1 = f.kc.y;
-    asm volatile("v_mov_b32 %0, %1" : "=v"(kc.x) : "s"(k0));
-    asm volatile("v_mov_b32 %0, %1" : "=v"(kc.y) : "s"(k1));
-  }
-  const T ar31 = f.ar * (T)4.656612873077392578125e-10;
-  const uint32_t Ly4 = (uint32_t)((g.Ly + 3) >> 2);
   __syncthreads();
 
 #pragma unroll
@@ -119,10 +148,8 @@ __global__ __launch_bounds__(64 * C::NW, 1) void k_block(const typename C::V2* _
     V2(*out)[NR][64] = buf[(l + 1) & 1];
     const bool last = l + 1 == TL;
     const int mq = last ? 0 : 1;          // intermediate levels: one quad of halo each side
-    const int nq = BY / 4 + 2 * mq;
+    const int nq = C::nq(l);
     const int dz = TL - 1 - l;            // planes of halo this level still needs
-    const int npl = BZ + 2 * dz;
-    const uint64_t tstep = (uint64_t)(a.t + l);
     // x ghosts of level l (the input): its boundary value.  Lane 0's left neighbour is added
     // last in the sum (in[x-1] + (in[x+1] + yz)), so adding it after the DPP sum (where the
     // missing lane read 0) is exact; lane 63's right neighbour is added first, so it goes into
@@ -131,7 +158,10 @@ __global__ __launch_bounds__(64 * C::NW, 1) void k_block(const typename C::V2* _
     const V2 gl = lane == 0 ? V2{bin, (T)0} : V2{(T)0, (T)0};
     const V2 gr = (a.gr && lane == 63) ? V2{bin, (T)0} : V2{(T)0, (T)0};
     const T bout = (T)gs::bc_u(a.t + l + 1);
-    for (int it = wave; it < nq * npl; it += NW) {
+#pragma unroll
+    for (int j = 0; j < C::per_wave(l); ++j) {
+      const int it = wave + j * NW;
+      if (it >= C::items(l)) break;  // wave-uniform
       const int zi = it / nq, qi = it - zi * nq;
       const int qy = y0 - 4 * mq + 4 * qi;  // local y of the quad's first row
       const int z = z0 - dz + zi;
@@ -146,13 +176,8 @@ __global__ __launch_bounds__(64 * C::NW, 1) void k_block(const typename C::V2* _
         pp[k] = lds_load2(&in[pz + 1][ry + k][lane]);
       }
       const int64_t gz = g.oz + z;
-      gs::U4 blk{0, 0, 0, 0};
-      if constexpr (C::NOISE) {
-        // k_fused's counter: gx + Lx * (gy4 + Ly4 * gz) (fits 32 bits: host check)
-        const uint32_t gy4 = (uint32_t)((g.oy + qy) >> 2);
-        const uint32_t qu = (uint32_t)g.Lx * (gy4 + Ly4 * (uint32_t)gz);
-        blk = philox_dev<true>(qu + (uint32_t)(g.ox + lane), 0u, tstep, seed);
-      }
+      // k_fused's counter gx + Lx * (gy4 + Ly4 * gz) (fits 32 bits: host check), drawn above
+      const gs::U4 blk = C::NOISE ? W[l][j] : gs::U4{0, 0, 0, 0};
       const bool zout = gz < 0 || gz >= g.Lz;
       const bool xout = g.ox + lane >= g.Lx;
 #pragma unroll
@@ -188,6 +213,9 @@ __global__ __launch_bounds__(64 * C::NW, 1) void k_block(const typename C::V2* _
 
 template <class C>
 bool run_block(const void* s, void* d, const FusedArgs& a0, const gs::Params& p, hipStream_t st) {
+  if constexpr (!C::FITS) {
+    return false;
+  } else {
   const Geom& g = a0.g;
   BlockArgs a{};
   a.g = g;
@@ -200,6 +228,7 @@ bool run_block(const void* s, void* d, const FusedArgs& a0, const gs::Params& p,
   k_block<C><<<(unsigned)(a.nby * nbz), 64 * C::NW, 0, st>>>(
       (const typename C::V2*)s, (typename C::V2*)d, a, f, p.seed);
   return true;
+  }
 }
 
 // whether k_block can run this launch: the whole interior (no z-runs / store mask / reserve),

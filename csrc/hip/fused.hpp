@@ -791,11 +791,11 @@ inline const FusedCfgEntry* fused_cfg_table(int* n) {
       {"4x16:1s", true, false},  // 19  64-row tile, 4 waves per SIMD (fits 128 VGPRs)
       // small grids (block.hpp): k_block, output blocks of whole x rows x BY rows x BZ planes,
       // NW waves; timed only on launches it supports (block_supported), else the default shape
-      {"blk8x2w8", true, false},  // 20
-      {"blk4x2w4", true, false},  // 21
-      {"blk8x1w8", true, false},  // 22
-      {"blk4x4w8", true, false},  // 23
-      {"blk4x1w4", true, false},  // 24
+      {"blk8x2w8", true, false},   // 20
+      {"blk4x4w8", true, false},   // 21
+      {"blk8x2w16", true, false},  // 22
+      {"blk4x4w16", true, false},  // 23
+      {"blk8x4w16", true, false},  // 24  (T=2 only: T=3 levels do not fit the LDS)
 #ifdef GS_ABLATION
       {"4x12:2s-abl1", true, false},  // 25  no barriers
       {"4x12:2s-abl2", true, false},  // 26  L2-resident loads
@@ -880,11 +880,11 @@ void run_fused_cfg(const void* s, void* d, const FusedArgs& a, const gs::Params&
       case 15: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true>, T>::run(s, d, a, p, st); return;
       case 18: FusedLaunch<FCfg<T, TL, 4, 16, 1, PER, NZ>, T>::run(s, d, a, p, st); return;
       case 19: FusedLaunch<FCfg<T, TL, 4, 16, 1, PER, NZ, true>, T>::run(s, d, a, p, st); return;
-      case 20: if (block_supported(a)) { run_block<BCfg<T, TL, 8, 2, 8, NZ>>(s, d, a, p, st); return; } break;
-      case 21: if (block_supported(a)) { run_block<BCfg<T, TL, 4, 2, 4, NZ>>(s, d, a, p, st); return; } break;
-      case 22: if (block_supported(a)) { run_block<BCfg<T, TL, 8, 1, 8, NZ>>(s, d, a, p, st); return; } break;
-      case 23: if (block_supported(a)) { run_block<BCfg<T, TL, 4, 4, 8, NZ>>(s, d, a, p, st); return; } break;
-      case 24: if (block_supported(a)) { run_block<BCfg<T, TL, 4, 1, 4, NZ>>(s, d, a, p, st); return; } break;
+      case 20: if (block_supported(a) && run_block<BCfg<T, TL, 8, 2, 8, NZ>>(s, d, a, p, st)) return; break;
+      case 21: if (block_supported(a) && run_block<BCfg<T, TL, 4, 4, 8, NZ>>(s, d, a, p, st)) return; break;
+      case 22: if (block_supported(a) && run_block<BCfg<T, TL, 8, 2, 16, NZ>>(s, d, a, p, st)) return; break;
+      case 23: if (block_supported(a) && run_block<BCfg<T, TL, 4, 4, 16, NZ>>(s, d, a, p, st)) return; break;
+      case 24: if (block_supported(a) && run_block<BCfg<T, TL, 8, 4, 16, NZ>>(s, d, a, p, st)) return; break;
 #ifdef GS_ABLATION
       case 25: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 1>, T>::run(s, d, a, p, st); return;
       case 26: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 2>, T>::run(s, d, a, p, st); return;
