@@ -122,3 +122,37 @@ def test_auto_depth_is_measured_single_rank():
     c = _run(64, 1, 24, backend="CPU", random=False)
     assert np.abs(g[0] - c[0]).max() < 2e-5
     assert np.abs(g[1] - c[1]).max() < 2e-5
+
+
+@pytest.mark.parametrize("L,k,step", [((48, 40, 36), 2, 7), ((64, 40, 36), 3, 5), ((36, 36, 36), 2, 0)])
+def test_block_kernel_raw_pass_reads_stored_ghosts(L, k, step):
+    """A raw fused pass (the timing / overlap-test primitive gs_fused_runs_raw) runs without the
+    engine's ensure_bc, so the stored x ghosts need not be the boundary value of the pass's time
+    (here: the init's u = 1 ghosts at an odd step).  k_fused reads them from the buffer; so must
+    k_block -- one pass of each, bit for bit, on a non-cubic domain."""
+    from grayscott_amd.ops import native
+    outs = []
+    try:
+        for cfg in ("4x8:1s", "blk8x2w8", "blk4x4w16"):
+            native.fused_select(cfg)
+            s = Settings(L=L[0], precision="Float32", F=0.02, k=0.048, dt=1.0, Du=0.2, Dv=0.1,
+                         noise=0.1, backend="AMDGPU", seed=99)
+            sim = GrayScott(s, init_domain(L, 1, 0), fuse=k)
+            try:
+                sim.init_fields()
+                sim.randomize_fields(seed=11)
+                sim.set_step(step)
+                lib, h = sim.engine.lib, sim.engine.h
+                nz = sim.domain.proc_sizes[2]
+                native.check(lib, lib.gs_fused_runs_raw(h, k, 0, nz, 0, 0, 0, 0), "full")
+                torch.cuda.synchronize()
+                outs.append(sim.full_state(1 - sim.engine.current).cpu().numpy().copy())
+            finally:
+                sim.close()
+    finally:
+        native.fused_unpin()
+    g = sim.geom
+    nx, ny, nz = init_domain(L, 1, 0).proc_sizes
+    inner = (slice(g.H, g.H + nz), slice(g.H, g.H + ny), slice(g.xo, g.xo + nx))
+    for o in outs[1:]:
+        np.testing.assert_array_equal(o[inner], outs[0][inner])
