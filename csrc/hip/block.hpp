@@ -169,8 +169,10 @@ __global__ __launch_bounds__(64 * C::NW, 1) void k_block(const typename C::V2* _
     // boundary value above (k_fused's reset).  Lane 0's left neighbour is added last in the sum
     // (in[x-1] + (in[x+1] + yz)), so adding it after the DPP sum (where the missing lane read
     // 0) is exact; lane 63's right neighbour is added first, so it goes into yz before the DPP
-    // sum.
-    const V2 gb{(T)gs::bc_u(a.t + l), (T)0};
+    // sum.  Other lanes add +0.
+    const T bin = (T)gs::bc_u(a.t + l);
+    V2 gl = lane == 0 ? V2{bin, (T)0} : V2{(T)0, (T)0};
+    V2 gr = (a.gr && lane == 63) ? V2{bin, (T)0} : V2{(T)0, (T)0};
     const T bout = (T)gs::bc_u(a.t + l + 1);
 #pragma unroll
     for (int j = 0; j < C::per_wave(l); ++j) {
@@ -197,12 +199,15 @@ __global__ __launch_bounds__(64 * C::NW, 1) void k_block(const typename C::V2* _
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const V2 c = row[k + 1];
-        // the corrections on lane 63 / lane 0 only (exec-masked: one add each; at level 0 the
-        // stored ghost of this row from LDS)
+        if (l == 0) {  // stored level-0 ghosts of this row (LDS broadcast reads)
+          const V2 L0 = xg[0][pz][ry + k], R0v = xg[1][pz][ry + k];
+          gl = lane == 0 ? L0 : V2{(T)0, (T)0};
+          gr = (a.gr && lane == 63) ? R0v : V2{(T)0, (T)0};
+        }
         V2 yz = (row[k] + row[k + 2]) + pm[k];
-        if (a.gr && lane == 63) yz = yz + (l == 0 ? xg[1][pz][ry + k] : gb);
+        if (a.gr) yz = yz + gr;
         V2 A{lane_pair_sum_add<false>(c.x, yz.x), lane_pair_sum_add<false>(c.y, yz.y)};
-        if (lane == 0) A = A + (l == 0 ? xg[0][pz][ry + k] : gb);
+        A = A + gl;
         const V2 sum = A + pp[k];
         const V2 tt = c * c.yy;
         const V2 uvv = tt.xx * c.yy;
