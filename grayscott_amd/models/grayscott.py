@@ -31,17 +31,14 @@ def default_fuse(backend: str, domain: CartDomain, dtype: str = "float32") -> in
     """Steps fused per halo exchange when ``fuse_steps = 0`` (auto)."""
     if backend != "hip":
         return 1
-    if dtype == "float64":
-        # fp64 doubles the per-cell register footprint: T=3 tiles lose occupancy, T=2 with the
-        # XCD-grouped schedule is fastest (L=512: 263k vs 224k MLUPS, profiles/r1_tune_f64.txt)
-        nx, ny, nz = domain.proc_sizes
-        return max(1, min(2, nx, ny, nz))
     # The temporally blocked kernel cuts HBM traffic per step by T; a deeper halo also cuts
     # the RCCL round trips.  Measured on MI355X with the round-2 kernel
     # (profiles/r2_fuse_small.txt; round 1: profiles/r1_tune_fuse_depth.txt): T=3 wins from
     # 192^2 x-y planes up (L=192: 407-411k vs 370-403k MLUPS, L=256: 495-505k vs 459-468k);
     # T=2 on smaller planes (L=128: 224-227k vs 191-192k, L=64: 54k vs 42k), where the
-    # 2T-cell tile halo costs more than the saved traffic.
+    # 2T-cell tile halo costs more than the saved traffic.  fp64 follows the same rule since
+    # round 3 (T=2 is HBM-bound there: L=512 344k vs 311k MLUPS, L=1024 332k vs 276k at T=3,
+    # profiles/r3_f64_depth.txt; round 1 measured the opposite, profiles/r1_tune_f64.txt).
     nx, ny, nz = domain.proc_sizes
     if not any(r >= 0 and r != domain.rank for i, r in enumerate(domain.nbr27) if i != 13):
         # no halo exchange to amortise: H = 3 ghost layers, and prepare() runs the depth (2 or
