@@ -107,7 +107,7 @@ class CheckpointWriter:
     def start(self, step: int, sim, snap=None) -> None:
         """Begin the checkpoint of ``step``.  ``snap`` = ``(u, v, wait)`` from
         ``sim.snapshot_fields()`` when the caller already took one for this step."""
-        from .output import _Job
+        from .output import worker
         self.finish()
         w = _open_writer(self.tmp, self.settings, self.domain, self.ctx)
         # its own snapshot buffers when not sharing the output step's: an output step still
@@ -118,7 +118,7 @@ class CheckpointWriter:
             wait()
             return _write_data(w, step, u, v)
 
-        self._pending = (w, _Job(job))
+        self._pending = (w, worker("gs-async-checkpoint").submit(job))
 
     def finish(self) -> None:
         job, self._pending = self._pending, None
