@@ -223,17 +223,13 @@ constexpr int gs_gcd(int a, int b) { return b == 0 ? a : gs_gcd(b, a % b); }
 constexpr int gs_lcm(int a, int b) { return a / gs_gcd(a, b) * b; }
 
 template <typename T_, int TL_, int ROWS_, int WAVES_, int PF_, bool PERIODIC_, bool NOISE_,
-          bool SKEW_ = false, bool Q32_ = true, int ABL_ = 0, bool RSKIP_ = false>
+          bool SKEW_ = false, bool Q32_ = true, int ABL_ = 0>
 struct FCfg {
   using T = T_;
   using V2 = typename PairT<T>::type;
   static constexpr int TL = TL_, ROWS = ROWS_, WAVES = WAVES_, PF = PF_;
   static constexpr bool PERIODIC = PERIODIC_, NOISE = NOISE_, SKEW = SKEW_, Q32 = Q32_;
   static constexpr int ABL = ABL_;
-  // rows outside a level's dependency cone are not computed (per row, wave-uniform branches):
-  // the 4-row wave granularity leaves up to 3 such rows at each tile edge per level (4x12 at
-  // T=3: 10 of 136 row updates per plane)
-  static constexpr bool RSKIP = RSKIP_;
   static constexpr bool KV = (ABL_ & 4) != 0;
   static constexpr int R = PF + 2;                    // level-0 ring slots
   // level-l output ring / xch buffers: 2 slots.  Skewed: level l+1 reads level l's outputs of
@@ -466,19 +462,7 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
           const V2 ym = j == 0 ? up : in[j - 1];
           const V2 yp = j == ROWS - 1 ? dn : in[j + 1];
           const uint32_t w = k == 0 ? blk.x : (k == 1 ? blk.y : (k == 2 ? blk.z : blk.w));
-          // RSKIP: a row outside [l + 1, need_hi(l)] is outside the cone at every plane: its
-          // output and its running sum A only ever feed rows outside the next level's cone
-          // (kept defined, not computed; wave-uniform branch)
-          if constexpr (C::RSKIP) {
-            const int row = sg.wave * ROWS + j;
-            V2 r = in[j], Aj = S.A[l][j];
-            if (!(row < l + 1 || row > C::need_hi(l)))
-              r = cell_update<C>(Aj, in[j], Cc[j], ym, yp, f, S.ar31, S.kc, w);
-            S.A[l][j] = Aj;
-            res[j] = r;
-          } else {
-            res[j] = cell_update<C>(S.A[l][j], in[j], Cc[j], ym, yp, f, S.ar31, S.kc, w);
-          }
+          res[j] = cell_update<C>(S.A[l][j], in[j], Cc[j], ym, yp, f, S.ar31, S.kc, w);
         }
       }
       if (l + 1 < TL) {
@@ -812,21 +796,17 @@ inline const FusedCfgEntry* fused_cfg_table(int* n) {
       {"blk8x2w16", true, false},  // 22
       {"blk4x4w16", true, false},  // 23
       {"blk8x4w16", true, false},  // 24  (T=2 only: T=3 levels do not fit the LDS)
-      // rows outside each level's cone skipped (FCfg RSKIP)
-      {"4x12:1sr", true, false},   // 25
-      {"4x12:2sr", true, false},   // 26
-      {"4x8:1sr", true, true},     // 27
 #ifdef GS_ABLATION
-      {"4x12:2s-abl1", true, false},  // 28  no barriers
-      {"4x12:2s-abl2", true, false},  // 29  L2-resident loads
-      {"4x12:1s-abl4", true, false},  // 30  Philox keys in VGPRs (exact)
-      {"4x12:2s-abl4", true, false},  // 31  Philox keys in VGPRs (exact)
-      {"4x12:1s-abl8", true, false},  // 32  DPP sums with the s_nop (exact)
-      {"4x12:1s-abl12", true, false}, // 33  abl4 + abl8 (exact)
-      {"4x12:1s-abl16", true, false}, // 34  pipeline fill computes every level (exact)
-      {"4x8:1s-abl16", true, true},   // 35  pipeline fill computes every level (exact)
-      {"4x6:2s-abl16", true, true},   // 36  pipeline fill computes every level (exact)
-      {"4x12:1s-abl32", true, false}, // 37  Philox only on lanes in the x cone (exact)
+      {"4x12:2s-abl1", true, false},  // 25  no barriers
+      {"4x12:2s-abl2", true, false},  // 26  L2-resident loads
+      {"4x12:1s-abl4", true, false},  // 27  Philox keys in VGPRs (exact)
+      {"4x12:2s-abl4", true, false},  // 28  Philox keys in VGPRs (exact)
+      {"4x12:1s-abl8", true, false},  // 29  DPP sums with the s_nop (exact)
+      {"4x12:1s-abl12", true, false}, // 30  abl4 + abl8 (exact)
+      {"4x12:1s-abl16", true, false}, // 31  pipeline fill computes every level (exact)
+      {"4x8:1s-abl16", true, true},   // 32  pipeline fill computes every level (exact)
+      {"4x6:2s-abl16", true, true},   // 33  pipeline fill computes every level (exact)
+      {"4x12:1s-abl32", true, false}, // 34  Philox only on lanes in the x cone (exact)
 #endif
   };
   *n = (int)(sizeof(t) / sizeof(t[0]));
@@ -875,10 +855,9 @@ void run_fused_cfg(const void* s, void* d, const FusedArgs& a, const gs::Params&
       case 15: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true>, T>::run(s, d, a, p, st); return;
       case 16: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
       case 17: FusedLaunch<FCfg<T, TL, 4, 4, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
-      case 27: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 0, true>, T>::run(s, d, a, p, st); return;
 #ifdef GS_ABLATION
-      case 35: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
-      case 36: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 32: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 33: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
 #endif
       default: break;
     }
@@ -906,20 +885,17 @@ void run_fused_cfg(const void* s, void* d, const FusedArgs& a, const gs::Params&
       case 22: if (block_supported(a) && run_block<BCfg<T, TL, 8, 2, 16, NZ>>(s, d, a, p, st)) return; break;
       case 23: if (block_supported(a) && run_block<BCfg<T, TL, 4, 4, 16, NZ>>(s, d, a, p, st)) return; break;
       case 24: if (block_supported(a) && run_block<BCfg<T, TL, 8, 4, 16, NZ>>(s, d, a, p, st)) return; break;
-      case 25: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 0, true>, T>::run(s, d, a, p, st); return;
-      case 26: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 0, true>, T>::run(s, d, a, p, st); return;
-      case 27: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 0, true>, T>::run(s, d, a, p, st); return;
 #ifdef GS_ABLATION
-      case 28: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 1>, T>::run(s, d, a, p, st); return;
-      case 29: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 2>, T>::run(s, d, a, p, st); return;
-      case 30: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;
-      case 31: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;
-      case 32: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 8>, T>::run(s, d, a, p, st); return;
-      case 33: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 12>, T>::run(s, d, a, p, st); return;
-      case 34: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
-      case 35: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
-      case 36: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
-      case 37: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 32>, T>::run(s, d, a, p, st); return;
+      case 25: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 1>, T>::run(s, d, a, p, st); return;
+      case 26: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 2>, T>::run(s, d, a, p, st); return;
+      case 27: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;
+      case 28: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;
+      case 29: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 8>, T>::run(s, d, a, p, st); return;
+      case 30: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 12>, T>::run(s, d, a, p, st); return;
+      case 31: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 32: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 33: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 34: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 32>, T>::run(s, d, a, p, st); return;
 #endif
       default: break;  // 0 and 14: the default shape below
     }

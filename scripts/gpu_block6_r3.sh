@@ -7,7 +7,5 @@ cd $R
 timeout -k 10 300 python -u -m pytest tests/test_gpu_block.py -x -v -s --timeout 120 --timeout-method thread > $O/blocktests.log 2>&1 &&
 timeout -k 10 120 python bench.py --L 64 --steps 2000 --warmup 200 > $O/l64.json 2> $O/l64.err &&
 timeout -k 10 120 python bench.py --L 64 --steps 2000 --warmup 200 > $O/l64b.json 2> $O/l64b.err &&
-timeout -k 10 300 python scripts/tune_inproc.py --L 64 48 --fuse 2 3 --cfg 4x6:2s blk8x2w8 blk4x4w8 blk8x2w16 blk4x4w16 --sched 2 --init random --rounds 3 --steps 400 > $O/ab.txt 2>&1 &&
-# (appended) fp32 L=512 T=3: rows outside the cone skipped (4x12:1sr / 4x12:2sr) vs the production tiles
-timeout -k 10 300 python scripts/tune_inproc.py --L 512 --fuse 3 --cfg 4x12:1s 4x12:1sr 4x12:2s 4x12:2sr --sched 1 2 --init random --rounds 3 --steps 60 > $O/ab_rskip.txt 2>&1
+timeout -k 10 300 python scripts/tune_inproc.py --L 64 48 --fuse 2 3 --cfg 4x6:2s blk8x2w8 blk4x4w8 blk8x2w16 blk4x4w16 --sched 2 --init random --rounds 3 --steps 400 > $O/ab.txt 2>&1
 echo "exit $?"
