@@ -196,14 +196,8 @@ __global__ __launch_bounds__(64 * C::NW, 1) void k_block(const typename C::V2* _
       const gs::U4 blk = C::NOISE ? W[l][j] : gs::U4{0, 0, 0, 0};
       const bool zout = gz < 0 || gz >= g.Lz;
       const bool xout = g.ox + lane >= g.Lx;
-      // rows of this quad inside the level's cone [y0 - dz, y0 + BY + dz): the outer quads of an
-      // intermediate level are partial (their other rows never reach a stored output, and the
-      // next level reads them only for rows outside its own cone); wave-uniform
-      const int klo = last ? 0 : max(0, y0 - dz - qy);
-      const int khi = last ? 4 : min(4, y0 + BY + dz - qy);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        if (!last && (k < klo || k >= khi)) continue;
         const V2 c = row[k + 1];
         if (l == 0) {  // stored level-0 ghosts of this row (LDS broadcast reads)
           const V2 L0 = xg[0][pz][ry + k], R0v = xg[1][pz][ry + k];

@@ -153,11 +153,7 @@ def block_pass(ustore, vstore, geo, t, TL, BY, BZ, fc):
                 pp = buf[inb, :, pz + 1, ry:ry + 4]
                 gz = oz + z
                 words = philox_words(oy + qy, gz, lane, L, t + lv)
-                klo = 0 if last else max(0, y0 - dz - qy)
-                khi = 4 if last else min(4, y0 + BY + dz - qy)
                 for k in range(4):
-                    if k < klo or k >= khi:  # outside the level's cone: not computed
-                        continue
                     if lv == 0:  # the stored level-0 ghosts of this row
                         gl = [np.where(lane == 0, xg[0, i, pz, ry + k], f32(0)).astype(f32)
                               for i in range(2)]
