@@ -25,10 +25,10 @@
 namespace gsk {
 extern template bool launch_fused<float>(const Vec2<float>::type*, Vec2<float>::type*, const Geom&,
                                          const gs::Params&, int, int64_t, hipStream_t, int, int,
-                                         int, int, int, int, int, int);
+                                         int, int, int, int, int, int, bool);
 extern template bool launch_fused<double>(const Vec2<double>::type*, Vec2<double>::type*,
                                           const Geom&, const gs::Params&, int, int64_t,
-                                          hipStream_t, int, int, int, int, int, int, int, int);
+                                          hipStream_t, int, int, int, int, int, int, int, int, bool);
 extern template bool launch_shell<float>(const void*, void*, const Geom&, const gs::Params&, int,
                                          int64_t, int, int, hipStream_t);
 extern template bool launch_shell<double>(const void*, void*, const Geom&, const gs::Params&, int,
@@ -171,7 +171,8 @@ class HipBackend final : public gs::Backend {
     // an explicit gs_fused_select / gs_fused_sched overrides the tuned choice at any time
     const bool pin = fused_pinned();
     const bool ok = gsk::launch_fused<T>(buf_[src], buf_[dst], g_, p_, n, t, stream_,
-                                         pin ? -1 : cfg_[n], pin ? -1 : sched_[n]);
+                                         pin ? -1 : cfg_[n], pin ? -1 : sched_[n], 0, -1, 0, 0,
+                                         0, 0, /*allow_block=*/true);
     if (ok) HIP_CHECK(hipGetLastError());
     return ok;
   }
@@ -399,6 +400,7 @@ class HipBackend final : public gs::Backend {
     // tile variants are instantiated for the production path only (fused.hpp run_fused_cfg)
     const bool variants = !g_.periodic && p_.noise != 0.0 && gsk::philox_q32(g_);
     std::vector<int> cfgs;
+    bool blk_ok = false;  // the block kernel is a candidate (whole-interior launch it supports)
     if (fixed_cfg >= 0) {
       cfgs = {fixed_cfg};
     } else if (!variants) {
@@ -417,7 +419,8 @@ class HipBackend final : public gs::Backend {
       fa.mx1 = g_.nx;
       fa.my1 = g_.ny;
       fa.reserve = pt.reserve;
-      const bool blk_ok = pt.mask == 0 && gsk::block_supported(fa);
+      fa.allow_block = 1;
+      blk_ok = pt.mask == 0 && gsk::block_supported(fa);
       for (int i = 0; i < nt; ++i)
         if ((sizeof(T) == 4 ? tab[i].f32 : tab[i].f64) && i != dflt && !strstr(tab[i].name, "-abl") &&
             (blk_ok || !gsk::fused_cfg_is_block(i)))
@@ -428,7 +431,8 @@ class HipBackend final : public gs::Backend {
       for (int sc = 0; sc < (gsk::fused_cfg_is_block(c) ? 1 : nsched); ++sc) cands.push_back({c, sc});
     auto launch = [&](const Cand& c) {
       return gsk::launch_fused<T>(buf_[src], buf_[dst], g_, p_, n, t, stream_, c.cfg, c.sched,
-                                  pt.zlo0, pt.zlen0, pt.zlo1, pt.zlen1, pt.reserve, pt.mask);
+                                  pt.zlo0, pt.zlen0, pt.zlo1, pt.zlen1, pt.reserve, pt.mask,
+                                  blk_ok);
     };
     // interleaved rounds (box-to-box and launch-to-launch jitter is several %): first launch
     // of each candidate is a warm-up, then the best of kRounds timed launches decides

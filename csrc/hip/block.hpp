@@ -44,7 +44,7 @@ struct BCfg {
   static constexpr int R0 = 5;
   static constexpr int NR = BY + 10;
   static constexpr int NP = BZ + 2 * TL;
-  static constexpr int LDS_BYTES = 2 * NP * NR * 65 * (int)sizeof(V2);  // + the x ghosts
+  static constexpr int LDS_BYTES = 2 * NP * NR * 64 * (int)sizeof(V2);
   // whether the two level buffers fit the CU's LDS (run_block falls back to k_fused if not)
   static constexpr bool FITS = LDS_BYTES <= 160 * 1024;
   static_assert(BY % 4 == 0, "blocks hold whole noise quads");
@@ -66,9 +66,6 @@ __global__ __launch_bounds__(64 * C::NW, 1) void k_block(const typename C::V2* _
   using V2 = typename C::V2;
   constexpr int TL = C::TL, BY = C::BY, BZ = C::BZ, NW = C::NW, NR = C::NR, NP = C::NP;
   __shared__ V2 buf[2][NP][NR][64];  // [level parity][plane][row][lane]
-  // level-0 x ghosts as stored (x = -1, and x = nx when nx == 64: no lane holds it); k_fused
-  // reads them from the buffer too, so k_block does not rely on their being boundary values
-  __shared__ V2 xg[2][NP][NR];
   const Geom& g = a.g;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -96,9 +93,7 @@ __global__ __launch_bounds__(64 * C::NW, 1) void k_block(const typename C::V2* _
   constexpr int JL = (NLD + NW - 1) / NW;
   {
     const int pzb = (int)(gs::plane_elems(g) * (int64_t)sizeof(V2));
-    V2 lv[JL], lg[JL];
-    // lane 0: the x = -1 ghost; lane 1: the x = nx ghost (needed when nx == 64)
-    const int gxo = lane == 0 ? g.xo - 1 : (lane == 1 && a.gr ? g.xo + g.nx : -1);
+    V2 lv[JL];
 #pragma unroll
     for (int j = 0; j < JL; ++j) {
       const int i = wave + j * NW;
@@ -110,8 +105,6 @@ __global__ __launch_bounds__(64 * C::NW, 1) void k_block(const typename C::V2* _
       const int off = lane < g.nx + g.H ? ((y + g.H) * g.px + lane + g.xo) * (int)sizeof(V2)
                                         : (int)0x80000000;
       lv[j] = bload(r, off, (V2*)nullptr);
-      lg[j] = bload(r, gxo >= 0 ? ((y + g.H) * g.px + gxo) * (int)sizeof(V2) : (int)0x80000000,
-                    (V2*)nullptr);
     }
     // the noise words of every item this wave will compute, at every level, while the loads
     // are in flight (they depend on the cell and the step only)
@@ -136,10 +129,7 @@ __global__ __launch_bounds__(64 * C::NW, 1) void k_block(const typename C::V2* _
     for (int j = 0; j < JL; ++j) {
       const int i = wave + j * NW;
       const int pz = i / NL, ry = C::R0 - TL + (i - pz * NL);
-      if (i < NLD) {
-        buf[0][pz][ry][lane] = lv[j];
-        if (lane < 2) xg[lane][pz][ry] = lg[j];
-      }
+      if (i < NLD) buf[0][pz][ry][lane] = lv[j];
     }
   }
   // rows the quads read beyond the cone (level 0: R0-5 .. R0-T-1 and R0+BY+T .. NR-1; the
@@ -147,13 +137,8 @@ __global__ __launch_bounds__(64 * C::NW, 1) void k_block(const typename C::V2* _
   constexpr int NZR = C::R0 - TL;  // zero rows per side of level 0
   for (int i = wave; i < NP * (2 * NZR + 2); i += NW) {
     const int pz = i / (2 * NZR + 2), j = i - pz * (2 * NZR + 2);
-    if (j < 2 * NZR) {
-      const int r = j < NZR ? j : NR - 2 * NZR + j;
-      buf[0][pz][r][lane] = V2{(T)0, (T)0};
-      if (lane < 2) xg[lane][pz][r] = V2{(T)0, (T)0};
-    } else {
-      buf[1][pz][j == 2 * NZR ? 0 : NR - 1][lane] = V2{(T)0, (T)0};
-    }
+    if (j < 2 * NZR) buf[0][pz][j < NZR ? j : NR - 2 * NZR + j][lane] = V2{(T)0, (T)0};
+    else buf[1][pz][j == 2 * NZR ? 0 : NR - 1][lane] = V2{(T)0, (T)0};
   }
   __syncthreads();
 
@@ -165,14 +150,15 @@ __global__ __launch_bounds__(64 * C::NW, 1) void k_block(const typename C::V2* _
     const int mq = last ? 0 : 1;          // intermediate levels: one quad of halo each side
     const int nq = C::nq(l);
     const int dz = TL - 1 - l;            // planes of halo this level still needs
-    // x ghosts of level l (the input): the stored ghost cells for level 0, the level's
-    // boundary value above (k_fused's reset).  Lane 0's left neighbour is added last in the sum
+    // x ghosts of level l (the input): the level's boundary value -- for level 0 the engine's
+    // ensure_bc fill (only Backend::fused() launches k_block, always after it), above it
+    // k_fused's reset rule.  Lane 0's left neighbour is added last in the sum
     // (in[x-1] + (in[x+1] + yz)), so adding it after the DPP sum (where the missing lane read
     // 0) is exact; lane 63's right neighbour is added first, so it goes into yz before the DPP
     // sum.  Other lanes add +0.
     const T bin = (T)gs::bc_u(a.t + l);
-    V2 gl = lane == 0 ? V2{bin, (T)0} : V2{(T)0, (T)0};
-    V2 gr = (a.gr && lane == 63) ? V2{bin, (T)0} : V2{(T)0, (T)0};
+    const V2 gl = lane == 0 ? V2{bin, (T)0} : V2{(T)0, (T)0};
+    const V2 gr = (a.gr && lane == 63) ? V2{bin, (T)0} : V2{(T)0, (T)0};
     const T bout = (T)gs::bc_u(a.t + l + 1);
 #pragma unroll
     for (int j = 0; j < C::per_wave(l); ++j) {
@@ -199,11 +185,6 @@ __global__ __launch_bounds__(64 * C::NW, 1) void k_block(const typename C::V2* _
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const V2 c = row[k + 1];
-        if (l == 0) {  // stored level-0 ghosts of this row (LDS broadcast reads)
-          const V2 L0 = xg[0][pz][ry + k], R0v = xg[1][pz][ry + k];
-          gl = lane == 0 ? L0 : V2{(T)0, (T)0};
-          gr = (a.gr && lane == 63) ? R0v : V2{(T)0, (T)0};
-        }
         V2 yz = (row[k] + row[k + 2]) + pm[k];
         if (a.gr) yz = yz + gr;
         V2 A{lane_pair_sum_add<false>(c.x, yz.x), lane_pair_sum_add<false>(c.y, yz.y)};
@@ -252,11 +233,12 @@ bool run_block(const void* s, void* d, const FusedArgs& a0, const gs::Params& p,
   }
 }
 
-// whether k_block can run this launch: the whole interior (no z-runs / store mask / reserve),
+// whether k_block can run this launch: one Backend::fused() allows (its x ghosts are the
+// boundary values ensure_bc wrote), the whole interior (no z-runs / store mask / reserve),
 // whole non-periodic x rows of at most 64 cells, a 32-bit Philox counter
 inline bool block_supported(const FusedArgs& a) {
   const Geom& g = a.g;
-  return !g.periodic && g.nx <= 64 && g.ox == 0 && g.nx == g.Lx && a.q32 && a.zlo[0] == 0 &&
+  return a.allow_block && !g.periodic && g.nx <= 64 && g.ox == 0 && g.nx == g.Lx && a.q32 && a.zlo[0] == 0 &&
          a.zlen[0] == g.nz && a.zlen[1] == 0 && a.mx0 == 0 && a.mx1 == g.nx && a.my0 == 0 &&
          a.my1 == g.ny && a.reserve == 0;
 }

@@ -58,6 +58,9 @@ struct FusedArgs {
   // planes of run 0 then run 1 (nzv = zlen[0] + zlen[1] units per tile)
   int32_t zlo[2], zlen[2];
   int32_t nzv;
+  // the small-grid block kernel may serve this launch (Backend::fused(), and the autotuner's
+  // timing of it): its level-0 x ghosts are then the engine's ensure_bc values (block.hpp)
+  int32_t allow_block;
 };
 
 template <typename T> struct PairT;
@@ -940,9 +943,10 @@ template <typename T>
 bool launch_fused(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, const Geom& g,
                   const gs::Params& p, int n, int64_t t, hipStream_t st, int cfg = -1,
                   int sched = -1, int zlo0 = 0, int zlen0 = -1, int zlo1 = 0, int zlen1 = 0,
-                  int reserve = 0, int mask = 0) {
+                  int reserve = 0, int mask = 0, bool allow_block = false) {
   if (!fused_supported(g, n)) return false;
   FusedArgs a{};
+  a.allow_block = allow_block ? 1 : 0;
   if (zlen0 < 0) zlen0 = g.nz;
   if (zlen1 <= 0) zlen1 = 0;
   if (zlen0 <= 0 || zlo0 < 0 || zlo0 + zlen0 > g.nz || (zlen1 && (zlo1 < 0 || zlo1 + zlen1 > g.nz)))

@@ -48,15 +48,11 @@ def update(c, s, w, fc):
     return out
 
 
-def global_step(u, v, t, L, fc, xghost=None):
-    """One step of the whole L^3 domain in k_fused's operation order.  xghost: optional
-    (u_left, v_left, u_right, v_right) x-face ghost planes (z, y) instead of the boundary value."""
+def global_step(u, v, t, L, fc):
+    """One step of the whole L^3 domain in k_fused's operation order."""
     b = f32(bc_u(t))
     up = np.pad(u, 1, constant_values=b)
     vp = np.pad(v, 1, constant_values=f32(0))
-    if xghost is not None:
-        up[1:-1, 1:-1, 0], vp[1:-1, 1:-1, 0] = xghost[0], xghost[1]
-        up[1:-1, 1:-1, -1], vp[1:-1, 1:-1, -1] = xghost[2], xghost[3]
     s = []
     for a in (up, vp):
         c = a[1:-1, 1:-1, 1:-1]
@@ -100,7 +96,6 @@ def block_pass(ustore, vstore, geo, t, TL, BY, BZ, fc):
         by, bz = bid % nby, bid // nby
         y0, z0 = yb + by * BY, bz * BZ
         buf = np.full((2, 2, NP, NR, 64), np.nan, dtype=f32)  # [level parity][u/v]...
-        xg = np.full((2, 2, NP, NR), np.nan, dtype=f32)  # level-0 x ghosts [left/right][u/v]
         NL = BY + 2 * TL
         for i in range(NP * NL):
             pz, ry = i // NL, R0 - TL + (i % NL)
@@ -113,13 +108,6 @@ def block_pass(ustore, vstore, geo, t, TL, BY, BZ, fc):
                 assert xs.max() < ustore.shape[2]
                 val[0, ok] = ustore[z + H, y + H, xs]
                 val[1, ok] = vstore[z + H, y + H, xs]
-                xg[0, :, pz, ry] = ustore[z + H, y + H, xo - 1], vstore[z + H, y + H, xo - 1]
-                if nx == 64:
-                    xg[1, :, pz, ry] = ustore[z + H, y + H, xo + nx], vstore[z + H, y + H, xo + nx]
-                else:
-                    xg[1, :, pz, ry] = 0
-            else:
-                xg[:, :, pz, ry] = 0
             buf[0, :, pz, ry] = val
         NZR = R0 - TL
         for i in range(NP * (2 * NZR + 2)):
@@ -128,7 +116,6 @@ def block_pass(ustore, vstore, geo, t, TL, BY, BZ, fc):
                 r = j if j < NZR else NR - 2 * NZR + j
                 assert 0 <= r < NR
                 buf[0, :, pz, r] = 0
-                xg[:, :, pz, r] = 0
             else:
                 buf[1, :, pz, 0 if j == 2 * NZR else NR - 1] = 0
         for lv in range(TL):
@@ -154,11 +141,6 @@ def block_pass(ustore, vstore, geo, t, TL, BY, BZ, fc):
                 gz = oz + z
                 words = philox_words(oy + qy, gz, lane, L, t + lv)
                 for k in range(4):
-                    if lv == 0:  # the stored level-0 ghosts of this row
-                        gl = [np.where(lane == 0, xg[0, i, pz, ry + k], f32(0)).astype(f32)
-                              for i in range(2)]
-                        gr = [np.where((lane == 63) & (nx == 64), xg[1, i, pz, ry + k],
-                                       f32(0)).astype(f32) for i in range(2)]
                     c = [row[0, k + 1], row[1, k + 1]]
                     s = []
                     for i in range(2):
@@ -188,7 +170,7 @@ def block_pass(ustore, vstore, geo, t, TL, BY, BZ, fc):
     return out_u, out_v
 
 
-def storage(gu, gv, geo, t, xghost=None):
+def storage(gu, gv, geo, t):
     """Sub-domain storage with H ghosts: neighbours' cells where the global grid has them, the
     boundary value of time t outside it (engine.h ensure_bc), x rows padded like gs::make_geom."""
     nx, ny, nz, H, oy, oz, L = (geo[k] for k in ("nx", "ny", "nz", "H", "oy", "oz", "L"))
@@ -196,9 +178,6 @@ def storage(gu, gv, geo, t, xghost=None):
     px = ((xo + nx + H + 7) // 8) * 8
     gpu = np.pad(gu, H, constant_values=f32(bc_u(t)))
     gpv = np.pad(gv, H, constant_values=f32(0))
-    if xghost is not None:  # x-face ghosts that are not boundary values (raw kernel calls)
-        gpu[H:-H, H:-H, H - 1], gpv[H:-H, H:-H, H - 1] = xghost[0], xghost[1]
-        gpu[H:-H, H:-H, H + L], gpv[H:-H, H:-H, H + L] = xghost[2], xghost[3]
     us = np.full((nz + 2 * H, ny + 2 * H, px), 7.0, dtype=f32)  # row padding: arbitrary
     vs = np.full_like(us, 7.0)
     us[:, :, xo - H:xo + nx + H] = gpu[oz:oz + nz + 2 * H, oy:oy + ny + 2 * H, :]
@@ -207,7 +186,6 @@ def storage(gu, gv, geo, t, xghost=None):
     return us, vs, geo
 
 
-@pytest.mark.parametrize("perturb", [False, True])
 @pytest.mark.parametrize("L,TL,BY,BZ,sub", [
     (16, 2, 8, 2, None), (16, 3, 4, 4, None), (14, 3, 8, 1, None), (18, 2, 4, 1, None),
     # sub-domains with y / z neighbours (oy not a multiple of 4: a partial first quad)
@@ -215,21 +193,17 @@ def storage(gu, gv, geo, t, xghost=None):
     # x rows filling the wave (nx = 64: lane 63 adds the +x ghost), at / away from the boundary
     (64, 3, 8, 2, (22, 8, 30, 4)), (64, 2, 4, 1, (0, 8, 60, 4)),
 ])
-def test_block_model_matches_global_steps(L, TL, BY, BZ, sub, perturb):
+def test_block_model_matches_global_steps(L, TL, BY, BZ, sub):
     fc = fold()
     u0, v0 = random_fields((L, L, L), seed=3, dtype=np.float32)
     u0, v0 = u0.astype(f32), v0.astype(f32)
     t = 4
-    xgh = None
-    if perturb:  # stored level-0 x ghosts that are not the boundary value of time t
-        r = np.random.default_rng(5)
-        xgh = [r.random((L, L), dtype=np.float32) for _ in range(4)]
     gu, gv = u0, v0
     for s in range(TL):
-        gu, gv = global_step(gu, gv, t + s, L, fc, xghost=xgh if s == 0 else None)
+        gu, gv = global_step(gu, gv, t + s, L, fc)
     oy, ny, oz, nz = sub if sub else (0, L, 0, L)
     geo = dict(nx=L, ny=ny, nz=nz, H=3, oy=oy, oz=oz, L=L)
-    us, vs, geo = storage(u0, v0, geo, t, xghost=xgh)
+    us, vs, geo = storage(u0, v0, geo, t)
     bu, bv = block_pass(us, vs, geo, t, TL, BY, BZ, fc)
     np.testing.assert_array_equal(bu, gu[oz:oz + nz, oy:oy + ny, :])
     np.testing.assert_array_equal(bv, gv[oz:oz + nz, oy:oy + ny, :])

@@ -128,8 +128,10 @@ def test_auto_depth_is_measured_single_rank():
 def test_block_kernel_raw_pass_reads_stored_ghosts(L, k, step):
     """A raw fused pass (the timing / overlap-test primitive gs_fused_runs_raw) runs without the
     engine's ensure_bc, so the stored x ghosts need not be the boundary value of the pass's time
-    (here: the init's u = 1 ghosts at an odd step).  k_fused reads them from the buffer; so must
-    k_block -- one pass of each, bit for bit, on a non-cubic domain."""
+    (here: the init's u = 1 ghosts at an odd step).  k_fused reads them from the buffer; k_block
+    takes them to be the boundary value (it costs 5-10 % at L=64 to read them,
+    profiles/r3_block.txt), so only Backend::fused() -- always after ensure_bc -- may launch it:
+    a raw pass with a block shape pinned runs k_fused and matches it bit for bit."""
     from grayscott_amd.ops import native
     outs = []
     try:
