@@ -9,16 +9,18 @@
 // 1-2 planes, so a pass is that fill chain's latency (~1.3 us per iteration, profiles/
 // r3_small_grid.txt: 9.5 us per T=2 pass, 55k MLUPS) while the chip's VALU work is ~0.6 us.
 // Here a workgroup owns an output block of whole x rows x BY rows x BZ planes, loads the block's
-// level-0 input (BY+10 rows x BZ+2T planes, independent loads: one memory latency) into LDS,
-// computes the T levels from LDS into LDS (ping-pong buffers, one barrier per level; each wave
-// takes whole 4-row noise quads, so one Philox draw serves 4 cells as in k_fused), and writes
-// the last level straight to HBM.  The intermediate levels are recomputed on the block's halo
-// (the dependency cone), which costs 2-4x the useful cell updates -- cheap at this size, where
-// the chip is otherwise idle.
+// level-0 dependency cone (BY+2T rows x BZ+2T planes, every load in flight at once: one memory
+// latency, with the Philox words of all its items drawn meanwhile) into LDS, computes the T
+// levels from LDS into LDS (ping-pong buffers, one barrier per level; each wave takes whole 4-row
+// noise quads, so one Philox draw serves 4 cells as in k_fused), and writes the last level
+// straight to HBM.  The intermediate levels are recomputed on the block's halo (the dependency
+// cone), which costs 2-4x the useful cell updates -- cheap at this size, where the chip is
+// otherwise idle (L=64: 55k -> 81k MLUPS, profiles/r3_block.txt).
 //
 // Scope: x rows fit one wave (nx <= 64) and both x faces are the global (non-periodic)
 // boundary, so no x halo is computed: a level's x ghost is the boundary value of its time level
-// (engine.h ensure_bc for level 0, the k_fused reset rule for the others) and enters the
+// (engine.h ensure_bc for level 0 -- so only Backend::fused(), always called after it, launches
+// k_block: FusedArgs.allow_block -- the k_fused reset rule for the others) and enters the
 // x-neighbour sum of lane 0 / lane 63 as an exact correction (below).  y / z faces may have
 // neighbours (their halos are H >= T deep, as for k_fused).
 //
