@@ -2,6 +2,7 @@
 // CPU backend: OpenMP implementation of every backend op.  It is both the `backend = "CPU"`
 // solver (reference: Simulation_CPU.jl:14-133, Threads.@threads over z) and the golden
 // model the gfx950 kernels are tested against.  Same Philox noise stream as the GPU.
+#include <emmintrin.h>
 #include <omp.h>
 #include <string.h>
 
@@ -14,6 +15,53 @@ namespace {
 
 using gs::Box;
 using gs::Geom;
+
+// One row of fp32 cell updates, two cells (u0 v0 u1 v1) per SSE2 vector.  The operations and
+// their order are those of gs::gs_update on each cell -- plain IEEE adds and multiplies (no FMA:
+// x86-64's baseline has none), so the result is bit-identical to the scalar loop below, which
+// also handles the last odd cell and fp64.  i: float index of the row's first cell, n: cells,
+// r: the cells' noise draws (or null).
+inline void row_update_f32(const float* s, float* d, int64_t i, int n, int64_t sy, int64_t sz,
+                           const gs::Coef<float>& c, const float* r) {
+  const __m128 k6 = _mm_setr_ps(c.Du6, c.Dv6, c.Du6, c.Dv6);
+  const __m128 kd = _mm_setr_ps(c.Du, c.Dv, c.Du, c.Dv);
+  const __m128 sg = _mm_setr_ps(-1.f, 1.f, -1.f, 1.f);
+  const __m128 kf = _mm_setr_ps(c.F, -c.Fk, c.F, -c.Fk);  // u: F * (1 - u), v: -(Fk * v)
+  const __m128 kn = _mm_set1_ps(c.noise);
+  const __m128 dt = _mm_set1_ps(c.dt);
+  const __m128 one = _mm_set1_ps(1.f);
+  const __m128 um = _mm_castsi128_ps(_mm_setr_epi32(-1, 0, -1, 0));  // u lanes
+  int x = 0;
+  for (; x + 2 <= n; x += 2, i += 4) {
+    const __m128 cc = _mm_loadu_ps(s + i);
+    const __m128 sum = _mm_add_ps(
+        _mm_add_ps(_mm_add_ps(_mm_loadu_ps(s + i - 2), _mm_loadu_ps(s + i + 2)),
+                   _mm_add_ps(_mm_loadu_ps(s + i - sy), _mm_loadu_ps(s + i + sy))),
+        _mm_add_ps(_mm_loadu_ps(s + i - sz), _mm_loadu_ps(s + i + sz)));
+    const __m128 uu = _mm_shuffle_ps(cc, cc, _MM_SHUFFLE(2, 2, 0, 0));
+    const __m128 vv = _mm_shuffle_ps(cc, cc, _MM_SHUFFLE(3, 3, 1, 1));
+    const __m128 uvv = _mm_mul_ps(_mm_mul_ps(uu, vv), vv);
+    __m128 dd = _mm_sub_ps(_mm_mul_ps(k6, sum), _mm_mul_ps(kd, cc));
+    dd = _mm_add_ps(dd, _mm_mul_ps(sg, uvv));
+    const __m128 pf = _mm_or_ps(_mm_and_ps(um, _mm_sub_ps(one, cc)), _mm_andnot_ps(um, cc));
+    dd = _mm_add_ps(dd, _mm_mul_ps(kf, pf));
+    // the u lanes add noise * r (noise * 0 without a draw, as gs_update does); v lanes keep dd
+    const __m128 rr = r ? _mm_setr_ps(r[x], 0.f, r[x + 1], 0.f) : _mm_setzero_ps();
+    const __m128 dn = _mm_add_ps(dd, _mm_mul_ps(kn, rr));
+    dd = _mm_or_ps(_mm_and_ps(um, dn), _mm_andnot_ps(um, dd));
+    _mm_storeu_ps(d + i, _mm_add_ps(cc, _mm_mul_ps(dd, dt)));
+  }
+  for (; x < n; ++x, i += 2) {
+    const float u = s[i], v = s[i + 1];
+    const float su = (s[i - 2] + s[i + 2]) + (s[i - sy] + s[i + sy]) + (s[i - sz] + s[i + sz]);
+    const float sv = (s[i - 1] + s[i + 3]) + (s[i - sy + 1] + s[i + sy + 1]) +
+                     (s[i - sz + 1] + s[i + sz + 1]);
+    float uo, vo;
+    gs::gs_update<float>(c, u, v, su, sv, r ? r[x] : 0.f, uo, vo);
+    d[i] = uo;
+    d[i + 1] = vo;
+  }
+}
 
 template <typename T>
 class CpuBackend final : public gs::Backend {
@@ -74,6 +122,7 @@ class CpuBackend final : public gs::Backend {
 #pragma omp parallel
     {
       gs::U4* cache = new gs::U4[R.nx > 0 ? R.nx : 1];
+      float* rrow = new float[R.nx > 0 ? R.nx : 1];
 #pragma omp for schedule(static)
       for (int z = R.z0; z < R.z0 + R.nz; ++z) {
         int64_t gz = g.oz + z;
@@ -89,6 +138,14 @@ class CpuBackend final : public gs::Backend {
             }
           }
           const int64_t base = 2 * gs::lin(g, 0, y, z);
+          if constexpr (sizeof(T) == 4) {
+            if (noise)
+              for (int x = 0; x < R.nx; ++x)
+                rrow[x] = gs::uniform_pm1<float>(gs::u4_get(cache[x], (int)(gy & 3)));
+            row_update_f32(s, d, base + 2 * (int64_t)R.x0, R.nx, sy, sz, c,
+                           noise ? rrow : nullptr);
+            continue;
+          }
           for (int x = R.x0; x < R.x0 + R.nx; ++x) {
             const int64_t i = base + 2 * (int64_t)x;
             const T u = s[i], v = s[i + 1];
@@ -105,6 +162,7 @@ class CpuBackend final : public gs::Backend {
         }
       }
       delete[] cache;
+      delete[] rrow;
     }
   }
 
