@@ -188,7 +188,7 @@ class HipBackend final : public gs::Backend {
     // inner box (slots left free), the z end slabs (short, latency-bound) -- gets its own tuned
     // tile shape / schedule; the whole interior keeps the choice made for it.
     int c = cfg_[n], sc = sched_[n];
-    const int reserve = leave_room ? overlap_reserve() : 0;
+    const int reserve = leave_room ? kOverlapReserve : 0;
     const bool whole = zlo0 == 0 && zlen0 == g_.nz && zlen1 <= 0 && mask == 0 && reserve == 0;
     if (!whole && !pin) {
       const PartChoice& pc =
@@ -859,12 +859,9 @@ class HipBackend final : public gs::Backend {
   // workgroup slots the inner part of an overlapped pass leaves free, so the communication
   // kernels (RCCL's, pack / unpack) start beside it (0-16 equal within noise, 64 slower:
   // profiles/r2_overlap_reserve.txt)
+  // workgroup slots the overlapped inner launch leaves free for the comm chain: 16, 48 and 96
+  // measured equal after the cell-granular split (profiles/r3_overlap_reserve.txt)
   static constexpr int kOverlapReserve = 16;
-  // EXPERIMENT (round 3, to be folded into the constant): GS_OVERLAP_RESERVE overrides it
-  static int overlap_reserve() {
-    static const int r = getenv("GS_OVERLAP_RESERVE") ? atoi(getenv("GS_OVERLAP_RESERVE")) : kOverlapReserve;
-    return r;
-  }
   Geom g_;
   gs::Params p_;
   hipStream_t stream_;
