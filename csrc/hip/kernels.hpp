@@ -140,7 +140,7 @@ constexpr int kPackItems = 4;
 // the total cell count matters: one workgroup row per message at the largest message's size
 // launched ~20k mostly empty workgroups for a 256^3 rank and took ~10 us per pack / unpack.
 // one workgroup's kPackItems x 256 cells: workgroup `blk` of the prefix table
-template <typename T, bool PACK>
+template <typename T, bool PACK, int ITEMS = kPackItems>
 __device__ __forceinline__ void pack_block(typename Vec2<T>::type* __restrict__ f, const Geom& g,
                                            const PackArgs& a, int blk, bool poison) {
   int m = 0;
@@ -151,12 +151,12 @@ __device__ __forceinline__ void pack_block(typename Vec2<T>::type* __restrict__ 
   // (the 64-bit divisions dominated this kernel)
   const uint32_t n = (uint32_t)gs::box_cells(b);
   const uint32_t bnx = (uint32_t)b.nx, bny = (uint32_t)b.ny;
-  const uint32_t base = (uint32_t)(blk - a.b0[m]) * (256u * kPackItems) + threadIdx.x;
-  // all loads first (kPackItems in flight per lane), then the stores
-  typename Vec2<T>::type c[kPackItems];
-  int64_t jj[kPackItems];
+  const uint32_t base = (uint32_t)(blk - a.b0[m]) * (256u * ITEMS) + threadIdx.x;
+  // all loads first (ITEMS in flight per lane), then the stores
+  typename Vec2<T>::type c[ITEMS];
+  int64_t jj[ITEMS];
 #pragma unroll
-  for (int k = 0; k < kPackItems; ++k) {
+  for (int k = 0; k < ITEMS; ++k) {
     const uint32_t i = base + 256u * k;
     const uint32_t r = i / bnx;
     const int x = (int)(i - r * bnx);
@@ -167,7 +167,7 @@ __device__ __forceinline__ void pack_block(typename Vec2<T>::type* __restrict__ 
     if (!PACK && poison) c[k].x = c[k].y = __builtin_nan("");
   }
 #pragma unroll
-  for (int k = 0; k < kPackItems; ++k) {
+  for (int k = 0; k < ITEMS; ++k) {
     const uint32_t i = base + 256u * k;
     if (i < n) {
       if (PACK) p[i] = c[k];
@@ -176,18 +176,18 @@ __device__ __forceinline__ void pack_block(typename Vec2<T>::type* __restrict__ 
   }
 }
 
-template <typename T, bool PACK>
+template <typename T, bool PACK, int ITEMS = kPackItems>
 __global__ __launch_bounds__(256) void k_pack(typename Vec2<T>::type* __restrict__ f,
                                               Geom g, PackArgs a) {
   // a timed-out IPC wait: poison the ghosts (wave-uniform load of a device word)
   const bool poison = !PACK && a.err && __hip_atomic_load(a.err, __ATOMIC_RELAXED,
                                                           __HIP_MEMORY_SCOPE_AGENT) != 0;
-  pack_block<T, PACK>(f, g, a, (int)blockIdx.x, poison);
+  pack_block<T, PACK, ITEMS>(f, g, a, (int)blockIdx.x, poison);
   if (PACK && a.fence) __builtin_amdgcn_s_waitcnt(0);
 }
 
 // msgs[i]'s packed cells live at ptrs[i] (any mix of local and peer-mapped buffers)
-template <typename T, bool PACK>
+template <typename T, bool PACK, int ITEMS = kPackItems>
 void launch_pack_ptrs(typename Vec2<T>::type* f, typename Vec2<T>::type* const* ptrs,
                       const Geom& g, const gs::HaloMsg* msgs, int n, hipStream_t st,
                       bool fence = false, const int* err = nullptr) {
@@ -201,11 +201,11 @@ void launch_pack_ptrs(typename Vec2<T>::type* f, typename Vec2<T>::type* const* 
     a.ptr[i] = ptrs[i];
     a.b0[i] = nb;
     const int64_t c = gs::box_cells(msgs[i].box);
-    nb += (int32_t)std::max<int64_t>(1, (c + 256 * kPackItems - 1) / (256 * kPackItems));
+    nb += (int32_t)std::max<int64_t>(1, (c + 256 * ITEMS - 1) / (256 * ITEMS));
   }
   a.b0[n] = nb;
   if (nb == 0) return;
-  k_pack<T, PACK><<<dim3(nb, 1, 1), 256, 0, st>>>(f, g, a);
+  k_pack<T, PACK, ITEMS><<<dim3(nb, 1, 1), 256, 0, st>>>(f, g, a);
 }
 
 // msgs[i]'s packed cells at buf + msgs[i].offset (the plan's send / receive buffer layout)
