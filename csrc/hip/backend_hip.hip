@@ -682,13 +682,9 @@ class HipBackend final : public gs::Backend {
     V2* ptrs[gs::kMaxMsgs];
     for (int i = 0; i < p.nrecv; ++i)
       ptrs[i] = (recv_peer_[i] < 0 ? recv_ : landing_ + slot * landing_cells_) + p.recv[i].offset;
-    // EXPERIMENT (round 3): GS_UNPACK_ITEMS=16 -- more loads in flight per lane from the
-    // uncached landing buffer (the unpack is latency-bound beside the inner launch)
-    static const int items = getenv("GS_UNPACK_ITEMS") ? atoi(getenv("GS_UNPACK_ITEMS")) : 4;
-    if (items >= 16)
-      gsk::launch_pack_ptrs<T, false, 16>(buf_[b], ptrs, g_, p.recv, p.nrecv, xs_, false, ipc_dflag_);
-    else
-      gsk::launch_pack_ptrs<T, false>(buf_[b], ptrs, g_, p.recv, p.nrecv, xs_, false, ipc_dflag_);
+    // 4 cells per lane: 16 (more loads in flight from the uncached landing buffer) measured
+    // no better, overlapped or not (profiles/r3_unpack_items.txt)
+    gsk::launch_pack_ptrs<T, false>(buf_[b], ptrs, g_, p.recv, p.nrecv, xs_, false, ipc_dflag_);
     HIP_CHECK(hipGetLastError());
   }
 
