@@ -35,14 +35,11 @@ struct BlockArgs {
   int32_t gr;   // nx == 64: no lane holds the +x ghost; lane 63 adds it explicitly
 };
 
-template <typename T_, int TL_, int BY_, int BZ_, int NW_, bool NOISE_, int HR_ = 4>
+template <typename T_, int TL_, int BY_, int BZ_, int NW_, bool NOISE_>
 struct BCfg {
   using T = T_;
   using V2 = typename PairT<T>::type;
   static constexpr int TL = TL_, BY = BY_, BZ = BZ_, NW = NW_;
-  // rows per work item: a whole 4-row noise quad, or half of one (HR = 2: twice the items, so
-  // the levels' items spread over more waves; the quad's Philox draw is made for each half)
-  static constexpr int HR = HR_, S = 4 / HR_;
   static constexpr bool NOISE = NOISE_;
   // LDS rows: local y0-5 .. y0+BY+4 (intermediate levels compute the quads [y0-4, y0+BY+4) and
   // read one row beyond); LDS planes z0-T .. z0+BZ+T-1
@@ -53,11 +50,11 @@ struct BCfg {
   // whether the two level buffers fit the CU's LDS (run_block falls back to k_fused if not)
   static constexpr bool FITS = LDS_BYTES <= 160 * 1024;
   static_assert(BY % 4 == 0, "blocks hold whole noise quads");
-  // level l+1's work items (HR rows of a noise quad, plane): intermediate levels one quad of
-  // halo on each side in y and TL-1-l planes in z; each wave takes items wave, wave + NW, ...
+  // level l+1's work items (noise quad, plane): intermediate levels one quad of halo on each
+  // side in y and TL-1-l planes in z; each wave takes items wave, wave + NW, ...
   static constexpr int nq(int l) { return BY / 4 + (l + 1 < TL ? 2 : 0); }
   static constexpr int npl(int l) { return BZ + 2 * (TL - 1 - l); }
-  static constexpr int items(int l) { return nq(l) * S * npl(l); }
+  static constexpr int items(int l) { return nq(l) * npl(l); }
   static constexpr int per_wave(int l) { return (items(l) + NW - 1) / NW; }
   static constexpr int JMAX = per_wave(0);
 };
@@ -85,7 +82,7 @@ __global__ __launch_bounds__(64 * C::NW, 1) void k_block(const typename C::V2* _
   }
   const T ar31 = f.ar * (T)4.656612873077392578125e-10;
   const uint32_t Ly4 = (uint32_t)((g.Ly + 3) >> 2);
-  uint32_t W[TL][C::JMAX][C::HR];  // noise words per (level, item of this wave, row)
+  gs::U4 W[TL][C::JMAX];  // noise words per (level, item of this wave)
 
   // level 0: the outputs' dependency cone, rows y0-T .. y0+BY+T-1 of every plane.  Rows /
   // planes outside the storage (beyond the H-deep ghosts) and lanes past the row's last ghost
@@ -120,20 +117,12 @@ __global__ __launch_bounds__(64 * C::NW, 1) void k_block(const typename C::V2* _
         for (int j = 0; j < C::per_wave(l); ++j) {
           const int it = wave + j * NW;
           if (it < C::items(l)) {
-            const int zi = it / (C::nq(l) * C::S), rem = it - zi * (C::nq(l) * C::S);
-            const int qi = rem / C::S, h = rem - qi * C::S;
+            const int zi = it / C::nq(l), qi = it - zi * C::nq(l);
             const int qy = y0 - (l + 1 < TL ? 4 : 0) + 4 * qi;
             const int z = z0 - (TL - 1 - l) + zi;
             const uint32_t gy4 = (uint32_t)((g.oy + qy) >> 2);
             const uint32_t qu = (uint32_t)g.Lx * (gy4 + Ly4 * (uint32_t)(g.oz + z));
-            const gs::U4 q =
-                philox_dev<true>(qu + (uint32_t)(g.ox + lane), 0u, (uint64_t)(a.t + l), seed);
-            if constexpr (C::HR == 4) {
-              W[l][j][0] = q.x; W[l][j][1] = q.y; W[l][j][2] = q.z; W[l][j][3] = q.w;
-            } else {  // the half's two words (h is wave-uniform)
-              W[l][j][0] = h == 0 ? q.x : q.z;
-              W[l][j][1] = h == 0 ? q.y : q.w;
-            }
+            W[l][j] = philox_dev<true>(qu + (uint32_t)(g.ox + lane), 0u, (uint64_t)(a.t + l), seed);
           }
         }
       }
@@ -177,28 +166,26 @@ __global__ __launch_bounds__(64 * C::NW, 1) void k_block(const typename C::V2* _
     for (int j = 0; j < C::per_wave(l); ++j) {
       const int it = wave + j * NW;
       if (it >= C::items(l)) break;  // wave-uniform
-      constexpr int HR = C::HR;
-      const int zi = it / (nq * C::S), rem = it - zi * (nq * C::S);
-      const int qi = rem / C::S, h = rem - qi * C::S;
-      // local y of the item's first row (a quad starts at a multiple of 4 in global y)
-      const int qy = y0 - 4 * mq + 4 * qi + h * HR;
+      const int zi = it / nq, qi = it - zi * nq;
+      const int qy = y0 - 4 * mq + 4 * qi;  // local y of the quad's first row
       const int z = z0 - dz + zi;
       const int pz = z - (z0 - TL);
       const int ry = qy - y0 + C::R0;
-      V2 row[HR + 2], pm[HR], pp[HR];
+      V2 row[6], pm[4], pp[4];
 #pragma unroll
-      for (int k = 0; k < HR + 2; ++k) row[k] = lds_load2(&in[pz][ry - 1 + k][lane]);
+      for (int k = 0; k < 6; ++k) row[k] = lds_load2(&in[pz][ry - 1 + k][lane]);
 #pragma unroll
-      for (int k = 0; k < HR; ++k) {
+      for (int k = 0; k < 4; ++k) {
         pm[k] = lds_load2(&in[pz - 1][ry + k][lane]);
         pp[k] = lds_load2(&in[pz + 1][ry + k][lane]);
       }
       const int64_t gz = g.oz + z;
       // k_fused's counter gx + Lx * (gy4 + Ly4 * gz) (fits 32 bits: host check), drawn above
+      const gs::U4 blk = C::NOISE ? W[l][j] : gs::U4{0, 0, 0, 0};
       const bool zout = gz < 0 || gz >= g.Lz;
       const bool xout = g.ox + lane >= g.Lx;
 #pragma unroll
-      for (int k = 0; k < HR; ++k) {
+      for (int k = 0; k < 4; ++k) {
         const V2 c = row[k + 1];
         V2 yz = (row[k] + row[k + 2]) + pm[k];
         if (a.gr) yz = yz + gr;
@@ -210,7 +197,10 @@ __global__ __launch_bounds__(64 * C::NW, 1) void k_block(const typename C::V2* _
         V2 P = __builtin_elementwise_fma(f.kd, uvv, kc);
         P = __builtin_elementwise_fma(f.ks, sum, P);
         P = __builtin_elementwise_fma(f.kcc, c, P);
-        if constexpr (C::NOISE) P.x = fma(ar31, (T)(int32_t)W[l][j][k], P.x);
+        if constexpr (C::NOISE) {
+          const uint32_t w = k == 0 ? blk.x : (k == 1 ? blk.y : (k == 2 ? blk.z : blk.w));
+          P.x = fma(ar31, (T)(int32_t)w, P.x);
+        }
         const int y = qy + k;
         if (!last) {
           const int64_t gy = g.oy + y;

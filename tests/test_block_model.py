@@ -80,7 +80,7 @@ def philox_words(gy, gz, gx, L, tstep):
     return philox4x32_10(q, np.zeros_like(q), st & np.uint64(M), st >> np.uint64(32), SEED)
 
 
-def block_pass(ustore, vstore, geo, t, TL, BY, BZ, fc, HR=4):
+def block_pass(ustore, vstore, geo, t, TL, BY, BZ, fc):
     """k_block over a sub-domain: storage arrays (pz, py, px) with H ghosts, x at offset xo."""
     nx, ny, nz, H, xo, oy, oz, L = (geo[k] for k in ("nx", "ny", "nz", "H", "xo", "oy", "oz",
                                                       "L"))
@@ -128,22 +128,19 @@ def block_pass(ustore, vstore, geo, t, TL, BY, BZ, fc, HR=4):
             b_in, b_out = f32(bc_u(t + lv)), f32(bc_u(t + lv + 1))
             gl = [np.where(lane == 0, b_in, f32(0)).astype(f32), np.zeros(64, f32)]
             gr = [np.where((lane == 63) & (nx == 64), b_in, f32(0)).astype(f32), np.zeros(64, f32)]
-            S = 4 // HR  # work items per noise quad (HR rows each)
-            for it in range(nq * S * npl):
-                zi, rem = it // (nq * S), it % (nq * S)
-                qi, h = rem // S, rem % S
-                qq = y0 - 4 * mq + 4 * qi  # the quad's first row
-                qy = qq + h * HR           # the item's first row
+            for it in range(nq * npl):
+                zi, qi = it // nq, it % nq
+                qy = y0 - 4 * mq + 4 * qi
                 z = z0 - dz + zi
                 pz = z - (z0 - TL)
                 ry = qy - y0 + R0
-                assert 1 <= pz <= NP - 2 and 1 <= ry and ry + HR < NR
-                row = buf[inb, :, pz, ry - 1:ry + HR + 1]
-                pm = buf[inb, :, pz - 1, ry:ry + HR]
-                pp = buf[inb, :, pz + 1, ry:ry + HR]
+                assert 1 <= pz <= NP - 2 and 1 <= ry and ry + 4 < NR
+                row = buf[inb, :, pz, ry - 1:ry + 5]
+                pm = buf[inb, :, pz - 1, ry:ry + 4]
+                pp = buf[inb, :, pz + 1, ry:ry + 4]
                 gz = oz + z
-                words = philox_words(oy + qq, gz, lane, L, t + lv)[h * HR:h * HR + HR]
-                for k in range(HR):
+                words = philox_words(oy + qy, gz, lane, L, t + lv)
+                for k in range(4):
                     c = [row[0, k + 1], row[1, k + 1]]
                     s = []
                     for i in range(2):
@@ -189,7 +186,6 @@ def storage(gu, gv, geo, t):
     return us, vs, geo
 
 
-@pytest.mark.parametrize("HR", [4, 2])
 @pytest.mark.parametrize("L,TL,BY,BZ,sub", [
     (16, 2, 8, 2, None), (16, 3, 4, 4, None), (14, 3, 8, 1, None), (18, 2, 4, 1, None),
     # sub-domains with y / z neighbours (oy not a multiple of 4: a partial first quad)
@@ -197,7 +193,7 @@ def storage(gu, gv, geo, t):
     # x rows filling the wave (nx = 64: lane 63 adds the +x ghost), at / away from the boundary
     (64, 3, 8, 2, (22, 8, 30, 4)), (64, 2, 4, 1, (0, 8, 60, 4)),
 ])
-def test_block_model_matches_global_steps(L, TL, BY, BZ, sub, HR):
+def test_block_model_matches_global_steps(L, TL, BY, BZ, sub):
     fc = fold()
     u0, v0 = random_fields((L, L, L), seed=3, dtype=np.float32)
     u0, v0 = u0.astype(f32), v0.astype(f32)
@@ -208,6 +204,6 @@ def test_block_model_matches_global_steps(L, TL, BY, BZ, sub, HR):
     oy, ny, oz, nz = sub if sub else (0, L, 0, L)
     geo = dict(nx=L, ny=ny, nz=nz, H=3, oy=oy, oz=oz, L=L)
     us, vs, geo = storage(u0, v0, geo, t)
-    bu, bv = block_pass(us, vs, geo, t, TL, BY, BZ, fc, HR)
+    bu, bv = block_pass(us, vs, geo, t, TL, BY, BZ, fc)
     np.testing.assert_array_equal(bu, gu[oz:oz + nz, oy:oy + ny, :])
     np.testing.assert_array_equal(bv, gv[oz:oz + nz, oy:oy + ny, :])
