@@ -14,7 +14,7 @@
 // levels from LDS into LDS (ping-pong buffers, one barrier per level; each wave takes whole 4-row
 // noise quads, so one Philox draw serves 4 cells as in k_fused), and writes the last level
 // straight to HBM.  The intermediate levels are recomputed on the block's halo (the dependency
-// cone), which costs 2-4x the useful cell updates -- cheap at this size, where the chip is
+// cone), which costs 2.5-3.7x the useful cell updates -- cheap at this size, where the chip is
 // otherwise idle (L=64: 55k -> 81k MLUPS, profiles/r3_block.txt).
 //
 // Scope: x rows fit one wave (nx <= 64) and both x faces are the global (non-periodic)
