@@ -35,12 +35,14 @@ struct BlockArgs {
   int32_t gr;   // nx == 64: no lane holds the +x ghost; lane 63 adds it explicitly
 };
 
-template <typename T_, int TL_, int BY_, int BZ_, int NW_, bool NOISE_>
+template <typename T_, int TL_, int BY_, int BZ_, int NW_, bool NOISE_, bool KV_ = false>
 struct BCfg {
   using T = T_;
   using V2 = typename PairT<T>::type;
   static constexpr int TL = TL_, BY = BY_, BZ = BZ_, NW = NW_;
   static constexpr bool NOISE = NOISE_;
+  // Philox round keys 4-10 held in VGPRs (filled once) instead of rebuilt on the SALU per draw
+  static constexpr bool KV = KV_;
   // LDS rows: local y0-5 .. y0+BY+4 (intermediate levels compute the quads [y0-4, y0+BY+4) and
   // read one row beyond); LDS planes z0-T .. z0+BZ+T-1
   static constexpr int R0 = 5;
@@ -83,6 +85,16 @@ __global__ __launch_bounds__(64 * C::NW, 1) void k_block(const typename C::V2* _
   const T ar31 = f.ar * (T)4.656612873077392578125e-10;
   const uint32_t Ly4 = (uint32_t)((g.Ly + 3) >> 2);
   gs::U4 W[TL][C::JMAX];  // noise words per (level, item of this wave)
+  uint32_t kv[C::KV ? 14 : 1];
+  if constexpr (C::KV) {
+#pragma unroll
+    for (int r = 3; r < 10; ++r) {
+      const uint32_t k0 = (uint32_t)seed + (uint32_t)r * kPhW0;
+      const uint32_t k1 = (uint32_t)(seed >> 32) + (uint32_t)r * kPhW1;
+      asm volatile("v_mov_b32 %0, %1" : "=v"(kv[2 * (r - 3)]) : "s"(k0));
+      asm volatile("v_mov_b32 %0, %1" : "=v"(kv[2 * (r - 3) + 1]) : "s"(k1));
+    }
+  }
 
   // level 0: the outputs' dependency cone, rows y0-T .. y0+BY+T-1 of every plane.  Rows /
   // planes outside the storage (beyond the H-deep ghosts) and lanes past the row's last ghost
@@ -122,7 +134,8 @@ __global__ __launch_bounds__(64 * C::NW, 1) void k_block(const typename C::V2* _
             const int z = z0 - (TL - 1 - l) + zi;
             const uint32_t gy4 = (uint32_t)((g.oy + qy) >> 2);
             const uint32_t qu = (uint32_t)g.Lx * (gy4 + Ly4 * (uint32_t)(g.oz + z));
-            W[l][j] = philox_dev<true>(qu + (uint32_t)(g.ox + lane), 0u, (uint64_t)(a.t + l), seed);
+            W[l][j] = philox_dev<true, C::KV>(qu + (uint32_t)(g.ox + lane), 0u,
+                                               (uint64_t)(a.t + l), seed, kv);
           }
         }
       }
