@@ -35,13 +35,14 @@ struct BlockArgs {
   int32_t gr;   // nx == 64: no lane holds the +x ghost; lane 63 adds it explicitly
 };
 
-template <typename T_, int TL_, int BY_, int BZ_, int NW_, bool NOISE_, bool KV_ = false>
+template <typename T_, int TL_, int BY_, int BZ_, int NW_, bool NOISE_, bool KV_ = true>
 struct BCfg {
   using T = T_;
   using V2 = typename PairT<T>::type;
   static constexpr int TL = TL_, BY = BY_, BZ = BZ_, NW = NW_;
   static constexpr bool NOISE = NOISE_;
-  // Philox round keys 4-10 held in VGPRs (filled once) instead of rebuilt on the SALU per draw
+  // Philox round keys 4-10 held in VGPRs (filled once) instead of rebuilt on the SALU per draw:
+  // L=64 T=3 83.5k vs 80.3k MLUPS, T=2 77.6k vs 72.3k (in-process A/B, profiles/r3_block.txt)
   static constexpr bool KV = KV_;
   // LDS rows: local y0-5 .. y0+BY+4 (intermediate levels compute the quads [y0-4, y0+BY+4) and
   // read one row beyond); LDS planes z0-T .. z0+BZ+T-1
