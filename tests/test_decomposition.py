@@ -168,3 +168,21 @@ def test_random_init_is_decomposition_invariant(world, L):
     un, vn, _ = run_ranks(world, cfgn)
     np.testing.assert_array_equal(un, u1)
     np.testing.assert_array_equal(vn, v1)
+
+
+def test_default_fuse_policy():
+    """Steps per pass when fuse_steps = 0 (models/grayscott.py default_fuse): one rank without
+    neighbours gets 3 ghost layers and lets the engine measure the depth; with neighbours the
+    depth follows the plane size (T=3 from 160^2 x-y planes, fp32 and fp64 alike since round 3,
+    profiles/r3_f64_depth.txt); the CPU backend steps one at a time."""
+    from grayscott_amd.models.grayscott import default_fuse
+
+    assert default_fuse("hip", init_domain(64, 1, 0)) == 3
+    assert default_fuse("hip", init_domain(64, 1, 0), "float64") == 3
+    assert default_fuse("hip", init_domain(2, 1, 0)) == 2  # capped by the sub-domain extent
+    big = init_domain(512, 8, 0, dims=[2, 2, 2])
+    small = init_domain(128, 8, 0, dims=[2, 2, 2])
+    for dt in ("float32", "float64"):
+        assert default_fuse("hip", big, dt) == 3
+        assert default_fuse("hip", small, dt) == 2
+    assert default_fuse("cpu", init_domain(64, 1, 0)) == 1
