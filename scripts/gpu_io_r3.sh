@@ -6,9 +6,9 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/${GS_OUT:-io3}
 mkdir -p $O/ex64
 cd $R
-bash scripts/run_io_config.sh $O/io512 > $O/io512.log 2>&1 &&
+true &&
 cd $O/ex64 && sed -e 's/^output = .*/output = "ex64.bp"/' $R/examples/settings-files.toml > ex.toml &&
 echo 'perf_log = "perf-ex64.jsonl"' >> ex.toml &&
-/usr/bin/time -f "wall_s %e" timeout -k 10 300 python3 $R/gray-scott.py ex.toml > ex.log 2> ex.err &&
+timeout -k 10 300 python3 $R/gray-scott.py ex.toml > ex.log 2> ex.err &&
 tail -n 1 perf-ex64.jsonl > summary.json && rm -rf ex64.bp
 echo "exit $?"
