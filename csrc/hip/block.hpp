@@ -35,7 +35,8 @@ struct BlockArgs {
   int32_t gr;   // nx == 64: no lane holds the +x ghost; lane 63 adds it explicitly
 };
 
-template <typename T_, int TL_, int BY_, int BZ_, int NW_, bool NOISE_, bool KV_ = true>
+template <typename T_, int TL_, int BY_, int BZ_, int NW_, bool NOISE_, bool KV_ = true,
+          bool LH_ = false>
 struct BCfg {
   using T = T_;
   using V2 = typename PairT<T>::type;
@@ -44,6 +45,9 @@ struct BCfg {
   // Philox round keys 4-10 held in VGPRs (filled once) instead of rebuilt on the SALU per draw:
   // L=64 T=3 83.5k vs 80.3k MLUPS, T=2 77.6k vs 72.3k (in-process A/B, profiles/r3_block.txt)
   static constexpr bool KV = KV_;
+  // the last level's items are half quads (2 rows): it has only BY/4 x BZ quads, so whole-quad
+  // items leave most waves idle there; the halves' Philox draws happen in the load shadow
+  static constexpr bool LH = LH_;
   // LDS rows: local y0-5 .. y0+BY+4 (intermediate levels compute the quads [y0-4, y0+BY+4) and
   // read one row beyond); LDS planes z0-T .. z0+BZ+T-1
   static constexpr int R0 = 5;
@@ -57,10 +61,22 @@ struct BCfg {
   // side in y and TL-1-l planes in z; each wave takes items wave, wave + NW, ...
   static constexpr int nq(int l) { return BY / 4 + (l + 1 < TL ? 2 : 0); }
   static constexpr int npl(int l) { return BZ + 2 * (TL - 1 - l); }
-  static constexpr int items(int l) { return nq(l) * npl(l); }
+  static constexpr int S(int l) { return (LH && l + 1 == TL) ? 2 : 1; }  // items per quad
+  static constexpr int items(int l) { return nq(l) * S(l) * npl(l); }
   static constexpr int per_wave(int l) { return (items(l) + NW - 1) / NW; }
   static constexpr int JMAX = per_wave(0);
 };
+
+// f(std::integral_constant<int, 0>), ..., f(std::integral_constant<int, N-1>): per-level code
+// with the level as a compile-time constant (array extents and trip counts depend on it)
+template <class F, int... I>
+__device__ __forceinline__ void for_levels_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void for_levels(F&& f) {
+  for_levels_impl(f, std::make_integer_sequence<int, N>{});
+}
 
 template <class C>
 __global__ __launch_bounds__(64 * C::NW, 1) void k_block(const typename C::V2* __restrict__ s,
@@ -124,22 +140,25 @@ __global__ __launch_bounds__(64 * C::NW, 1) void k_block(const typename C::V2* _
     // the noise words of every item this wave will compute, at every level, while the loads
     // are in flight (they depend on the cell and the step only)
     if constexpr (C::NOISE) {
-#pragma unroll
-      for (int l = 0; l < TL; ++l) {
+      for_levels<TL>([&](auto LC) {
+        constexpr int l = decltype(LC)::value;
 #pragma unroll
         for (int j = 0; j < C::per_wave(l); ++j) {
           const int it = wave + j * NW;
           if (it < C::items(l)) {
-            const int zi = it / C::nq(l), qi = it - zi * C::nq(l);
+            constexpr int S = C::S(l);
+            const int zi = it / (C::nq(l) * S), rem = it - zi * (C::nq(l) * S);
+            const int qi = rem / S, h = rem - qi * S;
             const int qy = y0 - (l + 1 < TL ? 4 : 0) + 4 * qi;
             const int z = z0 - (TL - 1 - l) + zi;
             const uint32_t gy4 = (uint32_t)((g.oy + qy) >> 2);
             const uint32_t qu = (uint32_t)g.Lx * (gy4 + Ly4 * (uint32_t)(g.oz + z));
-            W[l][j] = philox_dev<true, C::KV>(qu + (uint32_t)(g.ox + lane), 0u,
-                                               (uint64_t)(a.t + l), seed, kv);
+            const gs::U4 q = philox_dev<true, C::KV>(qu + (uint32_t)(g.ox + lane), 0u,
+                                                     (uint64_t)(a.t + l), seed, kv);
+            W[l][j] = (S == 1 || h == 0) ? q : gs::U4{q.z, q.w, q.z, q.w};  // a half's words first
           }
         }
-      }
+      });
     }
 #pragma unroll
     for (int j = 0; j < JL; ++j) {
@@ -158,11 +177,11 @@ __global__ __launch_bounds__(64 * C::NW, 1) void k_block(const typename C::V2* _
   }
   __syncthreads();
 
-#pragma unroll
-  for (int l = 0; l < TL; ++l) {
+  for_levels<TL>([&](auto LC) {
+    constexpr int l = decltype(LC)::value;
     const V2(*in)[NR][64] = buf[l & 1];
     V2(*out)[NR][64] = buf[(l + 1) & 1];
-    const bool last = l + 1 == TL;
+    constexpr bool last = l + 1 == TL;
     const int mq = last ? 0 : 1;          // intermediate levels: one quad of halo each side
     const int nq = C::nq(l);
     const int dz = TL - 1 - l;            // planes of halo this level still needs
@@ -180,16 +199,18 @@ __global__ __launch_bounds__(64 * C::NW, 1) void k_block(const typename C::V2* _
     for (int j = 0; j < C::per_wave(l); ++j) {
       const int it = wave + j * NW;
       if (it >= C::items(l)) break;  // wave-uniform
-      const int zi = it / nq, qi = it - zi * nq;
-      const int qy = y0 - 4 * mq + 4 * qi;  // local y of the quad's first row
+      constexpr int S = C::S(l), HR = 4 / S;  // rows per item
+      const int zi = it / (nq * S), rem = it - zi * (nq * S);
+      const int qi = rem / S, h = rem - qi * S;
+      const int qy = y0 - 4 * mq + 4 * qi + HR * h;  // local y of the item's first row
       const int z = z0 - dz + zi;
       const int pz = z - (z0 - TL);
       const int ry = qy - y0 + C::R0;
       V2 row[6], pm[4], pp[4];
 #pragma unroll
-      for (int k = 0; k < 6; ++k) row[k] = lds_load2(&in[pz][ry - 1 + k][lane]);
+      for (int k = 0; k < HR + 2; ++k) row[k] = lds_load2(&in[pz][ry - 1 + k][lane]);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < HR; ++k) {
         pm[k] = lds_load2(&in[pz - 1][ry + k][lane]);
         pp[k] = lds_load2(&in[pz + 1][ry + k][lane]);
       }
@@ -199,7 +220,7 @@ __global__ __launch_bounds__(64 * C::NW, 1) void k_block(const typename C::V2* _
       const bool zout = gz < 0 || gz >= g.Lz;
       const bool xout = g.ox + lane >= g.Lx;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < HR; ++k) {
         const V2 c = row[k + 1];
         V2 yz = (row[k] + row[k + 2]) + pm[k];
         if (a.gr) yz = yz + gr;
@@ -226,7 +247,7 @@ __global__ __launch_bounds__(64 * C::NW, 1) void k_block(const typename C::V2* _
       }
     }
     if (!last) __syncthreads();
-  }
+  });
 }
 
 template <class C>

@@ -799,17 +799,19 @@ inline const FusedCfgEntry* fused_cfg_table(int* n) {
       {"blk8x2w16", true, false},  // 22
       {"blk4x4w16", true, false},  // 23
       {"blk8x4w16", true, false},  // 24  (T=2 only: T=3 levels do not fit the LDS)
+      {"blk8x2w16l", true, false}, // 25  last level in half-quad items
+      {"blk4x4w16l", true, false}, // 26  last level in half-quad items
 #ifdef GS_ABLATION
-      {"4x12:2s-abl1", true, false},  // 25  no barriers
-      {"4x12:2s-abl2", true, false},  // 26  L2-resident loads
-      {"4x12:1s-abl4", true, false},  // 27  Philox keys in VGPRs (exact)
-      {"4x12:2s-abl4", true, false},  // 28  Philox keys in VGPRs (exact)
-      {"4x12:1s-abl8", true, false},  // 29  DPP sums with the s_nop (exact)
-      {"4x12:1s-abl12", true, false}, // 30  abl4 + abl8 (exact)
-      {"4x12:1s-abl16", true, false}, // 31  pipeline fill computes every level (exact)
-      {"4x8:1s-abl16", true, true},   // 32  pipeline fill computes every level (exact)
-      {"4x6:2s-abl16", true, true},   // 33  pipeline fill computes every level (exact)
-      {"4x12:1s-abl32", true, false}, // 34  Philox only on lanes in the x cone (exact)
+      {"4x12:2s-abl1", true, false},  // 27  no barriers
+      {"4x12:2s-abl2", true, false},  // 28  L2-resident loads
+      {"4x12:1s-abl4", true, false},  // 29  Philox keys in VGPRs (exact)
+      {"4x12:2s-abl4", true, false},  // 30  Philox keys in VGPRs (exact)
+      {"4x12:1s-abl8", true, false},  // 31  DPP sums with the s_nop (exact)
+      {"4x12:1s-abl12", true, false}, // 32  abl4 + abl8 (exact)
+      {"4x12:1s-abl16", true, false}, // 33  pipeline fill computes every level (exact)
+      {"4x8:1s-abl16", true, true},   // 34  pipeline fill computes every level (exact)
+      {"4x6:2s-abl16", true, true},   // 35  pipeline fill computes every level (exact)
+      {"4x12:1s-abl32", true, false}, // 36  Philox only on lanes in the x cone (exact)
 #endif
   };
   *n = (int)(sizeof(t) / sizeof(t[0]));
@@ -859,8 +861,8 @@ void run_fused_cfg(const void* s, void* d, const FusedArgs& a, const gs::Params&
       case 16: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
       case 17: FusedLaunch<FCfg<T, TL, 4, 4, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
 #ifdef GS_ABLATION
-      case 32: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
-      case 33: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 34: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 35: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
 #endif
       default: break;
     }
@@ -888,17 +890,19 @@ void run_fused_cfg(const void* s, void* d, const FusedArgs& a, const gs::Params&
       case 22: if (block_supported(a) && run_block<BCfg<T, TL, 8, 2, 16, NZ>>(s, d, a, p, st)) return; break;
       case 23: if (block_supported(a) && run_block<BCfg<T, TL, 4, 4, 16, NZ>>(s, d, a, p, st)) return; break;
       case 24: if (block_supported(a) && run_block<BCfg<T, TL, 8, 4, 16, NZ>>(s, d, a, p, st)) return; break;
+      case 25: if (block_supported(a) && run_block<BCfg<T, TL, 8, 2, 16, NZ, true, true>>(s, d, a, p, st)) return; break;
+      case 26: if (block_supported(a) && run_block<BCfg<T, TL, 4, 4, 16, NZ, true, true>>(s, d, a, p, st)) return; break;
 #ifdef GS_ABLATION
-      case 25: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 1>, T>::run(s, d, a, p, st); return;
-      case 26: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 2>, T>::run(s, d, a, p, st); return;
-      case 27: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;
-      case 28: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;
-      case 29: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 8>, T>::run(s, d, a, p, st); return;
-      case 30: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 12>, T>::run(s, d, a, p, st); return;
-      case 31: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
-      case 32: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
-      case 33: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
-      case 34: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 32>, T>::run(s, d, a, p, st); return;
+      case 27: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 1>, T>::run(s, d, a, p, st); return;
+      case 28: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 2>, T>::run(s, d, a, p, st); return;
+      case 29: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;
+      case 30: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;
+      case 31: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 8>, T>::run(s, d, a, p, st); return;
+      case 32: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 12>, T>::run(s, d, a, p, st); return;
+      case 33: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 34: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 35: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 36: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 32>, T>::run(s, d, a, p, st); return;
 #endif
       default: break;  // 0 and 14: the default shape below
     }

@@ -8,6 +8,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <utility>
 
 #include "gs/common.h"
 
