@@ -61,6 +61,9 @@ def parse_args(argv):
     ap.add_argument("--check", default="auto", choices=["auto", "golden", "none"],
                     help="golden-model check of the timed path (auto: 1 rank, HIP)")
     ap.add_argument("--check-steps", type=int, default=6)
+    ap.add_argument("--profile-passes", type=int, default=10,
+                    help="passes of the per-phase timing window run after the timed region "
+                         "(0 = off)")
     ap.add_argument("--tune-budget", type=float, default=float(os.environ.get("GS_TUNE_BUDGET_S",
                                                                                 "180")),
                     help="seconds for the multi-rank data-path tuning (checks + timing)")
@@ -150,6 +153,68 @@ def golden_check(sim, settings, dom, nsteps: int, init_seed):
     return err if err == err else float("inf")
 
 
+def profile_phases(sim, ctx, passes: int):
+    """Per-phase device timing of ``passes`` passes of this data path, run after
+    the timed region (csrc/include/gs/phase.h: hipEvents in stream order on the compute and
+    communication streams).  Returns (on rank 0) ``{"per_rank": [...], "summary": {...}}``: the
+    summary holds, per phase, the slowest rank's median microseconds per pass, and the slowest
+    rank's pass time, exchange span and critical path; ``accounted`` is the smallest share of a
+    rank's measured pass time that its parts explain."""
+    prof = sim.phase_profile(passes * max(1, int(sim.depth)))
+    rows = ctx.gather_object(prof)
+    if not rows:
+        return None
+    names = sorted(set().union(*(r["phase_us"] for r in rows)))
+    acc = [r["accounted"] for r in rows if r.get("accounted") is not None]
+    gbs = [r["link_GBps"] for r in rows if r.get("link_GBps")]
+    summary = {
+        "passes": rows[0]["passes"], "steps_per_pass": rows[0]["depth"],
+        "transport": rows[0]["transport"], "overlapped": rows[0]["overlapped"],
+        "pass_us": round(max(r["pass_us"] for r in rows), 2),
+        "phase_us": {k: round(max(r["phase_us"].get(k, 0.0) for r in rows), 2) for k in names},
+        "exchange_us": round(max(r["exchange_us"] for r in rows), 2),
+        "critical_us": round(max(r["critical_us"] for r in rows), 2),
+        "accounted": round(min(acc), 3) if acc else None,
+        "bytes_per_neighbour_max": max((max(r["bytes_per_neighbour"].values(), default=0)
+                                        for r in rows), default=0),
+        "link_GBps_min": min(gbs) if gbs else None,
+    }
+    for r in rows:
+        for k in ("window_us", "pass_us", "exchange_us", "critical_us"):
+            r[k] = round(r[k], 2)
+        r["phase_us"] = {k: round(v, 2) for k, v in r["phase_us"].items()}
+    return {"summary": summary, "per_rank": rows}
+
+
+def profile_reference_grid(settings, ctx, args, dims, row, passes: int):
+    """profile_phases on the reference's Dims_create grid with the data path (fuse depth,
+    transport, overlap, engine knobs) its best tuning row used."""
+    import copy
+
+    from grayscott_amd.models.grayscott import GrayScott
+    from grayscott_amd.parallel.autotune import _env
+    from grayscott_amd.parallel.decomp import init_domain
+
+    s = copy.copy(settings)
+    s.fuse_steps, s.transport, s.overlap = row["fuse"], row["transport"], row["overlap"]
+    env = dict(row.get("env", {}))
+    if not row.get("inplace_halos", True):
+        env["GS_INPLACE_HALO"] = "0"
+    with _env(env):
+        dom = init_domain(args.L, ctx.world_size, ctx.rank, periodic=False, dims=dims)
+        sim = GrayScott(s, dom, ctx)
+        try:
+            sim.init_fields()
+            sim.randomize_fields(seed=2024)
+            sim.iterate(4 * max(1, int(sim.depth)))
+            out = profile_phases(sim, ctx, passes)
+        finally:
+            sim.close()
+    if out is not None:
+        out["summary"]["dims"] = list(dims)
+    return out
+
+
 def run(args) -> int:
     import torch
 
@@ -218,6 +283,25 @@ def run(args) -> int:
     elapsed = ctx.allreduce(local, "max")
     stats = sim.global_stats()
     world_info = ctx.gather_object(sim.device_info())
+    phases = None
+    if args.profile_passes > 0:
+        # outside the timed region: the state it advances is reset by the golden check
+        t_prof = time.perf_counter()
+        phases = {"chosen": profile_phases(sim, ctx, args.profile_passes)}
+        if ctx.world_size > 1 and backend == "hip":
+            # the reference's Dims_create grid too, when the tuning chose another data path
+            bal = dims_create(ctx.world_size)
+            if list(dom.dims) != list(bal):
+                rows = [r for r in (tuning or {}).get("table", []) if r["dims"] == bal
+                        and r.get("ok")]
+                phases["reference_grid"] = None
+                if rows:
+                    r = min(rows, key=lambda r: r["ms_per_step"])
+                    phases["reference_grid"] = profile_reference_grid(
+                        settings, ctx, args, bal, r, args.profile_passes)
+            from grayscott_amd.ops import native
+            phases["peer_access"] = native.peer_access_matrix() if ctx.rank == 0 else None
+        phases["profile_s"] = round(time.perf_counter() - t_prof, 2)
     if do_golden:
         t_chk = time.perf_counter()
         err = golden_check(sim, settings, dom, args.check_steps,
@@ -289,6 +373,8 @@ def run(args) -> int:
             "check": {"mean_u": stats["mean_u"], "mean_v": stats["mean_v"],
                       "finite": all(map(lambda x: x == x, stats.values())), **check},
         }
+        if phases is not None:
+            rec["phases"] = phases
         if ref_grid is not None and ctx.world_size == 8 and ref_grid["dims"] == [2, 2, 2]:
             rec["config3_2x2x2"] = ref_grid
         os.write(_JSON_FD, (json.dumps(rec) + "\n").encode())

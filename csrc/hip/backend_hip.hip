@@ -136,6 +136,7 @@ class HipBackend final : public gs::Backend {
     if (ev_join_) (void)hipEventDestroy(ev_join_);
     for (hipEvent_t e : marks_)
       if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : prof_ev_) (void)hipEventDestroy(e);
     if (comm_stream_) (void)hipStreamDestroy(comm_stream_);
   }
 
@@ -286,6 +287,31 @@ class HipBackend final : public gs::Backend {
                      hipSuccess || cus < 1))
       cus = 256;
     return cus;
+  }
+
+  // Per-phase timing (gs/phase.h): one timing event per timestamp, recorded on the stream the
+  // phase is issued to -- halo and overlapped-pass phases follow comm_select, the rest (the
+  // whole-interior kernel, single steps, boundary fills, the window's stamps) run on the
+  // compute stream.  Events are created once and reused by later windows.
+  void prof_reserve(int n) override {
+    while ((int)prof_ev_.size() < n) {
+      hipEvent_t e;
+      HIP_CHECK(hipEventCreate(&e));
+      prof_ev_.push_back(e);
+    }
+    prof_n_ = n;
+  }
+  void prof_mark(int slot, int phase) override {
+    if (slot < 0 || slot >= prof_n_) return;
+    const bool selectable = phase >= gs::kPhPack && phase <= gs::kPhShell;
+    HIP_CHECK(hipEventRecord(prof_ev_[slot], selectable ? xs_ : stream_));
+  }
+  void prof_times(double* us, int n) override {
+    for (int i = 0; i < n; ++i) {
+      float ms = 0.f;
+      if (i > 0 && i < prof_n_) HIP_CHECK(hipEventElapsedTime(&ms, prof_ev_[0], prof_ev_[i]));
+      us[i] = 1e3 * (double)ms;
+    }
   }
 
   bool has_comm_stream() const override { return comm_stream_ != nullptr; }
@@ -662,10 +688,10 @@ class HipBackend final : public gs::Backend {
     HIP_CHECK(hipGetLastError());
   }
 
-  // the engine calls unpack on the stream of the same exchange's pack, with nothing between
-  // them on that stream, so the 'ready' signal is issued here, fused with the wait
-  void ipc_unpack(int b, const gs::HaloPlan& p) {
-    const int64_t slot = (int64_t)(xn_ & 1);
+  // The transport step of an IPC exchange (native_exchange): the engine issues it on the stream
+  // of the same exchange's pack, after it, so the 'ready' signal (this rank's stores into the
+  // peers have completed) is published here, fused with the wait for the peers' signals.
+  void ipc_signal_wait() {
     if (!send_peers_.empty() || !recv_peers_.empty()) {
       gsk::IpcFlags s{}, w{};
       for (int idx : send_peers_) {
@@ -678,7 +704,13 @@ class HipBackend final : public gs::Backend {
       }
       gsk::k_ipc_signal_wait<<<1, 64, 0, xs_>>>(s, w, ipc_ticks_, ipc_err_dev_, ipc_dflag_,
                                                 ipc_emulate_ticks_);
+      HIP_CHECK(hipGetLastError());
     }
+  }
+
+  // after ipc_signal_wait on the same stream: the peers' messages have landed in slot xn_ & 1
+  void ipc_unpack(int b, const gs::HaloPlan& p) {
+    const int64_t slot = (int64_t)(xn_ & 1);
     V2* ptrs[gs::kMaxMsgs];
     for (int i = 0; i < p.nrecv; ++i)
       ptrs[i] = (recv_peer_[i] < 0 ? recv_ : landing_ + slot * landing_cells_) + p.recv[i].offset;
@@ -737,7 +769,11 @@ class HipBackend final : public gs::Backend {
   }
 
   bool native_exchange(const gs::HaloPlan& p) override {
-    if (ipc_) return true;  // the IPC pack already stored every message at its peer
+    if (ipc_) {
+      // the IPC pack already stored every message at its peer: signal and wait
+      ipc_signal_wait();
+      return true;
+    }
     if (!comm_) return false;
     NCCL_CHECK(ncclGroupStart());
     for (int i = 0; i < p.nsend; ++i) {
@@ -874,6 +910,8 @@ class HipBackend final : public gs::Backend {
   hipEvent_t ev_ = nullptr;
   hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
   hipEvent_t marks_[4] = {nullptr, nullptr, nullptr, nullptr};
+  std::vector<hipEvent_t> prof_ev_;  // per-phase timing events (prof_reserve)
+  int prof_n_ = 0;
   hipStream_t comm_stream_ = nullptr;
   hipStream_t xs_ = nullptr;  // stream for halo traffic (compute or comm stream)
   bool inplace_off_ = getenv("GS_INPLACE_HALO") && atoi(getenv("GS_INPLACE_HALO")) == 0;
@@ -1018,6 +1056,21 @@ int gs_ipc_peers(gs_engine* e, int32_t dtype, int32_t* out, int32_t cap) {
     g_gs_err = ex.what();
     return -1;
   }
+}
+
+// Peer-access matrix of the devices this process sees: out[i * n + j] = 1 if device i can
+// access device j's memory (hipDeviceCanAccessPeer; the diagonal is 1).  Returns n, or -1.
+int gs_peer_access(int32_t* out, int32_t cap) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return -1;
+  if (n * n > cap) return -1;
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) {
+      int can = i == j ? 1 : 0;
+      if (i != j && hipDeviceCanAccessPeer(&can, i, j) != hipSuccess) can = -1;
+      out[i * n + j] = can;
+    }
+  return n;
 }
 
 // PCI bus id of the current HIP device ("0000:05:00.0"); returns its length or -1

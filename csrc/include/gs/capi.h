@@ -44,6 +44,12 @@ int gs_stats(gs_engine* e, double* out6);
 int gs_randomize(gs_engine* e, uint64_t seed, double lo, double hi);
 int gs_set_transport(gs_engine* e, int (*fn)(void*), void* user);
 int gs_drop_transport(gs_engine* e);  // forget RCCL / IPC / callback transport (fallback)
+// per-phase timing window (gs/phase.h): summary of gs_prof_len() doubles
+int gs_prof_len(void);
+int gs_phase_count(void);
+const char* gs_phase_name(int32_t i);
+int gs_prof_start(gs_engine* e, int32_t max_records);
+int gs_prof_stop(gs_engine* e, double* out);  // 0 ok, 1 records dropped, -1 error
 // halo plan introspection: counts and per-message (dir, peer, offset, cells)
 int gs_plan_info(gs_engine* e, int64_t* send_cells, int64_t* recv_cells, int32_t* nsend, int32_t* nrecv);
 int gs_plan_msg(gs_engine* e, int32_t which, int32_t i, int64_t* out4);

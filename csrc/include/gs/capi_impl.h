@@ -116,6 +116,24 @@ int gs_set_transport(gs_engine* e, int (*fn)(void*), void* user) {
 }
 int gs_drop_transport(gs_engine* e) { GS_TRY(e->eng->drop_transport()) }
 
+// Per-phase timing window (gs/phase.h): gs_prof_start(e, max_records) ... steps ...
+// gs_prof_stop(e, out) waits for the device and writes gs_prof_len() doubles (layout:
+// gs/phase.h kProfHead, then {median us, intervals per pass} per phase in gs_phase_name order).
+// gs_prof_stop returns 1 if the window had more records than max_records, 0, or -1 on error.
+int gs_prof_len(void) { return gs::kProfLen; }
+int gs_phase_count(void) { return gs::kNumPhases; }
+const char* gs_phase_name(int32_t i) { return gs::phase_name(i); }
+int gs_prof_start(gs_engine* e, int32_t max_records) { GS_TRY(e->eng->prof_start(max_records)) }
+int gs_prof_stop(gs_engine* e, double* out) {
+  static const double timeout = getenv("GS_COMM_TIMEOUT") ? atof(getenv("GS_COMM_TIMEOUT")) : 900.0;
+  try {
+    return e->eng->prof_stop(out, timeout);
+  } catch (const std::exception& ex) {
+    g_gs_err = ex.what();
+    return -1;
+  }
+}
+
 int gs_plan_info(gs_engine* e, int64_t* sc, int64_t* rc, int32_t* ns, int32_t* nr) {
   const gs::HaloPlan& p = e->eng->plan();
   *sc = p.send_cells; *rc = p.recv_cells; *ns = p.nsend; *nr = p.nrecv;

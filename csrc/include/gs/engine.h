@@ -13,10 +13,13 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <chrono>
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 #include "gs/common.h"
+#include "gs/phase.h"
 #include "gs/trace.h"
 
 namespace gs {
@@ -108,6 +111,24 @@ class Backend {
   virtual void seed(int b) = 0;
   // sum / min / max of u and v over the interior: out[6]
   virtual void stats(int b, double* out) = 0;
+
+  // Per-phase timing (gs/phase.h).  prof_reserve: room for n timestamps; prof_mark: take
+  // timestamp `slot` in stream order on the stream the phase's work is issued to (phase -1: the
+  // compute stream); prof_times: all n timestamps in microseconds from a common origin, once
+  // the work has finished.  The default is the host clock, exact for a synchronous backend.
+  virtual void prof_reserve(int n) { host_us_.assign((size_t)n, 0.0); }
+  virtual void prof_mark(int slot, int phase) {
+    (void)phase;
+    if (slot >= 0 && (size_t)slot < host_us_.size())
+      host_us_[(size_t)slot] = std::chrono::duration<double, std::micro>(
+                                   std::chrono::steady_clock::now().time_since_epoch()).count();
+  }
+  virtual void prof_times(double* us, int n) {
+    for (int i = 0; i < n; ++i) us[i] = (size_t)i < host_us_.size() ? host_us_[(size_t)i] : 0.0;
+  }
+
+ private:
+  std::vector<double> host_us_;
 };
 
 struct EngineConfig {
@@ -170,6 +191,26 @@ class Engine {
            g.nz >= 2 * k + 1 && g.nx >= 2 * k + 1 && g.ny >= 2 * k + 1;
   }
   double comm_calls() const { return (double)ncomm_; }
+
+  // Per-phase timing window (gs/phase.h): from prof_start on, every phase of every
+  // pass is bracketed by two timestamps in stream order (at most max_records in all);
+  // prof_stop waits for the device (watchdog: timeout_s) and writes the summary, kProfLen
+  // doubles.  Returns 1 if records were dropped (window too long for max_records), else 0.
+  void prof_start(int max_records) {
+    plog_.start((size_t)(max_records < 4 ? 4 : max_records));
+    be_->prof_reserve((int)plog_.cap);
+    pm(-1, true);  // the window's start, on the compute stream
+  }
+  int prof_stop(double* out, double timeout_s) {
+    if (!plog_.on) throw std::runtime_error("prof_stop without prof_start");
+    pm(-1, false);  // every pass ends joined to the compute stream
+    plog_.on = false;
+    be_->wait_all(timeout_s);
+    std::vector<double> t(plog_.recs.size(), 0.0);
+    if (!t.empty()) be_->prof_times(t.data(), (int)t.size());
+    summarize(plog_, t.data(), out);
+    return plog_.overflow ? 1 : 0;
+  }
 
   // Reference init (Simulation_CPU.jl:14-65): u = 1 everywhere (ghosts included), v = 0,
   // u_temp = v_temp = 0, then the 13^3 seed cube.
@@ -238,10 +279,16 @@ class Engine {
     TraceRange tr("gs.exchange_start");
     xpending_ = kNone;
     if (!has_nbr_) return;
-    if (plan_.zplanes && has_remote_ && be_->native_exchange_inplace(cur_, plan_)) {
-      ++ncomm_;
-      return;  // nothing to unpack
+    if (plan_.zplanes && has_remote_ && be_->can_exchange_inplace(plan_)) {
+      pm(kPhTransport, true);
+      const bool done = be_->native_exchange_inplace(cur_, plan_);
+      pm(kPhTransport, false);
+      if (done) {
+        ++ncomm_;
+        return;  // nothing to unpack
+      }
     }
+    pm(kPhPack, true);
     be_->pack(cur_, plan_);
     // self messages (periodic wrap onto the same rank)
     bool remote = false;
@@ -256,13 +303,17 @@ class Engine {
         remote = true;
       }
     }
+    pm(kPhPack, false);
     xpending_ = kUnpack;
     if (remote) {
       ++ncomm_;
+      const bool native = be_->has_native_transport();
+      if (native) pm(kPhTransport, true);
       if (!be_->native_exchange(plan_)) {
         if (!tfn_) throw std::runtime_error("halo exchange needs a transport (RCCL or callback)");
         xpending_ = kCallback;
       }
+      if (native) pm(kPhTransport, false);
     }
   }
 
@@ -271,11 +322,17 @@ class Engine {
     TraceRange tr("gs.exchange_finish");
     if (xpending_ == kCallback) {
       be_->host_sync();
+      pm(kPhTransport, true);
       if (tfn_(tuser_) != 0) throw std::runtime_error("transport callback failed");
+      pm(kPhTransport, false);
       // the callback's device copies were issued on the compute stream
       if (on_comm) be_->comm_fork();
     }
-    if (xpending_ != kNone) be_->unpack(cur_, plan_);
+    if (xpending_ != kNone) {
+      pm(kPhUnpack, true);
+      be_->unpack(cur_, plan_);
+      pm(kPhUnpack, false);
+    }
     xpending_ = kNone;
   }
 
@@ -304,7 +361,11 @@ class Engine {
         *c = H;
         faces[nf++] = bx;
       }
-    if (nf) be_->fill_boxes(b, faces, nf, u, 0.0);
+    if (nf) {
+      pm(kPhBc, true);
+      be_->fill_boxes(b, faces, nf, u, 0.0);
+      pm(kPhBc, false);
+    }
     bc_parity_[b] = par;
   }
 
@@ -328,12 +389,13 @@ class Engine {
     while (nsteps > 0) {
       const int k = (int)(nsteps < kmax ? nsteps : kmax);
       const int oth = 1 - cur_;
-      if (nsteps >= 2 * (int64_t)k && chained(k)) {
+      if (nsteps >= 2 * (int64_t)k && chained(k)) {  // (its passes are counted inside)
         const int64_t npass = nsteps / k;
         advance_chained(k, npass);
         nsteps -= npass * k;
         continue;
       }
+      plog_.begin_pass(k);
       if (overlapped(k)) {
         // One overlapped pass: the inner part (overlap_split) needs no halo, so it runs on
         // the compute stream while the exchange is in flight on the comm stream; the end
@@ -369,7 +431,10 @@ class Engine {
       if (k > 1 && cfg_.use_fused) {
         ensure_bc(cur_, t_);
         TraceRange tr("gs.fused");
-        if (be_->fused(cur_, oth, k, t_)) {
+        pm(kPhFused, true);
+        const bool done = be_->fused(cur_, oth, k, t_);
+        pm(kPhFused, false);
+        if (done) {
           cur_ = oth;
           t_ += k;
           nsteps -= k;
@@ -380,7 +445,9 @@ class Engine {
         ensure_bc(cur_, t_);
         const Box r = pass_region(cfg_.g, cfg_.nbr, k, s);
         TraceRange tr("gs.step");
+        pm(kPhStep, true);
         be_->step(cur_, 1 - cur_, r, t_);
+        pm(kPhStep, false);
         cur_ = 1 - cur_;
         ++t_;
       }
@@ -417,6 +484,7 @@ class Engine {
     be_->comm_fork();
     for (int64_t p = 0; p < npass; ++p) {
       const int oth = 1 - cur_;
+      plog_.begin_pass(k);
       be_->comm_select(true);
       exchange_start();      // in-place RCCL group, or pack + RCCL group, on the comm stream
       exchange_finish(true);  // (packed plans) unpack
@@ -463,12 +531,25 @@ class Engine {
   // the inner box: all x-y tiles over planes [z0, z1), outputs clipped by the x / y mask,
   // leaving workgroup slots free for the communication kernels that run beside it
   void inner_run(int src, int dst, int k, int64_t t, const Split& sp) {
-    if (sp.z1 > sp.z0) be_->fused_runs(src, dst, k, t, sp.z0, sp.z1 - sp.z0, 0, 0, true, sp.sides & 15);
+    if (sp.z1 <= sp.z0) return;
+    pm(kPhInner, true);
+    be_->fused_runs(src, dst, k, t, sp.z0, sp.z1 - sp.z0, 0, 0, true, sp.sides & 15);
+    pm(kPhInner, false);
   }
   // the shell: the k-deep face slabs, after the halos have landed
   void shell_run(int src, int dst, int k, int64_t t, const Split& sp) {
-    if (sp.sides && !be_->shell(src, dst, k, t, sp.sides))
+    if (!sp.sides) return;
+    pm(kPhShell, true);
+    if (!be_->shell(src, dst, k, t, sp.sides))
       throw std::runtime_error("overlapped pass: the backend has no shell kernel for this depth");
+    pm(kPhShell, false);
+  }
+
+  // a phase timestamp (profiling window only)
+  void pm(int phase, bool begin) {
+    if (!plog_.on) return;
+    const int slot = plog_.next(phase, begin);
+    if (slot >= 0) be_->prof_mark(slot, phase);
   }
 
   EngineConfig cfg_;
@@ -490,6 +571,7 @@ class Engine {
   TransportFn tfn_ = nullptr;
   void* tuser_ = nullptr;
   int64_t ncomm_ = 0;
+  PhaseLog plog_;
 };
 
 }  // namespace gs

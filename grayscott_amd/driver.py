@@ -42,7 +42,7 @@ from .models.grayscott import GrayScott
 from .parallel.decomp import choose_dims, init_domain
 from .parallel.dist import init_from_env
 from .utils.config import Settings, get_settings, load_backend_and_lang
-from .utils.timers import PerfLog, PhaseTimer
+from .utils.timers import DeviceTimer, PerfLog, PhaseTimer
 
 
 def initialization(args: Sequence[str]):
@@ -86,7 +86,9 @@ def _next_event(step: int, settings: Settings) -> int:
 def run(settings: Settings, out=sys.stdout) -> dict:
     ctx, settings, domain, sim = initialize_from_settings(settings)
     rank = ctx.rank
-    timer = PhaseTimer(sync=sim.synchronize)
+    timer = PhaseTimer(sync=sim.synchronize)  # host phases: output, checkpoint, restart
+    # compute intervals: timing events in stream order, nothing synchronised around them
+    dtimer = DeviceTimer(sim.device if sim.backend == "hip" else None)
     perf = PerfLog(settings.perf_log, enabled=(rank == 0))
     fail_at = int(os.environ.get("GS_FAIL_AT_STEP", "-1"))
     raise_at = int(os.environ.get("GS_RAISE_AT_STEP", "-1"))
@@ -112,16 +114,20 @@ def run(settings: Settings, out=sys.stdout) -> dict:
     ckpt = (CheckpointWriter(settings, domain, ctx)
             if ckpt_on and getattr(settings, "async_checkpoint", True) else None)
     t_loop = time.perf_counter()
-    compute_s = 0.0
     cells = float(domain.L[0]) * domain.L[1] * domain.L[2]
+
+    def log_compute(wait: bool = False) -> None:
+        for sec, m in dtimer.completed(wait=wait):
+            perf.write(step=m["step"], steps=m["steps"], compute_s=sec, io_s=m["io_s"],
+                       mlups=cells * m["steps"] / max(sec, 1e-12) / 1e6, ranks=ctx.world_size)
+
     while step < settings.steps:
         nxt = _next_event(step, settings)
-        t0 = time.perf_counter()
-        with timer.phase("compute"):
-            sim.iterate(nxt - step)
-        dt_c = time.perf_counter() - t0
-        compute_s += dt_c
+        tok = dtimer.start()
+        sim.iterate(nxt - step)
         nsteps = nxt - step
+        meta = {"step": nxt, "steps": nsteps, "io_s": 0.0}
+        dtimer.stop(tok, meta)
         step = nxt
         io_s = 0.0
         do_out = settings.plotgap > 0 and step % settings.plotgap == 0
@@ -155,8 +161,8 @@ def run(settings: Settings, out=sys.stdout) -> dict:
                 else:
                     write_checkpoint(settings.checkpoint_output, step, sim, settings, ctx)
             io_s += time.perf_counter() - t1
-        perf.write(step=step, steps=nsteps, compute_s=dt_c, io_s=io_s,
-                   mlups=cells * nsteps / max(dt_c, 1e-12) / 1e6, ranks=ctx.world_size)
+        meta["io_s"] = io_s  # the interval's record is written once its events have completed
+        log_compute()
         if raise_at >= 0 and step >= raise_at and fail_rank in (-1, rank):
             raise RuntimeError(f"injected failure on rank {rank} at step {step} "
                                "(GS_RAISE_AT_STEP)")
@@ -168,12 +174,19 @@ def run(settings: Settings, out=sys.stdout) -> dict:
     if ckpt is not None and ckpt.pending:
         with timer.phase("checkpoint"):
             ckpt.finish()
+    sim.synchronize()
     loop_s = time.perf_counter() - t_loop
+    log_compute(wait=True)
+    compute_s = dtimer.total
     with timer.phase("io_close"):
         stream.close()
     result = {"steps": step, "loop_s": loop_s, "compute_s": compute_s,
               "mlups_compute": cells * (step - first_step) / max(compute_s, 1e-12) / 1e6,
-              "timers": timer.summary(), "ranks": ctx.world_size, "fuse": sim.depth,
+              "timers": {**timer.summary(),
+                         "compute": {"seconds": compute_s, "calls": dtimer.count,
+                                     "clock": "device events" if dtimer.device is not None
+                                     else "host"}},
+              "ranks": ctx.world_size, "fuse": sim.depth,
               "transport": sim.transport}
     perf.write(summary=result)
     perf.close()

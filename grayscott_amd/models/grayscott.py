@@ -236,6 +236,56 @@ class GrayScott:
         if nsteps > 0:
             self.engine.advance(nsteps)
 
+    def halo_bytes(self) -> dict:
+        """Bytes this rank sends to each neighbour rank per halo exchange (every message of the
+        plan: faces, and with H > 1 edges and corners; z-plane plans send whole padded
+        planes)."""
+        itemsize = 4 if self.dtype == "float32" else 8
+        out = {}
+        for m in self.engine.plan()["send"]:
+            if m["peer"] == self.domain.rank and self.transport == "none":
+                continue  # periodic wrap onto this rank: a device copy, not a link
+            out[m["peer"]] = out.get(m["peer"], 0) + 2 * itemsize * m["cells"]
+        return out
+
+    def phase_profile(self, steps: int) -> dict:
+        """Advance ``steps`` steps with every phase of every pass timed in stream order on the
+        device (csrc/include/gs/phase.h): median microseconds per pass of pack,
+        transport, unpack, inner, shell, fused, step and bc, the halo exchange's span and the
+        window's time per pass.  Derived: ``critical_us`` -- the pass's critical path from the
+        parts (overlapped: max(inner, exchange) + shell + bc; otherwise their sum; bc weighted
+        by the share of passes that refill the boundary) -- and
+        ``accounted`` = critical_us / pass_us; ``bytes_per_neighbour`` and the achieved
+        ``link_GBps`` (bytes to the busiest neighbour / the exchange's data time: transport, plus
+        the pack for IPC, whose pack kernel stores straight into the peers)."""
+        depth = max(1, int(self.depth))
+        passes = max(1, -(-int(steps) // depth))
+        self.engine.prof_start(64 * passes + 16)
+        try:
+            self.engine.advance(int(steps))
+        finally:
+            r = self.engine.prof_stop()
+        ph = r["phase_us"]
+        xch = r["exchange_us"]
+        # a phase that runs in some passes only (the boundary refill after a depth change)
+        # counts with its share of the passes
+        bc = ph.get("bc", 0.0) * min(1.0, r["per_pass"].get("bc", 0.0))
+        if "inner" in ph or "shell" in ph:
+            crit = max(ph.get("inner", 0.0), xch) + ph.get("shell", 0.0) + bc
+        else:
+            crit = xch + ph.get("fused", 0.0) + ph.get("step", 0.0) + bc
+        r["critical_us"] = crit
+        r["accounted"] = crit / r["pass_us"] if r["pass_us"] > 0 else None
+        nb = self.halo_bytes()
+        r["bytes_per_neighbour"] = {str(k): v for k, v in sorted(nb.items())}
+        data_us = ph.get("transport", 0.0) + (ph.get("pack", 0.0) if self.transport == "ipc" else 0.0)
+        r["link_GBps"] = (float(f"{max(nb.values()) / (data_us * 1e3):.4g}")
+                          if nb and data_us > 0 else None)
+        r["transport"] = self.transport
+        r["overlapped"] = bool(self.overlapped)
+        r["depth"] = depth
+        return r
+
     @property
     def step(self) -> int:
         return self.engine.step

@@ -133,6 +133,19 @@ def _declare(lib) -> None:
         lib.gs_ipc_connect.restype = c_int
         lib.gs_ipc_peers.argtypes = [c_void_p, c_int32, POINTER(c_int32), c_int32]
         lib.gs_ipc_peers.restype = c_int
+    lib.gs_prof_len.argtypes = []
+    lib.gs_prof_len.restype = c_int
+    lib.gs_phase_count.argtypes = []
+    lib.gs_phase_count.restype = c_int
+    lib.gs_phase_name.argtypes = [c_int32]
+    lib.gs_phase_name.restype = c_char_p
+    lib.gs_prof_start.argtypes = [c_void_p, c_int32]
+    lib.gs_prof_start.restype = c_int
+    lib.gs_prof_stop.argtypes = [c_void_p, POINTER(c_double)]
+    lib.gs_prof_stop.restype = c_int
+    if hasattr(lib, "gs_peer_access"):
+        lib.gs_peer_access.argtypes = [POINTER(c_int32), c_int32]
+        lib.gs_peer_access.restype = c_int
     if hasattr(lib, "gs_fused_choice"):
         lib.gs_fused_choice.argtypes = [c_void_p, c_int32, c_int32, POINTER(c_int32),
                                         POINTER(ctypes.c_float)]
@@ -334,6 +347,31 @@ class Engine:
                                  "cells": int(buf[3])})
         return out
 
+    def prof_start(self, max_records: int) -> None:
+        """Open a per-phase timing window (csrc/include/gs/phase.h): every phase of every pass
+        from now on is bracketed by timestamps in stream order (hipEvents on the GPU)."""
+        self._chk(self.lib.gs_prof_start(self.h, int(max_records)), "prof_start")
+
+    def prof_stop(self) -> dict:
+        """Close the window: wait for the device, return the per-pass phase summary
+        ``{"passes", "steps", "window_us", "pass_us", "exchange_us", "phase_us": {name: median
+        us per pass}, "per_pass": {name: intervals per pass}, "truncated"}`` (phases that did not
+        occur are left out)."""
+        n = int(self.lib.gs_prof_len())
+        out = (c_double * n)()
+        rc = self.lib.gs_prof_stop(self.h, out)
+        if rc < 0:
+            raise RuntimeError(f"prof_stop failed: {last_error(self.lib)}")
+        res = {"passes": int(out[0]), "steps": int(out[1]), "window_us": out[2],
+               "pass_us": out[3], "exchange_us": out[4], "phase_us": {}, "per_pass": {},
+               "truncated": bool(rc == 1)}
+        for i in range(int(self.lib.gs_phase_count())):
+            name = self.lib.gs_phase_name(i).decode()
+            if out[6 + 2 * i] > 0:
+                res["phase_us"][name] = out[5 + 2 * i]
+                res["per_pass"][name] = out[6 + 2 * i]
+        return res
+
     def rccl_init(self, uid: bytes, nranks: int, rank: int):
         if not hasattr(self.lib, "gs_rccl_init"):
             raise RuntimeError("RCCL transport needs the HIP backend")
@@ -398,6 +436,19 @@ def device_pci_bus_id() -> str:
     buf = ctypes.create_string_buffer(64)
     n = lib.gs_device_pci(buf, 64)
     return buf.value.decode() if n > 0 else ""
+
+
+def peer_access_matrix():
+    """hipDeviceCanAccessPeer for every pair of the devices this process sees: an n x n list
+    of 1 / 0 (-1: the query failed); [] without the HIP library."""
+    lib = load("hip")
+    if not hasattr(lib, "gs_peer_access"):
+        return []
+    buf = (c_int32 * (64 * 64))()
+    n = lib.gs_peer_access(buf, 64 * 64)
+    if n < 0:
+        return []
+    return [[int(buf[i * n + j]) for j in range(n)] for i in range(n)]
 
 
 def rccl_unique_id() -> bytes:

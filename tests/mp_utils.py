@@ -49,10 +49,13 @@ def _worker(rank, world, port, outdir, cfg):
         sim.iterate(cfg["steps"])
         u, v = sim.get_fields()
         import json
+        # per-phase timing of a further window (after the fields were taken)
+        prof = sim.phase_profile(cfg["profile_steps"]) if cfg.get("profile_steps") else None
         info = json.dumps(sim.device_info())
         np.savez(os.path.join(outdir, f"rank{rank}.npz"), u=u, v=v, info=info,
                  offsets=np.array(dom.proc_offsets), sizes=np.array(dom.proc_sizes),
                  step=sim.step, transport=sim.transport, overlapped=sim.overlapped,
+                 profile=json.dumps(prof),
                  zplanes=sim.engine.plan()["zplanes"])
         sim.close()
         ctx.barrier()
@@ -88,5 +91,6 @@ def run_ranks(world: int, cfg: dict, timeout: float = 240.0):
             v[sl] = d["v"]
             meta.append({"step": int(d["step"]), "transport": str(d["transport"]),
                          "overlapped": bool(d["overlapped"]), "zplanes": bool(d["zplanes"]),
-                         "info": __import__("json").loads(str(d["info"]))})
+                         "info": __import__("json").loads(str(d["info"])),
+                         "profile": __import__("json").loads(str(d["profile"]))})
         return u, v, meta

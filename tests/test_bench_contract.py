@@ -31,6 +31,9 @@ def test_bench_single_process():
     assert KEYS <= set(d)
     assert d["steps"] == 6 and d["warmup"] == 2 and d["value"] > 0
     assert d["config"]["L"] == 32 and d["check"]["finite"]
+    # the per-phase timing window after the timed region
+    ph = d["phases"]["chosen"]["summary"]
+    assert ph["passes"] == 10 and ph["pass_us"] > 0 and "step" in ph["phase_us"]
 
 
 @pytest.mark.parametrize("decomp", ["z", "balanced"])
@@ -52,6 +55,11 @@ def test_bench_torchrun_two_ranks(decomp):
     # backend runs the golden model's own kernel, so the blocks agree bit for bit
     assert d["check"]["golden_ok"] and d["check"]["max_abs_err"] == 0.0
     assert d["check"]["golden_steps"] == 4
+    ph = d["phases"]["chosen"]
+    assert len(ph["per_rank"]) == 2
+    assert {"pack", "transport", "unpack"} <= set(ph["summary"]["phase_us"])
+    assert ph["summary"]["bytes_per_neighbour_max"] > 0
+    assert ph["summary"]["accounted"] is not None
 
 
 def test_bench_self_launch_two_ranks():
