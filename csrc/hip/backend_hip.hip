@@ -578,7 +578,7 @@ class HipBackend final : public gs::Backend {
     HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev_));
     const double to = getenv("GS_COMM_TIMEOUT") ? atof(getenv("GS_COMM_TIMEOUT")) : 900.0;
     ipc_ticks_ = (uint64_t)(std::max(1.0, to) * (double)std::max(khz, 1) * 1000.0);
-    const double emu = getenv("GS_IPC_EMULATE_US") ? atof(getenv("GS_IPC_EMULATE_US")) : 0.0;
+    const double emu = gs::debug_knobs().ipc_emulate_us;  // modelling only (gs/debug.h)
     ipc_emulate_ticks_ = (uint64_t)(std::max(0.0, emu) * (double)std::max(khz, 1) / 1000.0);
     xn_ = 0;
   }
@@ -940,7 +940,7 @@ class HipBackend final : public gs::Backend {
   int64_t landing_cells_ = 0;
   uint64_t xn_ = 0;  // exchanges issued
   uint64_t ipc_ticks_ = 0;
-  uint64_t ipc_emulate_ticks_ = 0;  // GS_IPC_EMULATE_US: minimum exchange wait (modelling)
+  uint64_t ipc_emulate_ticks_ = 0;  // debug knob ipc_emulate_us: minimum exchange wait (modelling)
   std::vector<PeerMap> peers_;
   std::vector<int> send_peers_, recv_peers_;  // distinct peers (indices into peers_)
   int send_peer_[gs::kMaxMsgs], recv_peer_[gs::kMaxMsgs];

@@ -969,9 +969,9 @@ bool launch_fused(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, co
   if (a.mx1 <= a.mx0 || a.my1 <= a.my0) return false;
   a.g = g;
   a.t = t;
-  // GS_PHILOX_GENERIC=1 forces the 64-bit-counter Philox path (tests: both paths agree bitwise)
-  static const bool generic = getenv("GS_PHILOX_GENERIC") && atoi(getenv("GS_PHILOX_GENERIC")) != 0;
-  a.q32 = (philox_q32(g) && !generic) ? 1 : 0;
+  // debug knob philox_generic (gs/debug.h) forces the 64-bit-counter Philox path (tests: both
+  // paths agree bitwise)
+  a.q32 = (philox_q32(g) && !gs::debug_knobs().philox_generic) ? 1 : 0;
   a.cfg = cfg >= 0 ? cfg : fused_cfg_env();
   a.sched = sched >= 0 ? sched : fused_sched_slot();
   if (zlen1) a.sched = 0;  // two short runs: one workgroup per (tile, run)

@@ -11,6 +11,7 @@
 #include <utility>
 
 #include "gs/common.h"
+#include "gs/debug.h"
 
 namespace gsk {
 
@@ -251,7 +252,7 @@ __device__ __forceinline__ void ipc_poll(const IpcFlags& a, uint64_t t0, uint64_
 
 // signal, then wait, in one launch (the pack -> signal -> wait -> unpack chain of one exchange
 // has one launch fewer); signalling first keeps two ranks waiting on each other deadlock-free
-//   min_ticks > 0 (GS_IPC_EMULATE_US, modelling only): the launch also lasts at least that long,
+//   min_ticks > 0 (debug switch ipc_emulate_us, gs/debug.h; modelling only): the launch also lasts at least that long,
 //   so a one-GPU loopback run can stand in for a slower inter-GPU link when timing overlap
 [[maybe_unused]] static __global__ __launch_bounds__(64) void k_ipc_signal_wait(
     IpcFlags s, IpcFlags w, uint64_t ticks, int* err, int* dflag, uint64_t min_ticks) {

@@ -46,6 +46,7 @@ int gs_set_transport(gs_engine* e, int (*fn)(void*), void* user);
 int gs_drop_transport(gs_engine* e);  // forget RCCL / IPC / callback transport (fallback)
 // per-phase timing window (gs/phase.h): summary of gs_prof_len() doubles
 int gs_prof_len(void);
+int gs_debug_set(const char* name, double value);  // test switches (gs/debug.h)
 int gs_phase_count(void);
 const char* gs_phase_name(int32_t i);
 int gs_prof_start(gs_engine* e, int32_t max_records);

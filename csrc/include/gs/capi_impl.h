@@ -121,6 +121,8 @@ int gs_drop_transport(gs_engine* e) { GS_TRY(e->eng->drop_transport()) }
 // gs/phase.h kProfHead, then {median us, intervals per pass} per phase in gs_phase_name order).
 // gs_prof_stop returns 1 if the window had more records than max_records, 0, or -1 on error.
 int gs_prof_len(void) { return gs::kProfLen; }
+// test / modelling switches (gs/debug.h); 0, or -1 for an unknown name
+int gs_debug_set(const char* name, double value) { return gs::debug_set(name, value); }
 int gs_phase_count(void) { return gs::kNumPhases; }
 const char* gs_phase_name(int32_t i) { return gs::phase_name(i); }
 int gs_prof_start(gs_engine* e, int32_t max_records) { GS_TRY(e->eng->prof_start(max_records)) }

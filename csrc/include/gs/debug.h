@@ -1,0 +1,40 @@
+// SPDX-License-Identifier: MIT
+// Test / modelling switches of the native libraries, set only through the C API
+// (gs_debug_set, grayscott_amd.ops.native.debug_set) -- never from the environment, so a stray
+// variable on a production node cannot change what the shipped kernels do.
+//   overlap_chain   1 (default): full-depth overlapped passes run chained on two streams
+//                   (engine.h advance_chained); 0: one overlapped pass at a time (tests of
+//                   the unchained path).  Read when an engine is created.
+//   philox_generic  0 (default); 1: the fused kernel always takes the 64-bit-counter Philox
+//                   path (tests: it equals the 32-bit one bit for bit).
+//   ipc_emulate_us  0 (default); > 0: every IPC exchange lasts at least this long (modelling a
+//                   slower link on one GPU when timing the overlap).  Read by ipc_export.
+#pragma once
+
+#include <string.h>
+
+namespace gs {
+
+struct DebugKnobs {
+  int overlap_chain = 1;
+  int philox_generic = 0;
+  double ipc_emulate_us = 0.0;
+};
+
+inline DebugKnobs& debug_knobs() {
+  static DebugKnobs k;
+  return k;
+}
+
+// 0 on success, -1 for an unknown knob
+inline int debug_set(const char* name, double value) {
+  DebugKnobs& k = debug_knobs();
+  if (!name) return -1;
+  if (!strcmp(name, "overlap_chain")) k.overlap_chain = value != 0.0 ? 1 : 0;
+  else if (!strcmp(name, "philox_generic")) k.philox_generic = value != 0.0 ? 1 : 0;
+  else if (!strcmp(name, "ipc_emulate_us")) k.ipc_emulate_us = value > 0.0 ? value : 0.0;
+  else return -1;
+  return 0;
+}
+
+}  // namespace gs

@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "gs/common.h"
+#include "gs/debug.h"
 #include "gs/phase.h"
 #include "gs/trace.h"
 
@@ -561,8 +562,8 @@ class Engine {
   int depth_ = 0;  // measured steps per pass (0: cfg_.fuse)
   bool auto_depth_ = false;
   bool loopback_ = false;
-  // GS_OVERLAP_CHAIN=0: run in-place overlapped passes one by one (A/B of advance_chained)
-  bool chain_ = !(getenv("GS_OVERLAP_CHAIN") && atoi(getenv("GS_OVERLAP_CHAIN")) == 0);
+  // debug knob overlap_chain = 0 (tests): overlapped passes one by one (gs/debug.h)
+  bool chain_ = debug_knobs().overlap_chain != 0;
   enum { kNone, kUnpack, kCallback };
   int xpending_ = kNone;
   int cur_ = 0;

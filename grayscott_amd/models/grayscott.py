@@ -12,6 +12,7 @@ memory on MI355X, host memory for the CPU backend) and updated in place by the n
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Tuple
 
 import numpy as np
@@ -118,6 +119,8 @@ class GrayScott:
         kind = (kind or "auto").lower()
         if kind == "auto":
             chain = ["rccl", "torch", "host"] if self.backend == "hip" else ["torch"]
+            if os.environ.get("GS_TUNE_SKIP_RCCL") == "1" and self.backend == "hip":
+                chain = ["torch", "host"]  # RCCL failed to set up earlier in this job (tuning)
             errors = []
             for k in chain:
                 try:

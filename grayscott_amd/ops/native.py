@@ -451,6 +451,18 @@ def peer_access_matrix():
     return [[int(buf[i * n + j]) for j in range(n)] for i in range(n)]
 
 
+def debug_set(name: str, value: float, which: str = "hip") -> None:
+    """Set a test / modelling switch of a native library (csrc/include/gs/debug.h):
+    ``overlap_chain`` (0: overlapped passes one at a time; read at engine creation),
+    ``philox_generic`` (1: the 64-bit-counter Philox path), ``ipc_emulate_us`` (minimum IPC
+    exchange time).  Process-wide; never read from the environment."""
+    lib = load(which)
+    lib.gs_debug_set.argtypes = [ctypes.c_char_p, c_double]
+    lib.gs_debug_set.restype = c_int
+    if lib.gs_debug_set(name.encode(), float(value)) != 0:
+        raise ValueError(f"unknown debug switch {name!r}")
+
+
 def rccl_unique_id() -> bytes:
     lib = load("hip")
     buf = ctypes.create_string_buffer(256)

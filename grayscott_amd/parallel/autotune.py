@@ -168,7 +168,13 @@ def tune_data_path(settings, ctx, L: int, backend: str,
     ``budget_s`` bounds the whole tuning phase: once it is spent (rank 0's clock, agreed by all
     ranks) the remaining candidates are skipped (``"skipped": "budget"`` in the table), but at
     least two are always tried.  Once one candidate's transport passed its check, later
-    candidates do not retry the fallback transports: a failure there is the path's own."""
+    candidates do not retry the fallback transports: a failure there is the path's own.
+
+    Fail fast per transport: once a pinned transport (IPC) fails a candidate's check -- a peer
+    wait that timed out, a mapping error, a mismatch -- every later candidate pinned to it is
+    skipped (``"skipped": "ipc failed: <reason>"``), so a node whose cross-device IPC
+    misbehaves pays its timeout once, not once per IPC row.  Likewise, once RCCL failed to set
+    up, later candidates' fallback chains start after it (``GS_TUNE_SKIP_RCCL``)."""
     from ..models.grayscott import default_fuse
 
     cands = list(cands) if cands is not None else candidates(L, ctx.world_size, backend)
@@ -176,6 +182,7 @@ def tune_data_path(settings, ctx, L: int, backend: str,
     best = None
     t_start = time.perf_counter()
     proven = None  # transport that passed a check on this node
+    failed: Dict[str, str] = {}  # pinned transport -> why it failed on this node
     for ci, cand in enumerate(cands):
         over = budget_s is not None and time.perf_counter() - t_start > budget_s
         if ci >= 2 and ctx.allreduce(1.0 if over else 0.0, "max") > 0:
@@ -198,6 +205,12 @@ def tune_data_path(settings, ctx, L: int, backend: str,
             row["env"] = env0
         if tr0:
             row["transport_req"] = tr0
+        if tr0 and tr0 in failed:
+            # (every rank holds the same `failed`: it is built from agreed results only)
+            row["skipped"] = f"{tr0} failed: {failed[tr0]}"
+            row["ok"] = False
+            table.append(row)
+            continue
         chosen = None
         attempts = [(settings.transport, ov0, {}),
                     (settings.transport, "off", {"GS_INPLACE_HALO": "0"}),
@@ -210,6 +223,9 @@ def tune_data_path(settings, ctx, L: int, backend: str,
             # a fixed transport: no fallback chain; a peer that never signals ends its device
             # waits after 20 s instead of GS_COMM_TIMEOUT
             attempts = [(tr0, ov0, {"GS_COMM_TIMEOUT": "20"})]
+        if "rccl" in failed:
+            # the fallback chain of "auto" starts after RCCL (its set-up failed before)
+            attempts = [(tr, ov, {**extra, "GS_TUNE_SKIP_RCCL": "1"}) for tr, ov, extra in attempts]
         for tr, ov, extra in attempts:
             env = {**env0, **extra}
             with _env(env):
@@ -221,6 +237,13 @@ def tune_data_path(settings, ctx, L: int, backend: str,
                 row.setdefault("check_errors", []).append(
                     f"{tr}: {text}" if text else f"{tr}: max |err| {err:.3g} vs golden")
             ok = ctx.allreduce(1.0 if ok else 0.0, "min") > 0
+            # agreed failure reasons (every rank the same): rank 0's text, or the mismatch
+            why = ctx.broadcast_object((text or f"max |err| {err:.3g} vs golden")[:120], src=0)
+            if not ok and tr0:
+                failed[tr0] = why
+            if not ok and "rccl" in why.lower() and ("init" in why.lower() or
+                                                     "unique" in why.lower()):
+                failed["rccl"] = why
             if ok:
                 chosen = (used, ov, {**env0, **(extra if not tr0 else {})})
                 if not extra and not tr0:

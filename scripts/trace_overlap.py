@@ -27,7 +27,15 @@ def run(a):
     from grayscott_amd.parallel.decomp import init_domain
     from grayscott_amd.utils.config import Settings
 
+    from grayscott_amd.ops import native
+
     torch.cuda.set_device(0)
+    # modelling switches (csrc/include/gs/debug.h; the round-2/3 scripts passed them as
+    # GS_IPC_EMULATE_US / GS_OVERLAP_CHAIN, which the libraries no longer read)
+    emu = a.emulate_us if a.emulate_us is not None else float(os.environ.get("GS_IPC_EMULATE_US", 0))
+    chain = a.chain if a.chain is not None else int(os.environ.get("GS_OVERLAP_CHAIN", 1))
+    native.debug_set("ipc_emulate_us", emu)
+    native.debug_set("overlap_chain", chain)
     L = (a.L, a.L, a.nz)
     s = Settings(L=a.L, precision="Float32", F=0.02, k=0.048, dt=1.0, Du=0.2, Dv=0.1, noise=0.1,
                  backend="AMDGPU", overlap=a.overlap)
@@ -48,7 +56,7 @@ def run(a):
     torch.cuda.synchronize()
     us = (time.perf_counter() - t0) / a.passes * 1e6
     print(f"mode={a.mode} overlap={a.overlap} overlapped={sim.overlapped} "
-          f"transport={sim.transport} chain={os.environ.get('GS_OVERLAP_CHAIN', '1')} "
+          f"transport={sim.transport} chain={chain} emulate_us={emu:g} "
           f"fuse={a.fuse} us_per_pass={us:.1f}", flush=True)
     sim.close()
 
@@ -83,6 +91,9 @@ def main():
     ap.add_argument("--overlap", choices=["on", "off"], default="on")
     ap.add_argument("--summarise", default="")
     ap.add_argument("--transport", choices=["rccl", "ipc"], default="rccl")
+    ap.add_argument("--emulate-us", type=float, default=None,
+                    help="hold every IPC exchange at least this long (debug switch ipc_emulate_us)")
+    ap.add_argument("--chain", type=int, default=None, help="0: overlapped passes one at a time")
     a = ap.parse_args()
     if a.summarise:
         summarise(a.summarise)

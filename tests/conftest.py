@@ -13,6 +13,23 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running CPU test")
 
 
+@pytest.fixture
+def debug_knob():
+    """Set native test switches (csrc/include/gs/debug.h) for one test, restored afterwards:
+    ``debug_knob("overlap_chain", 0)``."""
+    from grayscott_amd.ops import native
+    defaults = {"overlap_chain": 1, "philox_generic": 0, "ipc_emulate_us": 0}
+    touched = []
+
+    def _set(name, value, which="hip"):
+        native.debug_set(name, value, which)
+        touched.append((name, which))
+
+    yield _set
+    for name, which in touched:
+        native.debug_set(name, defaults[name], which)
+
+
 @pytest.fixture(scope="session", autouse=True)
 def _native_built():
     """Build the native libraries once per session if they are missing."""

@@ -15,9 +15,20 @@ def _worker(rank, world, port, out):
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": "0",
                        "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
                        "OMP_NUM_THREADS": "1"})
+    from grayscott_amd.parallel import autotune
     from grayscott_amd.parallel import dist as gdist
     from grayscott_amd.parallel.autotune import candidates, tune_data_path
     from grayscott_amd.utils.config import Settings
+
+    # count the self-checks per transport (fail fast: a failed pinned transport is tried once)
+    calls = []
+    real = autotune.selfcheck
+
+    def counting(ctx, backend, dims, fuse, transport, overlap, **kw):
+        calls.append(transport)
+        return real(ctx, backend, dims, fuse, transport, overlap, **kw)
+
+    autotune.selfcheck = counting
 
     ctx = gdist.init_from_env("cpu")
     s = Settings(L=24, precision="Float32", F=0.02, k=0.048, dt=1.0, Du=0.2, Dv=0.1, noise=0.1,
@@ -26,8 +37,11 @@ def _worker(rank, world, port, out):
     # the third candidate pins the IPC transport, which the CPU backend cannot run: it must be
     # reported as failed without disturbing the others (no fallback chain for pinned transports)
     r = tune_data_path(s, ctx, 24, "cpu", cands=[([1, 1, 2], 1), ([2, 1, 1], 0),
-                                                  ([1, 1, 2], 1, "auto", {}, "ipc")],
+                                                  ([1, 1, 2], 1, "auto", {}, "ipc"),
+                                                  ([2, 1, 1], 0, "auto", {}, "ipc"),
+                                                  ([2, 1, 1], 0, "off", {}, "ipc")],
                        steps=4, warmup=1)
+    r["selfcheck_calls"] = calls
     with open(os.path.join(out, f"r{rank}.json"), "w") as fh:
         json.dump(r, fh)
     ctx.finalize()
@@ -39,10 +53,17 @@ def test_tune_data_path_two_ranks():
                            start_method="spawn")
         r0, r1 = (json.load(open(os.path.join(out, f"r{i}.json"))) for i in range(2))
     assert r0["dims"] == r1["dims"] and r0["dims"] in ([1, 1, 2], [2, 1, 1])
-    assert [row["dims"] for row in r0["table"]] == [[1, 1, 2], [2, 1, 1], [1, 1, 2]]
+    assert [row["dims"] for row in r0["table"]] == [[1, 1, 2], [2, 1, 1], [1, 1, 2], [2, 1, 1],
+                                                   [2, 1, 1]]
     assert all(row["ok"] and row["ms_per_step"] > 0 for row in r0["table"][:2])
     assert r0["table"][2]["transport_req"] == "ipc" and r0["table"][2]["ok"] is False
     assert "ipc" in r0["table"][2]["check_errors"][0]
+    # fail fast: the later IPC rows are skipped with the first failure's reason, and IPC was
+    # self-checked once on each rank
+    for row in r0["table"][3:]:
+        assert row["ok"] is False and row["skipped"].startswith("ipc failed: ")
+        assert "check_errors" not in row
+    assert r0["selfcheck_calls"].count("ipc") == 1 and r1["selfcheck_calls"].count("ipc") == 1
     assert r0["transport"] == "torch" and r0["fuse"] == 1
 
 

@@ -23,6 +23,9 @@ from grayscott_amd.models.grayscott import GrayScott
 from grayscott_amd.parallel.decomp import init_domain
 from grayscott_amd.utils.config import Settings
 L, prec, fuse, steps = int(sys.argv[2]), sys.argv[3], int(sys.argv[4]), int(sys.argv[5])
+if len(sys.argv) > 6 and sys.argv[6] == "philox_generic":
+    from grayscott_amd.ops import native
+    native.debug_set("philox_generic", 1)
 sims = {}
 for backend in ("AMDGPU", "CPU"):
     s = Settings(L=L, precision=prec, F=0.02, k=0.048, dt=1.0, Du=0.2, Dv=0.1, noise=0.1,
@@ -47,10 +50,11 @@ print(err)
 """
 
 
-def _run(L, prec, fuse, steps, env=None, timeout=600):
+def _run(L, prec, fuse, steps, env=None, timeout=600, extra=()):
     e = dict(os.environ)
     e.update(env or {})
-    r = subprocess.run([sys.executable, "-c", _SNIPPET, ROOT, str(L), prec, str(fuse), str(steps)],
+    r = subprocess.run([sys.executable, "-c", _SNIPPET, ROOT, str(L), prec, str(fuse), str(steps),
+                        *extra],
                        env=e, capture_output=True, text=True, timeout=timeout)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = r.stdout.strip().splitlines()
@@ -82,7 +86,7 @@ def test_philox_q32_path_matches_generic():
     """The 32-bit-counter Philox path (rounds 1-3 on the SALU) and the generic 64-bit one give
     bit-identical results: same stream, same kernel otherwise."""
     a, da = _run(96, "Float32", 3, 6)
-    b, db = _run(96, "Float32", 3, 6, env={"GS_PHILOX_GENERIC": "1"})
+    b, db = _run(96, "Float32", 3, 6, extra=("philox_generic",))
     assert a < 2e-5 and b < 2e-5
     digest = lambda info: info.split("digest ")[1].split()[0]  # noqa: E731
     assert digest(da) == digest(db)

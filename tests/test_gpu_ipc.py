@@ -94,10 +94,10 @@ def test_ipc_c_api_rejects_wrong_engine():
 
 
 @pytest.mark.parametrize("chain", ["1", "0"])
-def test_ipc_loopback_zplanes_chained(chain, monkeypatch):
+def test_ipc_loopback_zplanes_chained(chain, debug_knob):
     """z wraps only: whole-plane messages through the landing buffer, overlapped passes chained
     on two streams (or one at a time), with a trailing partial pass."""
-    monkeypatch.setenv("GS_OVERLAP_CHAIN", chain)
+    debug_knob("overlap_chain", int(chain))
     L = 48
     dom = _z_only(init_domain(L, 1, 0, periodic=True))
     s = _settings(L, overlap="on")

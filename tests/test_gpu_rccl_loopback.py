@@ -106,12 +106,13 @@ def test_rccl_loopback_zplanes_not_inplace(monkeypatch):
 
 @pytest.mark.parametrize("mode", ["zplanes", "packed"])
 @pytest.mark.parametrize("chain", ["1", "0"])
-def test_rccl_loopback_chained_long_run(mode, chain, monkeypatch):
+def test_rccl_loopback_chained_long_run(mode, chain, debug_knob):
     """Many chained passes (advance_chained: exchange -> end slabs -> next exchange on the comm
     stream, inner part on the compute stream) stay bit-identical to self copies, also with a
     trailing partial pass that leaves the chain; and the same run one overlapped pass at a time
-    (GS_OVERLAP_CHAIN=0: inner launch ordered after the RCCL launch by an event mark)."""
-    monkeypatch.setenv("GS_OVERLAP_CHAIN", chain)
+    (debug switch overlap_chain = 0: inner launch ordered after the RCCL launch by an event
+    mark)."""
+    debug_knob("overlap_chain", int(chain))
     L = 48
     dom = init_domain(L, 1, 0, periodic=True)
     if mode == "zplanes":
