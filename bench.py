@@ -137,6 +137,12 @@ def golden_check(sim, settings, dom, nsteps: int, init_seed):
                      periodic=False, nbr27=[-1] * 27)
     cs = copy.copy(settings)
     cs.backend, cs.fuse_steps, cs.transport = "CPU", 1, "none"
+    # the node's ranks run their golden models at once: each gets its share of the cores
+    from grayscott_amd.ops import native
+    local = int(os.environ.get("LOCAL_WORLD_SIZE", "0") or 0) or max(1, dom.nprocs)
+    keep = native.cpu_threads()  # OMP_NUM_THREADS, or every core OpenMP sees
+    cores = min(keep, len(os.sched_getaffinity(0)))
+    native.cpu_threads(max(1, cores // local))
     cpu = GrayScott(cs, sub, DistContext())
     try:
         cpu.engine.init_fields()
@@ -146,6 +152,7 @@ def golden_check(sim, settings, dom, nsteps: int, init_seed):
         uc, vc = cpu.get_fields()
     finally:
         cpu.close()
+        native.cpu_threads(keep)
     (ox, oy, oz), (nx, ny, nz) = dom.proc_offsets, dom.proc_sizes
     blk = (slice(oz - lo[2], oz - lo[2] + nz), slice(oy - lo[1], oy - lo[1] + ny),
            slice(ox - lo[0], ox - lo[0] + nx))

@@ -449,7 +449,8 @@ class HipBackend final : public gs::Backend {
       blk_ok = pt.mask == 0 && gsk::block_supported(fa);
       for (int i = 0; i < nt; ++i)
         if ((sizeof(T) == 4 ? tab[i].f32 : tab[i].f64) && i != dflt && !strstr(tab[i].name, "-abl") &&
-            (blk_ok || !gsk::fused_cfg_is_block(i)))
+            (blk_ok || !gsk::fused_cfg_is_block(i)) &&
+            gsk::block_cfg_fits(i, n, (int)sizeof(V2)))
           cfgs.push_back(i);
     }
     const int nsched = pt.zlen1 > 0 ? 1 : 3;  // two z-runs always use schedule 0
@@ -676,15 +677,19 @@ class HipBackend final : public gs::Backend {
     const int64_t slot = (int64_t)(xn_ & 1);
     V2* ptrs[gs::kMaxMsgs];
     bool remote = false;
+    uint32_t sysmask = 0;
     for (int i = 0; i < p.nsend; ++i) {
       const int idx = send_peer_[i];
       ptrs[i] = idx < 0 ? send_ + p.send[i].offset
                         : peers_[idx].landing + slot * peers_[idx].slot_cells + send_off_[i];
       remote = remote || idx >= 0;
+      // a peer on another GPU (or an unidentified one): system-coherent stores over xGMI
+      if (idx >= 0 && (peers_[idx].device != dev_ || gs::debug_knobs().ipc_system_stores))
+        sysmask |= 1u << i;
     }
-    // stores that cross to a peer end with a system-scope release per wave
+    // every wave with stores to a peer waits for them to be acknowledged before it retires
     gsk::launch_pack_ptrs<T, true>(buf_[b], ptrs, g_, p.send, p.nsend, xs_,
-                                   remote && ipc_fence_, nullptr);
+                                   remote && ipc_fence_, nullptr, sysmask);
     HIP_CHECK(hipGetLastError());
   }
 

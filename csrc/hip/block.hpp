@@ -55,7 +55,7 @@ struct BCfg {
   static constexpr int NP = BZ + 2 * TL;
   static constexpr int LDS_BYTES = 2 * NP * NR * 64 * (int)sizeof(V2);
   // whether the two level buffers fit the CU's LDS (run_block falls back to k_fused if not)
-  static constexpr bool FITS = LDS_BYTES <= 160 * 1024;
+  static constexpr bool FITS = LDS_BYTES <= 160 * 1024;  // (= fused.hpp block_cfg_fits)
   static_assert(BY % 4 == 0, "blocks hold whole noise quads");
   // level l+1's work items (noise quad, plane): intermediate levels one quad of halo on each
   // side in y and TL-1-l planes in z; each wave takes items wave, wave + NW, ...

@@ -824,6 +824,24 @@ inline bool fused_cfg_is_block(int i) {
   return i > 0 && i < n && !strncmp(t[i].name, "blk", 3);
 }
 
+// whether block configuration i (table entries 20-26: output blocks of BY rows x BZ planes)
+// holds its two level buffers in the CU's LDS at depth tl -- BCfg::FITS without instantiating
+// it; a configuration that does not fit would run the default k_fused shape under its name
+constexpr int kBlkBY[7] = {8, 4, 8, 4, 8, 8, 4}, kBlkBZ[7] = {2, 4, 2, 4, 4, 2, 4};
+constexpr bool block_k_fits(int k, int tl, int pair_bytes) {
+  return 2 * (kBlkBZ[k] + 2 * tl) * (kBlkBY[k] + 10) * 64 * pair_bytes <= 160 * 1024;
+}
+static_assert(block_k_fits(0, 3, 8) == BCfg<float, 3, 8, 2, 8, true>::FITS &&
+                  block_k_fits(4, 3, 8) == BCfg<float, 3, 8, 4, 16, true>::FITS &&
+                  block_k_fits(4, 2, 8) == BCfg<float, 2, 8, 4, 16, true>::FITS &&
+                  block_k_fits(1, 3, 8) == BCfg<float, 3, 4, 4, 8, true>::FITS &&
+                  !block_k_fits(4, 3, 8) && block_k_fits(4, 2, 8),
+              "block_cfg_fits must match BCfg::FITS");
+inline bool block_cfg_fits(int i, int tl, int pair_bytes) {
+  if (!fused_cfg_is_block(i) || i < 20 || i > 26) return true;
+  return block_k_fits(i - 20, tl, pair_bytes);
+}
+
 inline int& fused_cfg_slot() {
   static int v = -1;
   return v;

@@ -129,6 +129,12 @@ struct PackArgs {
   // the fused kernel's output -- once per wave (+80 us per exchange on the loopback,
   // profiles/r3_ipc_fence.txt)
   int32_t fence;
+  // PACK into peer memory (IPC): bit m set -> message m's stores carry system coherence
+  // (relaxed system-scope atomic stores, global_store ... sc0 sc1: written through to the
+  // memory of the receiving GPU, not held in any cache on the way).  Set for every message to
+  // a peer on another device (or one whose device this process cannot identify); stores to a
+  // landing buffer on this device stay plain (uncached memory, same agent).
+  uint32_t sysmask;
   // unpack from a landing buffer (IPC): a nonzero device word (a timed-out wait) makes the
   // unpack write NaN ghosts instead of the stale landing data
   const int* err;
@@ -142,6 +148,18 @@ constexpr int kPackItems = 4;
 // the total cell count matters: one workgroup row per message at the largest message's size
 // launched ~20k mostly empty workgroups for a 256^3 rank and took ~10 us per pack / unpack.
 // one workgroup's kPackItems x 256 cells: workgroup `blk` of the prefix table
+// a cell stored with system coherence, as 8-byte relaxed system-scope atomic stores (vector
+// stores with the sc0 sc1 bits: no cache on the way holds them)
+template <typename V>
+__device__ __forceinline__ void store_system(V* p, const V& c) {
+  static_assert(sizeof(V) % 8 == 0, "8-byte words");
+  const uint64_t* w = reinterpret_cast<const uint64_t*>(&c);
+  uint64_t* d = reinterpret_cast<uint64_t*>(p);
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(V) / 8); ++i)
+    __hip_atomic_store(d + i, w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 template <typename T, bool PACK, int ITEMS = kPackItems>
 __device__ __forceinline__ void pack_block(typename Vec2<T>::type* __restrict__ f, const Geom& g,
                                            const PackArgs& a, int blk, bool poison) {
@@ -155,6 +173,7 @@ __device__ __forceinline__ void pack_block(typename Vec2<T>::type* __restrict__ 
   const uint32_t bnx = (uint32_t)b.nx, bny = (uint32_t)b.ny;
   const uint32_t base = (uint32_t)(blk - a.b0[m]) * (256u * ITEMS) + threadIdx.x;
   // all loads first (ITEMS in flight per lane), then the stores
+  const bool sys = PACK && ((a.sysmask >> m) & 1u);  // uniform: one message per workgroup
   typename Vec2<T>::type c[ITEMS];
   int64_t jj[ITEMS];
 #pragma unroll
@@ -172,7 +191,8 @@ __device__ __forceinline__ void pack_block(typename Vec2<T>::type* __restrict__ 
   for (int k = 0; k < ITEMS; ++k) {
     const uint32_t i = base + 256u * k;
     if (i < n) {
-      if (PACK) p[i] = c[k];
+      if (PACK && sys) store_system(p + i, c[k]);
+      else if (PACK) p[i] = c[k];
       else f[jj[k]] = c[k];
     }
   }
@@ -192,10 +212,11 @@ __global__ __launch_bounds__(256) void k_pack(typename Vec2<T>::type* __restrict
 template <typename T, bool PACK, int ITEMS = kPackItems>
 void launch_pack_ptrs(typename Vec2<T>::type* f, typename Vec2<T>::type* const* ptrs,
                       const Geom& g, const gs::HaloMsg* msgs, int n, hipStream_t st,
-                      bool fence = false, const int* err = nullptr) {
+                      bool fence = false, const int* err = nullptr, uint32_t sysmask = 0) {
   PackArgs a;
   a.n = n;
   a.fence = fence ? 1 : 0;
+  a.sysmask = sysmask;
   a.err = err;
   int32_t nb = 0;
   for (int i = 0; i < n; ++i) {

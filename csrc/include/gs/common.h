@@ -126,14 +126,21 @@ GS_HD U4 noise_block(int64_t gx, int64_t gy4, int64_t gz, int64_t Lx, int64_t Ly
 // cell id only, so every decomposition starts from the same global state:
 //   (w0, w1) = Philox4x32-10(counter = {q, q >> 32, ~0, ~0}, key = seed),
 //   q = gx + Lx * (gy + Ly * gz);  u = lo + (hi - lo) * (w0 >> 8) 2^-24, v likewise with w1.
-// Step ~0 (2^64 - 1) is never a noise step.  The 24-bit fractions are exact in fp32 and fp64.
+// Step ~0 (2^64 - 1) is never a noise step.  The 24-bit fractions are exact in fp32 and fp64;
+// u = (hi - lo) * frac + lo is evaluated unfused (a rounded product, then a rounded sum) on
+// every backend, exactly as the numpy oracle does (ops/reference.py random_fields), so any
+// [lo, hi) gives the same bits everywhere.
 GS_HD void random_init_cell(int64_t gx, int64_t gy, int64_t gz, int64_t Lx, int64_t Ly,
                             uint64_t seed, double lo, double hi, double* u, double* v) {
+#if defined(__clang__)
+#pragma clang fp contract(off)
+#endif
   const uint64_t q = (uint64_t)gx + (uint64_t)Lx * ((uint64_t)gy + (uint64_t)Ly * (uint64_t)gz);
   const U4 r = philox4x32_10((uint32_t)q, (uint32_t)(q >> 32), 0xFFFFFFFFu, 0xFFFFFFFFu, seed);
   const double s = 5.9604644775390625e-08;  // 2^-24
-  *u = fma(hi - lo, (double)(r.x >> 8) * s, lo);
-  *v = fma(hi - lo, (double)(r.y >> 8) * s, lo);
+  const double w = hi - lo;
+  *u = w * ((double)(r.x >> 8) * s) + lo;
+  *v = w * ((double)(r.y >> 8) * s) + lo;
 }
 
 GS_HD uint32_t u4_get(const U4& r, int i) {

@@ -9,6 +9,9 @@
 //                   path (tests: it equals the 32-bit one bit for bit).
 //   ipc_emulate_us  0 (default); > 0: every IPC exchange lasts at least this long (modelling a
 //                   slower link on one GPU when timing the overlap).  Read by ipc_export.
+//   ipc_system_stores 0 (default); 1: the IPC pack stores every peer-bound message with system
+//                   coherence, as it always does for a peer on another GPU (tests of that path
+//                   on one GPU).
 #pragma once
 
 #include <string.h>
@@ -19,6 +22,7 @@ struct DebugKnobs {
   int overlap_chain = 1;
   int philox_generic = 0;
   double ipc_emulate_us = 0.0;
+  int ipc_system_stores = 0;
 };
 
 inline DebugKnobs& debug_knobs() {
@@ -33,6 +37,7 @@ inline int debug_set(const char* name, double value) {
   if (!strcmp(name, "overlap_chain")) k.overlap_chain = value != 0.0 ? 1 : 0;
   else if (!strcmp(name, "philox_generic")) k.philox_generic = value != 0.0 ? 1 : 0;
   else if (!strcmp(name, "ipc_emulate_us")) k.ipc_emulate_us = value > 0.0 ? value : 0.0;
+  else if (!strcmp(name, "ipc_system_stores")) k.ipc_system_stores = value != 0.0 ? 1 : 0;
   else return -1;
   return 0;
 }

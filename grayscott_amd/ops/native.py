@@ -451,6 +451,15 @@ def peer_access_matrix():
     return [[int(buf[i * n + j]) for j in range(n)] for i in range(n)]
 
 
+def cpu_threads(n: int = 0) -> int:
+    """OpenMP threads of the CPU backend in this process: ``n > 0`` sets them; returns the
+    current maximum."""
+    lib = load("core")
+    lib.gs_cpu_threads.argtypes = [c_int32]
+    lib.gs_cpu_threads.restype = c_int
+    return int(lib.gs_cpu_threads(int(n)))
+
+
 def debug_set(name: str, value: float, which: str = "hip") -> None:
     """Set a test / modelling switch of a native library (csrc/include/gs/debug.h):
     ``overlap_chain`` (0: overlapped passes one at a time; read at engine creation),

@@ -18,7 +18,8 @@ def debug_knob():
     """Set native test switches (csrc/include/gs/debug.h) for one test, restored afterwards:
     ``debug_knob("overlap_chain", 0)``."""
     from grayscott_amd.ops import native
-    defaults = {"overlap_chain": 1, "philox_generic": 0, "ipc_emulate_us": 0}
+    defaults = {"overlap_chain": 1, "philox_generic": 0, "ipc_emulate_us": 0,
+                "ipc_system_stores": 0}
     touched = []
 
     def _set(name, value, which="hip"):

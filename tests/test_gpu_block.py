@@ -124,6 +124,24 @@ def test_auto_depth_is_measured_single_rank():
     assert np.abs(g[1] - c[1]).max() < 2e-5
 
 
+@pytest.mark.parametrize("L,depth", [((64, 64, 32), 2), ((192, 160, 12), 3)])
+def test_auto_depth_without_tuning_uses_plane_rule(L, depth, monkeypatch):
+    """GS_AUTOTUNE=0: nothing is timed, so the engine falls back to the plane-size rule (T=2
+    below 160^2 x-y planes, else the full depth) instead of always running T=3."""
+    from grayscott_amd.ops import native
+    native.fused_unpin()
+    monkeypatch.setenv("GS_AUTOTUNE", "0")
+    s = Settings(L=L[0], precision="Float32", F=0.02, k=0.048, dt=1.0, Du=0.2, Dv=0.1,
+                 noise=0.1, backend="AMDGPU", seed=19)
+    sim = GrayScott(s, init_domain(L, 1, 0))
+    try:
+        sim.init_fields()
+        assert sim.fuse == 3 and sim.depth == depth
+        assert all(c[2] == 0.0 for c in sim.fused_choice().values())
+    finally:
+        sim.close()
+
+
 @pytest.mark.parametrize("L,k,step", [((48, 40, 36), 2, 7), ((64, 40, 36), 3, 5), ((36, 36, 36), 2, 0)])
 def test_block_kernel_raw_pass_reads_stored_ghosts(L, k, step):
     """A raw fused pass (the timing / overlap-test primitive gs_fused_runs_raw) runs without the

@@ -75,6 +75,22 @@ def test_ipc_loopback_periodic_packed(L, fuse, prec, overlap):
     np.testing.assert_array_equal(v1, v0)
 
 
+@pytest.mark.parametrize("prec", ["Float32", "Float64"])
+def test_ipc_system_coherent_stores(prec, debug_knob):
+    """The pack's store path for peers on another GPU (relaxed system-scope stores, sc0 sc1;
+    kernels.hpp store_system), forced for the loopback peer on this GPU: bit-identical to self
+    copies, fp32 (one 8-byte word per cell) and fp64 (two)."""
+    debug_knob("ipc_system_stores", 1)
+    L = 32
+    dom = init_domain(L, 1, 0, periodic=True)
+    s = _settings(L, prec, "auto")
+    u0, v0, _ = _run(dom, s, 2, 13, loopback=False)
+    u1, v1, i1 = _run(dom, s, 2, 13, transport="ipc", loopback=True)
+    assert i1["transport"] == "ipc"
+    np.testing.assert_array_equal(u1, u0)
+    np.testing.assert_array_equal(v1, v0)
+
+
 def test_ipc_c_api_rejects_wrong_engine():
     """The IPC / RCCL entry points check the engine's backend type: a dtype that does not match
     the engine is an error, not an unchecked cast (VERDICT r2 weak #8)."""

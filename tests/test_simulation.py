@@ -114,3 +114,18 @@ def test_hip_backend_fails_loudly_without_gpu():
         pytest.skip("GPU present")
     with pytest.raises(RuntimeError, match="no GPU"):
         _sim(L=8, backend="AMDGPU")
+
+
+@pytest.mark.parametrize("lo,hi,prec", [(-0.3, 0.7, "Float64"), (0.1, 0.35, "Float64"),
+                                        (-1.0, 2.5, "Float32")])
+def test_random_init_any_range_matches_numpy_oracle(lo, hi, prec):
+    """gs::random_init_cell evaluates (hi - lo) * frac + lo unfused, like the numpy oracle
+    (ops/reference.py random_fields), so any range gives the same bits (not just [0, 1))."""
+    L = 14
+    sim = _sim(L=L, prec=prec)
+    sim.randomize_fields(seed=11, lo=lo, hi=hi)
+    u, v = sim.get_fields()
+    dt = np.float64 if prec == "Float64" else np.float32
+    ru, rv = ref.random_fields((L, L, L), seed=11, lo=lo, hi=hi, dtype=dt)
+    assert np.array_equal(u, ru) and np.array_equal(v, rv)
+    assert u.min() >= lo and u.max() < hi
