@@ -170,3 +170,111 @@ def run(L, nsteps: int, F=0.02, k=0.048, dt=1.0, Du=0.2, Dv=0.1, noise_amp=0.0, 
     for t in range(nsteps):
         u, v = step(u, v, t, F, k, dt, Du, Dv, noise_amp, seed, periodic, backend)
     return u, v
+
+
+# ------------------------------------------------------------------------------------------
+# The same oracle as whole-tensor PyTorch code that runs on any device (the GPU tests run it on
+# the MI355X itself, so the production kernels can be checked at L = 256 / 512 in seconds).
+# Philox is re-derived once more for int64 tensors -- torch has no unsigned 64-bit multiply, so
+# each 32 x 32-bit product is split at 16 bits -- and shares no code with csrc/ or the numpy
+# version above (a CPU test checks the two streams agree bit for bit).
+# ------------------------------------------------------------------------------------------
+_M32 = 0xFFFFFFFF
+
+
+def _mulhilo32_t(a, m: int):
+    """(hi, lo) 32-bit halves of a * m for int64 tensors a in [0, 2^32), m < 2^32."""
+    a_hi, a_lo = a >> 16, a & 0xFFFF
+    x = a_lo * m                     # < 2^48
+    y = a_hi * m                     # < 2^48
+    hi = (y + (x >> 16)) >> 16       # floor(a m / 2^32)
+    lo = (((y & 0xFFFF) << 16) + x) & _M32
+    return hi, lo
+
+
+def philox4x32_10_torch(c0, c1, c2, c3, seed: int):
+    """Philox4x32-10 on int64 tensors holding uint32 values; returns 4 such tensors."""
+    k0, k1 = seed & _M32, (seed >> 32) & _M32
+    for _ in range(10):
+        hi0, lo0 = _mulhilo32_t(c0, 0xD2511F53)
+        hi1, lo1 = _mulhilo32_t(c2, 0xCD9E8D57)
+        c0, c1, c2, c3 = hi1 ^ c1 ^ k0, lo1, hi0 ^ c3 ^ k1, lo0
+        k0 = (k0 + W0) & _M32
+        k1 = (k1 + W1) & _M32
+    return c0, c1, c2, c3
+
+
+def _global_index(L, device, torch):
+    Lx, Ly, Lz = (int(v) for v in L)
+    gz = torch.arange(Lz, dtype=torch.int64, device=device)[:, None, None]
+    gy = torch.arange(Ly, dtype=torch.int64, device=device)[None, :, None]
+    gx = torch.arange(Lx, dtype=torch.int64, device=device)[None, None, :]
+    return gx, gy, gz
+
+
+def random_fields_torch(L, seed: int, lo: float = 0.0, hi: float = 1.0, dtype=None, device="cpu"):
+    """random_fields on a torch device: (u, v) as (Lz, Ly, Lx) tensors."""
+    import torch
+    dtype = dtype or torch.float32
+    Lx, Ly, _ = (int(v) for v in L)
+    gx, gy, gz = _global_index(L, device, torch)
+    q = gx + Lx * (gy + Ly * gz)
+    full = torch.full_like(q, _M32)
+    w0, w1, _, _ = philox4x32_10_torch(q & _M32, q >> 32, full, full, seed)
+    s = 2.0 ** -24
+    u = (hi - lo) * ((w0 >> 8).to(torch.float64) * s) + lo
+    v = (hi - lo) * ((w1 >> 8).to(torch.float64) * s) + lo
+    return u.to(dtype), v.to(dtype)
+
+
+def noise_torch(L, step: int, seed: int, dtype=None, device="cpu"):
+    """noise() for the whole domain on a torch device: Uniform[-1, 1) draws, (Lz, Ly, Lx)."""
+    import torch
+    dtype = dtype or torch.float32
+    Lx, Ly, Lz = (int(v) for v in L)
+    Ly4 = (Ly + 3) // 4
+    gz = torch.arange(Lz, dtype=torch.int64, device=device)[:, None, None]
+    g4 = torch.arange(Ly4, dtype=torch.int64, device=device)[None, :, None]
+    gx = torch.arange(Lx, dtype=torch.int64, device=device)[None, None, :]
+    q = gx + Lx * (g4 + Ly4 * gz)                                      # one block per y-quad
+    w = philox4x32_10_torch(q & _M32, q >> 32, torch.full_like(q, step & _M32),
+                            torch.full_like(q, (step >> 32) & _M32), seed)
+    words = torch.stack(w, dim=2).reshape(Lz, Ly4 * 4, Lx)[:, :Ly]  # row gy: word gy & 3
+    signed = torch.where(words >= 2 ** 31, words - 2 ** 32, words)
+    return signed.to(dtype) * (2.0 ** -31)
+
+
+def run_torch(L, nsteps: int, F=0.02, k=0.048, dt=1.0, Du=0.2, Dv=0.1, noise_amp=0.0, seed=0,
+              dtype=None, device="cpu", init_seed=None, init_lo=0.0, init_hi=1.0, u0=None,
+              v0=None):
+    """``run`` as device-resident PyTorch (non-periodic reference boundary): from
+    the reference init, the benchmarks' random init (``init_seed``) or given (u0, v0); every
+    operation in ``dtype`` (default float32).  Returns (u, v) tensors on ``device``."""
+    import torch
+    import torch.nn.functional as Fn
+    dtype = dtype or torch.float32
+    if isinstance(L, int):
+        L = (L, L, L)
+    if u0 is not None:
+        u, v = u0.to(device=device, dtype=dtype), v0.to(device=device, dtype=dtype)
+    elif init_seed is not None:
+        u, v = random_fields_torch(L, init_seed, init_lo, init_hi, dtype, device)
+    else:
+        a, b = init_fields(L, dtype=np.float64)
+        u = torch.as_tensor(a).to(device=device, dtype=dtype)
+        v = torch.as_tensor(b).to(device=device, dtype=dtype)
+
+    def nsum(p):
+        return ((p[1:-1, 1:-1, :-2] + p[1:-1, 1:-1, 2:]) + (p[1:-1, :-2, 1:-1] + p[1:-1, 2:, 1:-1])
+                + (p[:-2, 1:-1, 1:-1] + p[2:, 1:-1, 1:-1]))
+
+    for t in range(nsteps):
+        su = nsum(Fn.pad(u, (1, 1, 1, 1, 1, 1), mode="constant", value=bc_u(t)))
+        sv = nsum(Fn.pad(v, (1, 1, 1, 1, 1, 1), mode="constant", value=0.0))
+        uvv = u * v * v
+        du = (Du / 6.0) * su - Du * u - uvv + F * (1.0 - u)
+        if noise_amp != 0:
+            du = du + noise_amp * noise_torch(L, t, seed, dtype, device)
+        dv = (Dv / 6.0) * sv - Dv * v + uvv - (F + k) * v
+        u, v = u + du * dt, v + dv * dt
+    return u, v

@@ -1,0 +1,106 @@
+"""The production kernels against the independent PyTorch fp32 oracle (ops/reference.py
+run_torch), on the MI355X.
+
+The other GPU tests compare the kernels with the native OpenMP golden model, which shares
+gs/common.h (Philox, boundary handling) with them; a bug in shared code would pass both.  The
+oracle here shares nothing with csrc/: its own Philox (int64 torch tensors), its own random
+init, plain tensor arithmetic.  It runs on the GPU too, so the headline configurations are
+checked directly: the autotuned T=3 k_fused at L=256, a pinned production tile at L=512
+(BASELINE.json's size), and the small-grid k_block at the reference example's L=64
+(examples/settings-files.toml).  The pattern is the reference's backend-parity test
+(test/unit/simulation/unit-Simulation_CUDA.jl:10-32).
+"""
+import numpy as np
+import pytest
+import torch
+
+from grayscott_amd.models.grayscott import GrayScott
+from grayscott_amd.ops import reference as ref
+from grayscott_amd.parallel.decomp import init_domain
+from grayscott_amd.utils.config import Settings
+
+pytestmark = pytest.mark.gpu
+
+PHYS = dict(F=0.02, k=0.048, dt=1.0, Du=0.2, Dv=0.1)
+TOL = 2e-5
+
+
+@pytest.fixture(autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from grayscott_amd.ops import native
+    native.load("hip")
+    native.fused_unpin()
+    yield
+    native.fused_unpin()
+
+
+def _kernel_run(L, fuse, steps, cfg=None, sched=None, seed=2024, init_seed=7):
+    from grayscott_amd.ops import native
+    if cfg is not None:
+        native.fused_select(cfg)
+    if sched is not None:
+        native.fused_sched(sched)
+    s = Settings(L=L, precision="Float32", noise=0.1, backend="AMDGPU", seed=seed, **PHYS)
+    sim = GrayScott(s, init_domain(L, 1, 0), fuse=fuse)
+    try:
+        sim.init_fields()
+        sim.randomize_fields(seed=init_seed)
+        sim.iterate(steps)
+        u, v = sim.get_fields_device()
+        torch.cuda.synchronize()
+        return u, v, sim.fused_choice(), sim.depth
+    finally:
+        sim.close()
+
+
+def _oracle(L, steps, seed=2024, init_seed=7):
+    return ref.run_torch(L, steps, noise_amp=0.1, seed=seed, dtype=torch.float32,
+                         device="cuda", init_seed=init_seed, **PHYS)
+
+
+def _err(a, b):
+    return max(float((a[0] - b[0]).abs().max()), float((a[1] - b[1]).abs().max()))
+
+
+def test_autotuned_t3_fused_l256_vs_torch_oracle():
+    u, v, choice, depth = _kernel_run(256, 3, 9)
+    assert depth == 3
+    err = _err((u, v), _oracle(256, 9))
+    print("L=256 T=3 autotuned", choice, "max|d|", err)
+    assert err < TOL, (err, choice)
+
+
+def test_pinned_tile_l512_vs_torch_oracle():
+    """One pinned production tile / schedule at the headline size (6 steps = 2 T=3 passes)."""
+    u, v, choice, _ = _kernel_run(512, 3, 6, cfg="4x12:1s", sched=1)
+    err = _err((u, v), _oracle(512, 6))
+    print("L=512 4x12:1s sched 1", "max|d|", err)
+    assert err < TOL, err
+
+
+@pytest.mark.parametrize("cfg,fuse", [("blk8x2w16l", 3), ("blk4x4w8", 2), (None, 3)])
+def test_block_kernel_l64_vs_torch_oracle(cfg, fuse):
+    """k_block at the reference example's size (None: the autotuner's pick among all shapes)."""
+    u, v, choice, _ = _kernel_run(64, fuse, 30, cfg=cfg)
+    err = _err((u, v), _oracle(64, 30))
+    print("L=64", cfg, fuse, choice, "max|d|", err)
+    assert err < TOL, (err, choice)
+
+
+@pytest.mark.parametrize("prec", ["Float32", "Float64"])
+def test_gpu_random_init_any_range_bitwise(prec):
+    """k_randomize with a range other than [0, 1): the same bits as the numpy oracle."""
+    L = 40
+    s = Settings(L=L, precision=prec, noise=0.1, backend="AMDGPU", **PHYS)
+    sim = GrayScott(s, init_domain(L, 1, 0))
+    try:
+        sim.init_fields()
+        sim.randomize_fields(seed=13, lo=-0.4, hi=0.85)
+        u, v = sim.get_fields()
+    finally:
+        sim.close()
+    dt = np.float32 if prec == "Float32" else np.float64
+    ru, rv = ref.random_fields((L, L, L), seed=13, lo=-0.4, hi=0.85, dtype=dt)
+    assert np.array_equal(u, ru) and np.array_equal(v, rv)

@@ -1,0 +1,81 @@
+"""Device per-phase timing on the MI355X (csrc/include/gs/phase.h): hipEvents
+recorded in stream order around pack / transport / unpack / inner / shell / fused / bc.  The
+parts must account for the measured pass (within 15 %), single rank and for the driver's
+multi-rank bench command run on one GPU (two ranks, IPC transport), whose JSON carries the
+per-phase record the first 8-GPU scaling run will report."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from grayscott_amd.models.grayscott import GrayScott
+from grayscott_amd.parallel.decomp import init_domain
+from grayscott_amd.utils.config import Settings
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def test_single_rank_phases_account_for_the_pass():
+    s = Settings(L=256, precision="Float32", F=0.02, k=0.048, dt=1.0, Du=0.2, Dv=0.1,
+                 noise=0.1, backend="AMDGPU")
+    sim = GrayScott(s, init_domain(256, 1, 0), fuse=3)
+    try:
+        sim.init_fields()
+        sim.randomize_fields(seed=1)
+        sim.iterate(6)
+        r = sim.phase_profile(30)
+    finally:
+        sim.close()
+    print(json.dumps(r))
+    assert r["passes"] == 10 and r["steps"] == 30 and not r["truncated"]
+    assert r["per_pass"]["fused"] == 1.0 and r["phase_us"]["fused"] > 0
+    assert 0.85 <= r["accounted"] <= 1.15, r
+
+
+def test_periodic_loopback_phases():
+    """One rank with periodic wraps through the RCCL loopback: pack, transport, unpack all
+    appear (the packed 26-message plan)."""
+    s = Settings(L=64, precision="Float32", F=0.02, k=0.048, dt=1.0, Du=0.2, Dv=0.1,
+                 noise=0.1, backend="AMDGPU", overlap="off")
+    sim = GrayScott(s, init_domain(64, 1, 0, periodic=True), fuse=2, loopback=True)
+    try:
+        sim.init_fields()
+        r = sim.phase_profile(20)
+    finally:
+        sim.close()
+    print(json.dumps(r))
+    assert {"pack", "transport", "unpack", "fused"} <= set(r["phase_us"])
+    assert r["exchange_us"] >= r["phase_us"]["transport"]
+    assert 0.85 <= r["accounted"] <= 1.15, r
+
+
+def test_bench_two_ranks_reports_phases():
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "12", "--warmup",
+                        "3", "--timeout", "240"], cwd=ROOT, capture_output=True, text=True,
+                       timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    ph = d["phases"]
+    summ = ph["chosen"]["summary"]
+    print(json.dumps(summ))
+    assert len(ph["chosen"]["per_rank"]) == 2
+    assert {"pack", "transport", "unpack"} <= set(summ["phase_us"])
+    assert summ["bytes_per_neighbour_max"] > 0 and summ["link_GBps_min"] > 0
+    assert 0.85 <= summ["accounted"] <= 1.15, summ
+    assert len(ph["peer_access"]) >= 1 and all(len(row) == len(ph["peer_access"])
+                                               for row in ph["peer_access"])
+    if d["config"]["dims"] != [2, 1, 1]:
+        assert ph["reference_grid"]["summary"]["dims"] == [2, 1, 1]
