@@ -365,7 +365,10 @@ __device__ __forceinline__ void slab_unit(const typename C::V2* __restrict__ s,
   }
 }
 
-template <typename T, int TL, bool PER, bool NOISE, bool Q32>
+// OM: the face orientations compiled in (bit o: orientation o).  A unit's registers are those of
+// the heaviest orientation in the kernel, so a launch without z faces (the x / y slabs next to
+// z slabs computed by k_fused, backend shell variant 1) uses the x / y-only instantiation.
+template <typename T, int TL, bool PER, bool NOISE, bool Q32, int OM = 7>
 __global__ __launch_bounds__(256) void k_slab(const typename PairT<T>::type* __restrict__ s,
                                               typename PairT<T>::type* __restrict__ d,
                                               SlabArgs a, FoldCoef<T> f, uint64_t seed) {
@@ -376,11 +379,12 @@ __global__ __launch_bounds__(256) void k_slab(const typename PairT<T>::type* __r
   while (fi + 1 < a.nface && unit >= a.f[fi + 1].u0) ++fi;
   const SlabFace& F = a.f[fi];
   const T ar31 = f.ar * (T)4.656612873077392578125e-10;  // exact: power-of-two scaling
-  switch (F.orient) {
-    case 0: slab_unit<SCfg<T, TL, PER, NOISE, Q32, 0>, T>(s, d, a, F, unit - F.u0, f, ar31, seed); break;
-    case 1: slab_unit<SCfg<T, TL, PER, NOISE, Q32, 1>, T>(s, d, a, F, unit - F.u0, f, ar31, seed); break;
-    default: slab_unit<SCfg<T, TL, PER, NOISE, Q32, 2>, T>(s, d, a, F, unit - F.u0, f, ar31, seed); break;
-  }
+  if constexpr ((OM & 1) != 0)
+    if (F.orient == 0) slab_unit<SCfg<T, TL, PER, NOISE, Q32, 0>, T>(s, d, a, F, unit - F.u0, f, ar31, seed);
+  if constexpr ((OM & 2) != 0)
+    if (F.orient == 1) slab_unit<SCfg<T, TL, PER, NOISE, Q32, 1>, T>(s, d, a, F, unit - F.u0, f, ar31, seed);
+  if constexpr ((OM & 4) != 0)
+    if (F.orient == 2) slab_unit<SCfg<T, TL, PER, NOISE, Q32, 2>, T>(s, d, a, F, unit - F.u0, f, ar31, seed);
 }
 
 // Host side: the face slabs of one overlapped pass.  faces[i] = {orient, side (-1 / +1)};
@@ -389,22 +393,22 @@ struct SlabSpec {
   int orient, n0, a0, a1, m0, m1;
 };
 
-template <typename T, int TL, bool PER, bool NZ, bool Q32>
+template <typename T, int TL, bool PER, bool NZ, bool Q32, int OM = 7>
 void launch_slab_kernel(const void* s, void* d, const SlabArgs& a, const gs::Params& p,
                         hipStream_t st) {
   using V2 = typename PairT<T>::type;
-  k_slab<T, TL, PER, NZ, Q32><<<(unsigned)((a.nunits + 3) / 4), 256, 0, st>>>(
+  k_slab<T, TL, PER, NZ, Q32, OM><<<(unsigned)((a.nunits + 3) / 4), 256, 0, st>>>(
       (const V2*)s, (V2*)d, a, make_fold<T>(p), p.seed);
 }
 
 // resident 4-wave workgroups per CU of one k_slab instantiation (its register footprint:
 // fp32 T=3 ~210 VGPRs, two waves per SIMD; fp64 T=3 one)
-template <typename T, int TL, bool PER, bool NZ, bool Q32>
+template <typename T, int TL, bool PER, bool NZ, bool Q32, int OM = 7>
 int slab_occupancy() {
   static int occ = -1;
   if (occ < 0) {
     int o = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k_slab<T, TL, PER, NZ, Q32>, 256, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k_slab<T, TL, PER, NZ, Q32, OM>, 256, 0) !=
             hipSuccess || o < 1)
       o = 1;
     occ = o;
@@ -419,7 +423,12 @@ void launch_slabs_tl(const void* s, void* d, const Geom& g, const gs::Params& p,
   a.g = g;
   a.t = t;
   const bool per = g.periodic != 0, nz = p.noise != 0.0, q32 = philox_q32(g);
-  const int occ = !nz ? (per ? slab_occupancy<T, TL, true, false, true>()
+  // the production combination without z faces: the x / y-only kernel (fewer registers)
+  bool zf = false;
+  for (int i = 0; i < nspec; ++i) zf = zf || spec[i].orient == 2;
+  const bool xy = !per && nz && q32 && !zf;
+  const int occ = xy ? slab_occupancy<T, TL, false, true, true, 3>()
+                : !nz ? (per ? slab_occupancy<T, TL, true, false, true>()
                              : slab_occupancy<T, TL, false, false, true>())
                 : q32 ? (per ? slab_occupancy<T, TL, true, true, true>()
                              : slab_occupancy<T, TL, false, true, true>())
@@ -473,7 +482,9 @@ void launch_slabs_tl(const void* s, void* d, const Geom& g, const gs::Params& p,
   }
   a.nunits = u0;
   if (u0 == 0) return;
-  if (!nz) {
+  if (xy) {
+    launch_slab_kernel<T, TL, false, true, true, 3>(s, d, a, p, st);
+  } else if (!nz) {
     if (per) launch_slab_kernel<T, TL, true, false, true>(s, d, a, p, st);
     else launch_slab_kernel<T, TL, false, false, true>(s, d, a, p, st);
   } else if (q32) {
