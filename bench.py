@@ -304,8 +304,12 @@ def run(args) -> int:
                 phases["reference_grid"] = None
                 if rows:
                     r = min(rows, key=lambda r: r["ms_per_step"])
-                    phases["reference_grid"] = profile_reference_grid(
-                        settings, ctx, args, bal, r, args.profile_passes)
+                    try:
+                        # the same construction the tuning timed for this row
+                        phases["reference_grid"] = profile_reference_grid(
+                            settings, ctx, args, bal, r, args.profile_passes)
+                    except Exception as ex:  # recorded; the headline is already measured
+                        phases["reference_grid"] = {"error": str(ex)[:200]}
             from grayscott_amd.ops import native
             phases["peer_access"] = native.peer_access_matrix() if ctx.rank == 0 else None
         phases["profile_s"] = round(time.perf_counter() - t_prof, 2)

@@ -96,6 +96,10 @@ def main():
                 if bits:
                     for v in ((0, 1) if name == "z" else (0,)):
                         faces[f"{name}_v{v}_us"] = round(timed(("faces", bits, v)), 1)
+            # the whole shell through each variant (2: z slabs on a side stream, concurrently)
+            if (sides & 48) and (sides & 15):
+                for v in (0, 1, 2):
+                    faces[f"all_v{v}_us"] = round(timed(("faces", sides, v)), 1)
             row = {"local": [a.L, a.L, nz], "k": k, "packed": a.packed, "faces": faces,
                    "one_sided": a.one_sided, "full_us": round(full, 1),
                    "inner_us": round(inner, 1), "shell_us": round(shell, 1),
