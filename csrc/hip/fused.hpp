@@ -801,17 +801,22 @@ inline const FusedCfgEntry* fused_cfg_table(int* n) {
       {"blk8x4w16", true, false},  // 24  (T=2 only: T=3 levels do not fit the LDS)
       {"blk8x2w16l", true, false}, // 25  last level in half-quad items
       {"blk4x4w16l", true, false}, // 26  last level in half-quad items
+      // the same shapes through the SALU-lean block kernel (block.hpp SL: one buffer descriptor,
+      // per-wave load indexing, step-uniform Philox parts hoisted, branch-free boundary resets)
+      {"blk8x2w16s", true, false}, // 27
+      {"blk4x4w16s", true, false}, // 28
+      {"blk8x2w8s", true, false},  // 29
 #ifdef GS_ABLATION
-      {"4x12:2s-abl1", true, false},  // 27  no barriers
-      {"4x12:2s-abl2", true, false},  // 28  L2-resident loads
-      {"4x12:1s-abl4", true, false},  // 29  Philox keys in VGPRs (exact)
-      {"4x12:2s-abl4", true, false},  // 30  Philox keys in VGPRs (exact)
-      {"4x12:1s-abl8", true, false},  // 31  DPP sums with the s_nop (exact)
-      {"4x12:1s-abl12", true, false}, // 32  abl4 + abl8 (exact)
-      {"4x12:1s-abl16", true, false}, // 33  pipeline fill computes every level (exact)
-      {"4x8:1s-abl16", true, true},   // 34  pipeline fill computes every level (exact)
-      {"4x6:2s-abl16", true, true},   // 35  pipeline fill computes every level (exact)
-      {"4x12:1s-abl32", true, false}, // 36  Philox only on lanes in the x cone (exact)
+      {"4x12:2s-abl1", true, false},  // 30  no barriers
+      {"4x12:2s-abl2", true, false},  // 31  L2-resident loads
+      {"4x12:1s-abl4", true, false},  // 32  Philox keys in VGPRs (exact)
+      {"4x12:2s-abl4", true, false},  // 33  Philox keys in VGPRs (exact)
+      {"4x12:1s-abl8", true, false},  // 34  DPP sums with the s_nop (exact)
+      {"4x12:1s-abl12", true, false}, // 35  abl4 + abl8 (exact)
+      {"4x12:1s-abl16", true, false}, // 36  pipeline fill computes every level (exact)
+      {"4x8:1s-abl16", true, true},   // 37  pipeline fill computes every level (exact)
+      {"4x6:2s-abl16", true, true},   // 38  pipeline fill computes every level (exact)
+      {"4x12:1s-abl32", true, false}, // 39  Philox only on lanes in the x cone (exact)
 #endif
   };
   *n = (int)(sizeof(t) / sizeof(t[0]));
@@ -824,10 +829,10 @@ inline bool fused_cfg_is_block(int i) {
   return i > 0 && i < n && !strncmp(t[i].name, "blk", 3);
 }
 
-// whether block configuration i (table entries 20-26: output blocks of BY rows x BZ planes)
+// whether block configuration i (table entries 20-29: output blocks of BY rows x BZ planes)
 // holds its two level buffers in the CU's LDS at depth tl -- BCfg::FITS without instantiating
 // it; a configuration that does not fit would run the default k_fused shape under its name
-constexpr int kBlkBY[7] = {8, 4, 8, 4, 8, 8, 4}, kBlkBZ[7] = {2, 4, 2, 4, 4, 2, 4};
+constexpr int kBlkBY[10] = {8, 4, 8, 4, 8, 8, 4, 8, 4, 8}, kBlkBZ[10] = {2, 4, 2, 4, 4, 2, 4, 2, 4, 2};
 constexpr bool block_k_fits(int k, int tl, int pair_bytes) {
   return 2 * (kBlkBZ[k] + 2 * tl) * (kBlkBY[k] + 10) * 64 * pair_bytes <= 160 * 1024;
 }
@@ -838,7 +843,7 @@ static_assert(block_k_fits(0, 3, 8) == BCfg<float, 3, 8, 2, 8, true>::FITS &&
                   !block_k_fits(4, 3, 8) && block_k_fits(4, 2, 8),
               "block_cfg_fits must match BCfg::FITS");
 inline bool block_cfg_fits(int i, int tl, int pair_bytes) {
-  if (!fused_cfg_is_block(i) || i < 20 || i > 26) return true;
+  if (!fused_cfg_is_block(i) || i < 20 || i > 29) return true;
   return block_k_fits(i - 20, tl, pair_bytes);
 }
 
@@ -879,8 +884,8 @@ void run_fused_cfg(const void* s, void* d, const FusedArgs& a, const gs::Params&
       case 16: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
       case 17: FusedLaunch<FCfg<T, TL, 4, 4, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
 #ifdef GS_ABLATION
-      case 34: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
-      case 35: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 37: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 38: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
 #endif
       default: break;
     }
@@ -910,17 +915,20 @@ void run_fused_cfg(const void* s, void* d, const FusedArgs& a, const gs::Params&
       case 24: if (block_supported(a) && run_block<BCfg<T, TL, 8, 4, 16, NZ>>(s, d, a, p, st)) return; break;
       case 25: if (block_supported(a) && run_block<BCfg<T, TL, 8, 2, 16, NZ, true, true>>(s, d, a, p, st)) return; break;
       case 26: if (block_supported(a) && run_block<BCfg<T, TL, 4, 4, 16, NZ, true, true>>(s, d, a, p, st)) return; break;
+      case 27: if (block_supported(a) && run_block<BCfg<T, TL, 8, 2, 16, NZ, true, false, true>>(s, d, a, p, st)) return; break;
+      case 28: if (block_supported(a) && run_block<BCfg<T, TL, 4, 4, 16, NZ, true, false, true>>(s, d, a, p, st)) return; break;
+      case 29: if (block_supported(a) && run_block<BCfg<T, TL, 8, 2, 8, NZ, true, false, true>>(s, d, a, p, st)) return; break;
 #ifdef GS_ABLATION
-      case 27: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 1>, T>::run(s, d, a, p, st); return;
-      case 28: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 2>, T>::run(s, d, a, p, st); return;
-      case 29: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;
-      case 30: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;
-      case 31: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 8>, T>::run(s, d, a, p, st); return;
-      case 32: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 12>, T>::run(s, d, a, p, st); return;
-      case 33: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
-      case 34: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
-      case 35: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
-      case 36: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 32>, T>::run(s, d, a, p, st); return;
+      case 30: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 1>, T>::run(s, d, a, p, st); return;
+      case 31: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 2>, T>::run(s, d, a, p, st); return;
+      case 32: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;
+      case 33: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;
+      case 34: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 8>, T>::run(s, d, a, p, st); return;
+      case 35: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 12>, T>::run(s, d, a, p, st); return;
+      case 36: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 37: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 38: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 39: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 32>, T>::run(s, d, a, p, st); return;
 #endif
       default: break;  // 0 and 14: the default shape below
     }

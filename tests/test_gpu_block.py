@@ -17,7 +17,8 @@ from grayscott_amd.utils.config import Settings
 
 pytestmark = pytest.mark.gpu
 
-BLOCKS = ["blk8x2w8", "blk4x4w8", "blk8x2w16", "blk4x4w16", "blk8x4w16", "blk8x2w16l", "blk4x4w16l"]
+BLOCKS = ["blk8x2w8", "blk4x4w8", "blk8x2w16", "blk4x4w16", "blk8x4w16", "blk8x2w16l", "blk4x4w16l",
+          "blk8x2w16s", "blk4x4w16s", "blk8x2w8s"]
 
 
 @pytest.fixture(scope="module", autouse=True)
