@@ -378,6 +378,10 @@ __global__ __launch_bounds__(64 * C::NW, 1) void k_block_sl(const typename C::V2
   // byte offset of cone row 0 of cone plane 0 (may be negative: rows above the storage)
   const int base = ((z0 - TL + g.H) * g.py + (y0 - TL + g.H)) * pitchb;
   gs::U4 W[TL][C::JMAX];  // noise words per (level, item of this wave)
+  // LDS target of a load past the cone (never read): the writes stay unconditional, so the
+  // compiler keeps every load ahead of the noise draws instead of sinking each one into its own
+  // branch with a full wait (seven memory latencies in a row)
+  __shared__ V2 sink[64];
   {
     V2 lv[JL];
     int lds[JL];
@@ -388,10 +392,15 @@ __global__ __launch_bounds__(64 * C::NW, 1) void k_block_sl(const typename C::V2
         r -= NL;
         ++pz;
       }
-      lds[j] = pz < NP ? pz * NR + (C::R0 - TL) + r : -1;
-      const int roff = pz < NP ? base + pz * pzb + r * pitchb : 0x40000000;
+      // (a load past the cone -- the last j of some waves -- re-reads the cone's last plane and
+      // is not written to LDS: no select on the address)
+      lds[j] = pz < NP ? pz * NR + (C::R0 - TL) + r : -1;  // (-1: the sink)
+      const int roff = base + min(pz, NP - 1) * pzb + r * pitchb;
       lv[j] = bload(rs, lane_ld + roff, (V2*)nullptr);
     }
+    // a compiler memory barrier: the loads may not sink below it towards their first use -- they
+    // must all be in flight while the noise words are drawn
+    asm volatile("" ::: "memory");
     // the noise words of every item this wave will compute, at every level, while the loads
     // are in flight (they depend on the cell and the step only)
     if constexpr (C::NOISE) {
@@ -417,8 +426,10 @@ __global__ __launch_bounds__(64 * C::NW, 1) void k_block_sl(const typename C::V2
     }
     V2(*b0)[64] = &buf[0][0][0];
 #pragma unroll
-    for (int j = 0; j < JL; ++j)
-      if (lds[j] >= 0) b0[lds[j]][lane] = lv[j];
+    for (int j = 0; j < JL; ++j) {
+      V2* dst = lds[j] >= 0 ? &b0[lds[j]][lane] : &sink[lane];
+      *dst = lv[j];
+    }
   }
   // rows the quads read beyond the cone (level 0: R0-5 .. R0-T-1 and R0+BY+T .. NR-1; the
   // level-1 buffer's first and last rows are never computed): defined zeros
