@@ -102,7 +102,7 @@ class HipBackend final : public gs::Backend {
   // the shell variant chosen per (depth, sides) (see shell())
   struct ShellChoice {
     int n, sides, variant;
-    float ms[3];
+    float ms[2];
   };
 
   HipBackend(const Geom& g, const gs::Params& p, void* b0, void* b1, void* send, void* recv,
@@ -125,10 +125,6 @@ class HipBackend final : public gs::Backend {
     int lo = 0, hi = 0;
     HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
     HIP_CHECK(hipStreamCreateWithPriority(&comm_stream_, hipStreamNonBlocking, hi));
-    // the shell's side stream (shell variant 2), also high priority: it is on the critical path
-    HIP_CHECK(hipStreamCreateWithPriority(&side_stream_, hipStreamNonBlocking, hi));
-    HIP_CHECK(hipEventCreateWithFlags(&ev_side_, hipEventDisableTiming));
-    HIP_CHECK(hipEventCreateWithFlags(&ev_side_join_, hipEventDisableTiming));
     xs_ = stream_;
   }
   ~HipBackend() override {
@@ -142,9 +138,6 @@ class HipBackend final : public gs::Backend {
       if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : prof_ev_) (void)hipEventDestroy(e);
     if (comm_stream_) (void)hipStreamDestroy(comm_stream_);
-    if (side_stream_) (void)hipStreamDestroy(side_stream_);
-    if (ev_side_) (void)hipEventDestroy(ev_side_);
-    if (ev_side_join_) (void)hipEventDestroy(ev_side_join_);
   }
 
   void fill_box(int b, const Box& bx, double u, double v) override {
@@ -227,24 +220,23 @@ class HipBackend final : public gs::Backend {
   }
 
   // The shell of an overlapped pass (engine.h shell_run): the n-deep slabs at the faces in
-  // `sides`.  Three ways, timed against each other at first use per (n, sides) and the fastest
+  // `sides`.  Two ways, timed against each other at first use per (n, sides) and the faster
   // kept: (0) one k_slab launch for every face; (1) the z slabs as one two-run k_fused launch
-  // (its own tuned tile) and the x / y slabs as a k_slab launch after it; (2) the same two
-  // launches side by side -- the z slabs on a side stream forked from and joined back into the
-  // shell's stream (they write disjoint cells and only read the source buffer; each launch is
-  // latency-bound and leaves most of the device idle).
+  // (its own tuned tile) and the x / y slabs as a k_slab launch after it.  (Round 4 also tried
+  // the two launches of (1) side by side, the z slabs on a forked side stream: 49.6 us vs 38.3
+  // sequential and 26.2 for (0), one-sided 256^3 at k=3, profiles/r4_shell.txt -- removed.)
   bool shell(int src, int dst, int n, int64_t t, int sides, int variant) override {
     if (!gsk::fused_supported(g_, n) || !sides) return sides == 0;
     if (!tuned_[n]) autotune(src, dst, n, t);
     if (variant >= 0) {
-      shell_variant(src, dst, n, t, sides, variant % 3);
+      shell_variant(src, dst, n, t, sides, variant & 1);
       return true;
     }
     ShellChoice* sc = nullptr;
     for (ShellChoice& q : shells_)
       if (q.n == n && q.sides == sides) sc = &q;
     if (!sc) {
-      shells_.push_back(ShellChoice{n, sides, 0, {0.f, 0.f, 0.f}});
+      shells_.push_back(ShellChoice{n, sides, 0, {0.f, 0.f}});
       sc = &shells_.back();
       if (sides & 48) {
         // warm both (the first k_fused z-run launch tunes its own shape), then best of 3
@@ -253,9 +245,9 @@ class HipBackend final : public gs::Backend {
         hipEvent_t e0, e1;
         HIP_CHECK(hipEventCreate(&e0));
         HIP_CHECK(hipEventCreate(&e1));
-        float best[3] = {1e30f, 1e30f, 1e30f};
+        float best[2] = {1e30f, 1e30f};
         for (int r = 0; r < 4; ++r)
-          for (int v = 0; v < 3; ++v) {
+          for (int v = 0; v < 2; ++v) {
             HIP_CHECK(hipEventRecord(e0, stream_));
             shell_variant(src, dst, n, t, sides, v);
             HIP_CHECK(hipEventRecord(e1, stream_));
@@ -267,10 +259,9 @@ class HipBackend final : public gs::Backend {
         (void)hipEventDestroy(e0);
         (void)hipEventDestroy(e1);
         xs_ = keep;
-        sc->variant = 0;
-        for (int v = 1; v < 3; ++v)
-          if (best[v] < best[sc->variant]) sc->variant = v;
-        for (int v = 0; v < 3; ++v) sc->ms[v] = best[v];
+        sc->variant = best[1] < best[0] ? 1 : 0;
+        sc->ms[0] = best[0];
+        sc->ms[1] = best[1];
       }
     }
     shell_variant(src, dst, n, t, sides, sc->variant);
@@ -279,30 +270,16 @@ class HipBackend final : public gs::Backend {
 
   void shell_variant(int src, int dst, int n, int64_t t, int sides, int variant) {
     int slab_sides = sides;
-    bool joined = false;
-    if (variant >= 1 && (sides & 48)) {
+    if (variant == 1 && (sides & 48)) {
       const int la = (sides & 16) ? n : 0, lb = (sides & 32) ? n : 0;
-      hipStream_t keep = xs_;
-      if (variant == 2 && (sides & 15)) {
-        // fork: the side stream starts where the shell's stream is now
-        HIP_CHECK(hipEventRecord(ev_side_, keep));
-        HIP_CHECK(hipStreamWaitEvent(side_stream_, ev_side_, 0));
-        xs_ = side_stream_;
-        joined = true;
-      }
       if (la > 0) fused_runs(src, dst, n, t, 0, la, g_.nz - lb, lb, false, 0);
       else fused_runs(src, dst, n, t, g_.nz - lb, lb, 0, 0, false, 0);
-      xs_ = keep;
       slab_sides = sides & 15;
     }
     if (slab_sides) {
       if (!gsk::launch_shell<T>(buf_[src], buf_[dst], g_, p_, n, t, slab_sides, num_cus(), xs_))
         throw std::runtime_error("shell: unsupported sub-domain (needs >= 2n cells per axis)");
       HIP_CHECK(hipGetLastError());
-    }
-    if (joined) {  // join: the shell's stream continues after both launches
-      HIP_CHECK(hipEventRecord(ev_side_join_, side_stream_));
-      HIP_CHECK(hipStreamWaitEvent(xs_, ev_side_join_, 0));
     }
   }
 
@@ -943,8 +920,6 @@ class HipBackend final : public gs::Backend {
   std::vector<hipEvent_t> prof_ev_;  // per-phase timing events (prof_reserve)
   int prof_n_ = 0;
   hipStream_t comm_stream_ = nullptr;
-  hipStream_t side_stream_ = nullptr;  // shell variant 2: the z slabs beside the x / y slabs
-  hipEvent_t ev_side_ = nullptr, ev_side_join_ = nullptr;
   hipStream_t xs_ = nullptr;  // stream for halo traffic (compute or comm stream)
   bool inplace_off_ = getenv("GS_INPLACE_HALO") && atoi(getenv("GS_INPLACE_HALO")) == 0;
   int dev_ = 0;

@@ -15,7 +15,8 @@
 // noise quads, so one Philox draw serves 4 cells as in k_fused), and writes the last level
 // straight to HBM.  The intermediate levels are recomputed on the block's halo (the dependency
 // cone), which costs 2.5-3.7x the useful cell updates -- cheap at this size, where the chip is
-// otherwise idle (L=64: 55k -> 81k MLUPS, profiles/r3_block.txt).
+// otherwise idle (L=64: 55k -> 81k MLUPS in round 3, profiles/r3_block.txt; 99k with round 4's
+// scalar-unit work cut, below).
 //
 // Scope: x rows fit one wave (nx <= 64) and both x faces are the global (non-periodic)
 // boundary, so no x halo is computed: a level's x ghost is the boundary value of its time level
@@ -36,7 +37,7 @@ struct BlockArgs {
 };
 
 template <typename T_, int TL_, int BY_, int BZ_, int NW_, bool NOISE_, bool KV_ = true,
-          bool LH_ = false, bool SL_ = false>
+          bool LH_ = false>
 struct BCfg {
   using T = T_;
   using V2 = typename PairT<T>::type;
@@ -48,16 +49,12 @@ struct BCfg {
   // the last level's items are half quads (2 rows): it has only BY/4 x BZ quads, so whole-quad
   // items leave most waves idle there; the halves' Philox draws happen in the load shadow
   static constexpr bool LH = LH_;
-  // SALU-lean variant (k_block_sl): the scalar unit, one per CU and shared by its 16 waves, was
-  // this kernel's bottleneck (per wave ~1050 SALU vs ~610 VALU instructions in the code object,
-  // r3_final_check.txt: 2.72 M SALU vs 1.70 M VALU per pass)
-  static constexpr bool SL = SL_;
   // LDS rows: local y0-5 .. y0+BY+4 (intermediate levels compute the quads [y0-4, y0+BY+4) and
   // read one row beyond); LDS planes z0-T .. z0+BZ+T-1
   static constexpr int R0 = 5;
   static constexpr int NR = BY + 10;
   static constexpr int NP = BZ + 2 * TL;
-  static constexpr int LDS_BYTES = 2 * NP * NR * 64 * (int)sizeof(V2);
+  static constexpr int LDS_BYTES = (2 * NP * NR + 1) * 64 * (int)sizeof(V2);  // + the load sink
   // whether the two level buffers fit the CU's LDS (run_block falls back to k_fused if not)
   static constexpr bool FITS = LDS_BYTES <= 160 * 1024;  // (= fused.hpp block_cfg_fits)
   static_assert(BY % 4 == 0, "blocks hold whole noise quads");
@@ -82,192 +79,21 @@ __device__ __forceinline__ void for_levels(F&& f) {
   for_levels_impl(f, std::make_integer_sequence<int, N>{});
 }
 
-template <class C>
-__global__ __launch_bounds__(64 * C::NW, 1) void k_block(const typename C::V2* __restrict__ s,
-                                                       typename C::V2* __restrict__ d,
-                                                       BlockArgs a, FoldCoef<typename C::T> f,
-                                                       uint64_t seed) {
-  using T = typename C::T;
-  using V2 = typename C::V2;
-  constexpr int TL = C::TL, BY = C::BY, BZ = C::BZ, NW = C::NW, NR = C::NR, NP = C::NP;
-  __shared__ V2 buf[2][NP][NR][64];  // [level parity][plane][row][lane]
-  const Geom& g = a.g;
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int by = blockIdx.x % a.nby, bz = blockIdx.x / a.nby;
-  const int y0 = a.yb + by * BY, z0 = bz * BZ;
-
-  V2 kc;
-  {
-    const T k0 = f.kc.x, k1 = f.kc.y;
-    asm volatile("v_mov_b32 %0, %1" : "=v"(kc.x) : "s"(k0));
-    asm volatile("v_mov_b32 %0, %1" : "=v"(kc.y) : "s"(k1));
-  }
-  const T ar31 = f.ar * (T)4.656612873077392578125e-10;
-  const uint32_t Ly4 = (uint32_t)((g.Ly + 3) >> 2);
-  gs::U4 W[TL][C::JMAX];  // noise words per (level, item of this wave)
-  uint32_t kv[C::KV ? 14 : 1];
-  if constexpr (C::KV) {
-#pragma unroll
-    for (int r = 3; r < 10; ++r) {
-      const uint32_t k0 = (uint32_t)seed + (uint32_t)r * kPhW0;
-      const uint32_t k1 = (uint32_t)(seed >> 32) + (uint32_t)r * kPhW1;
-      asm volatile("v_mov_b32 %0, %1" : "=v"(kv[2 * (r - 3)]) : "s"(k0));
-      asm volatile("v_mov_b32 %0, %1" : "=v"(kv[2 * (r - 3) + 1]) : "s"(k1));
-    }
-  }
-
-  // level 0: the outputs' dependency cone, rows y0-T .. y0+BY+T-1 of every plane.  Rows /
-  // planes outside the storage (beyond the H-deep ghosts) and lanes past the row's last ghost
-  // read 0: they only feed cells outside every stored output's cone.
-  // Every load of a wave is issued before the first LDS write (one memory latency, not one per
-  // row): a fully unrolled loop into registers, through plane buffer descriptors whose
-  // out-of-range accesses return 0 (no branches).
-  constexpr int NL = BY + 2 * TL;
-  constexpr int NLD = NP * NL;
-  constexpr int JL = (NLD + NW - 1) / NW;
-  {
-    const int pzb = (int)(gs::plane_elems(g) * (int64_t)sizeof(V2));
-    V2 lv[JL];
-#pragma unroll
-    for (int j = 0; j < JL; ++j) {
-      const int i = wave + j * NW;
-      const int pz = i / NL, ry = C::R0 - TL + (i - pz * NL);
-      const int z = z0 - TL + pz, y = y0 - C::R0 + ry;
-      const bool ok = i < NLD && z >= -g.H && z < g.nz + g.H && y >= -g.H && y < g.ny + g.H;
-      const __amdgpu_buffer_rsrc_t r =
-          plane_rsrc((const char*)s + (int64_t)(ok ? z + g.H : 0) * pzb, ok ? pzb : 0);
-      const int off = lane < g.nx + g.H ? ((y + g.H) * g.px + lane + g.xo) * (int)sizeof(V2)
-                                        : (int)0x80000000;
-      lv[j] = bload(r, off, (V2*)nullptr);
-    }
-    // the noise words of every item this wave will compute, at every level, while the loads
-    // are in flight (they depend on the cell and the step only)
-    if constexpr (C::NOISE) {
-      for_levels<TL>([&](auto LC) {
-        constexpr int l = decltype(LC)::value;
-#pragma unroll
-        for (int j = 0; j < C::per_wave(l); ++j) {
-          const int it = wave + j * NW;
-          if (it < C::items(l)) {
-            constexpr int S = C::S(l);
-            const int zi = it / (C::nq(l) * S), rem = it - zi * (C::nq(l) * S);
-            const int qi = rem / S, h = rem - qi * S;
-            const int qy = y0 - (l + 1 < TL ? 4 : 0) + 4 * qi;
-            const int z = z0 - (TL - 1 - l) + zi;
-            const uint32_t gy4 = (uint32_t)((g.oy + qy) >> 2);
-            const uint32_t qu = (uint32_t)g.Lx * (gy4 + Ly4 * (uint32_t)(g.oz + z));
-            const gs::U4 q = philox_dev<true, C::KV>(qu + (uint32_t)(g.ox + lane), 0u,
-                                                     (uint64_t)(a.t + l), seed, kv);
-            W[l][j] = (S == 1 || h == 0) ? q : gs::U4{q.z, q.w, q.z, q.w};  // a half's words first
-          }
-        }
-      });
-    }
-#pragma unroll
-    for (int j = 0; j < JL; ++j) {
-      const int i = wave + j * NW;
-      const int pz = i / NL, ry = C::R0 - TL + (i - pz * NL);
-      if (i < NLD) buf[0][pz][ry][lane] = lv[j];
-    }
-  }
-  // rows the quads read beyond the cone (level 0: R0-5 .. R0-T-1 and R0+BY+T .. NR-1; the
-  // level-1 buffer's first and last rows are never computed): defined zeros
-  constexpr int NZR = C::R0 - TL;  // zero rows per side of level 0
-  for (int i = wave; i < NP * (2 * NZR + 2); i += NW) {
-    const int pz = i / (2 * NZR + 2), j = i - pz * (2 * NZR + 2);
-    if (j < 2 * NZR) buf[0][pz][j < NZR ? j : NR - 2 * NZR + j][lane] = V2{(T)0, (T)0};
-    else buf[1][pz][j == 2 * NZR ? 0 : NR - 1][lane] = V2{(T)0, (T)0};
-  }
-  __syncthreads();
-
-  for_levels<TL>([&](auto LC) {
-    constexpr int l = decltype(LC)::value;
-    const V2(*in)[NR][64] = buf[l & 1];
-    V2(*out)[NR][64] = buf[(l + 1) & 1];
-    constexpr bool last = l + 1 == TL;
-    const int mq = last ? 0 : 1;          // intermediate levels: one quad of halo each side
-    const int nq = C::nq(l);
-    const int dz = TL - 1 - l;            // planes of halo this level still needs
-    // x ghosts of level l (the input): the level's boundary value -- for level 0 the engine's
-    // ensure_bc fill (only Backend::fused() launches k_block, always after it), above it
-    // k_fused's reset rule.  Lane 0's left neighbour is added last in the sum
-    // (in[x-1] + (in[x+1] + yz)), so adding it after the DPP sum (where the missing lane read
-    // 0) is exact; lane 63's right neighbour is added first, so it goes into yz before the DPP
-    // sum.  Other lanes add +0.
-    const T bin = (T)gs::bc_u(a.t + l);
-    const V2 gl = lane == 0 ? V2{bin, (T)0} : V2{(T)0, (T)0};
-    const V2 gr = (a.gr && lane == 63) ? V2{bin, (T)0} : V2{(T)0, (T)0};
-    const T bout = (T)gs::bc_u(a.t + l + 1);
-#pragma unroll
-    for (int j = 0; j < C::per_wave(l); ++j) {
-      const int it = wave + j * NW;
-      if (it >= C::items(l)) break;  // wave-uniform
-      constexpr int S = C::S(l), HR = 4 / S;  // rows per item
-      const int zi = it / (nq * S), rem = it - zi * (nq * S);
-      const int qi = rem / S, h = rem - qi * S;
-      const int qy = y0 - 4 * mq + 4 * qi + HR * h;  // local y of the item's first row
-      const int z = z0 - dz + zi;
-      const int pz = z - (z0 - TL);
-      const int ry = qy - y0 + C::R0;
-      V2 row[6], pm[4], pp[4];
-#pragma unroll
-      for (int k = 0; k < HR + 2; ++k) row[k] = lds_load2(&in[pz][ry - 1 + k][lane]);
-#pragma unroll
-      for (int k = 0; k < HR; ++k) {
-        pm[k] = lds_load2(&in[pz - 1][ry + k][lane]);
-        pp[k] = lds_load2(&in[pz + 1][ry + k][lane]);
-      }
-      const int64_t gz = g.oz + z;
-      // k_fused's counter gx + Lx * (gy4 + Ly4 * gz) (fits 32 bits: host check), drawn above
-      const gs::U4 blk = C::NOISE ? W[l][j] : gs::U4{0, 0, 0, 0};
-      const bool zout = gz < 0 || gz >= g.Lz;
-      const bool xout = g.ox + lane >= g.Lx;
-#pragma unroll
-      for (int k = 0; k < HR; ++k) {
-        const V2 c = row[k + 1];
-        V2 yz = (row[k] + row[k + 2]) + pm[k];
-        if (a.gr) yz = yz + gr;
-        V2 A{lane_pair_sum_add<false>(c.x, yz.x), lane_pair_sum_add<false>(c.y, yz.y)};
-        A = A + gl;
-        const V2 sum = A + pp[k];
-        const V2 tt = c * c.yy;
-        const V2 uvv = tt.xx * c.yy;
-        V2 P = __builtin_elementwise_fma(f.kd, uvv, kc);
-        P = __builtin_elementwise_fma(f.ks, sum, P);
-        P = __builtin_elementwise_fma(f.kcc, c, P);
-        if constexpr (C::NOISE) {
-          const uint32_t w = k == 0 ? blk.x : (k == 1 ? blk.y : (k == 2 ? blk.z : blk.w));
-          P.x = fma(ar31, (T)(int32_t)w, P.x);
-        }
-        const int y = qy + k;
-        if (!last) {
-          const int64_t gy = g.oy + y;
-          if (zout || xout || gy < 0 || gy >= g.Ly) P = V2{bout, (T)0};
-          out[pz][ry + k][lane] = P;
-        } else if (lane < g.nx && y >= 0 && y < g.ny && z < g.nz) {
-          d[gs::lin(g, lane, y, z)] = P;
-        }
-      }
-    }
-    if (!last) __syncthreads();
-  });
-}
-
 // ------------------------------------------------------------------------------------------
-// k_block_sl: the same block computation with the scalar work cut (BCfg::SL).  The scalar unit is
-// shared by the CU's waves, so with 16 waves per CU the per-wave SALU count, not the VALU count,
-// set k_block's pass time: in its code object a wave issues ~540 SALU before the first barrier
-// (a division per load, storage-bounds checks and a descriptor per load, the Philox rounds 1-3
-// key schedule per draw) and ~140 per level item (64-bit row / plane bounds, exec-masked boundary
-// resets, 64-bit store addresses), ~1050 in all against ~610 VALU.  Here:
+// The kernel is written for the scalar unit: it is shared by the CU's waves, so with 16 waves per
+// CU the per-wave SALU count, not the VALU count, sets the pass time.  Round 3's version issued
+// per wave ~540 SALU before the first barrier (a division per load, storage-bounds checks and a
+// descriptor per load, the Philox rounds 1-3 key schedule per draw) and ~140 per level item
+// (64-bit row / plane bounds, exec-masked boundary resets, 64-bit store addresses), ~1050 in all
+// against ~610 VALU; L=64 ran at 81k MLUPS.  This one issues ~630 SALU (L=64: 99k MLUPS,
+// profiles/r4_block_sl.txt):
 //   * one buffer descriptor over each whole state buffer (< 1 GiB: block_supported): a row or plane
 //     outside the storage is an offset outside the buffer (loads read 0, stores are dropped), and
 //     a load's plane / row come from a per-wave split of the wave index plus one carry;
 //   * the step-uniform words of each level's Philox rounds 1-3 (philox_uniform) once per level;
 //   * boundary resets as bit selects (a per-lane x mask, a uniform row condition; no exec
 //     branches), 32-bit coordinates, stores through the descriptor behind a uniform row branch.
-// Bit-identical to k_block / k_fused: same sum order, Philox words and resets.
+// Bit-identical to k_fused: same sum order, Philox words and resets.
 // ------------------------------------------------------------------------------------------
 
 // The step-uniform part of philox_dev<true>(c0, 0, step, seed): the words of rounds 1-3 that do
@@ -326,13 +152,13 @@ __device__ __forceinline__ float fsel(uint32_t m, float a, float b) {
 }
 
 template <class C>
-__global__ __launch_bounds__(64 * C::NW, 1) void k_block_sl(const typename C::V2* __restrict__ s,
+__global__ __launch_bounds__(64 * C::NW, 1) void k_block(const typename C::V2* __restrict__ s,
                                                           typename C::V2* __restrict__ d,
                                                           BlockArgs a, FoldCoef<typename C::T> f,
                                                           uint64_t seed) {
   using T = typename C::T;
   using V2 = typename C::V2;
-  static_assert(sizeof(T) == 4 && C::KV, "the SALU-lean block kernel: fp32, VGPR Philox keys");
+  static_assert(sizeof(T) == 4 && C::KV, "k_block: fp32, Philox round keys in VGPRs");
   constexpr int TL = C::TL, BY = C::BY, BZ = C::BZ, NW = C::NW, NR = C::NR, NP = C::NP;
   __shared__ V2 buf[2][NP][NR][64];  // [level parity][plane][row][lane]
   const Geom& g = a.g;
@@ -527,12 +353,8 @@ bool run_block(const void* s, void* d, const FusedArgs& a0, const gs::Params& p,
   a.gr = g.nx == 64 ? 1 : 0;
   const int nbz = (g.nz + C::BZ - 1) / C::BZ;
   const FoldCoef<typename C::T> f = make_fold<typename C::T>(p);
-  if constexpr (C::SL)
-    k_block_sl<C><<<(unsigned)(a.nby * nbz), 64 * C::NW, 0, st>>>(
-        (const typename C::V2*)s, (typename C::V2*)d, a, f, p.seed);
-  else
-    k_block<C><<<(unsigned)(a.nby * nbz), 64 * C::NW, 0, st>>>(
-        (const typename C::V2*)s, (typename C::V2*)d, a, f, p.seed);
+  k_block<C><<<(unsigned)(a.nby * nbz), 64 * C::NW, 0, st>>>(
+      (const typename C::V2*)s, (typename C::V2*)d, a, f, p.seed);
   return true;
   }
 }
@@ -540,7 +362,7 @@ bool run_block(const void* s, void* d, const FusedArgs& a0, const gs::Params& p,
 // whether k_block can run this launch: one Backend::fused() allows (its x ghosts are the
 // boundary values ensure_bc wrote), the whole interior (no z-runs / store mask / reserve),
 // whole non-periodic x rows of at most 64 cells, a 32-bit Philox counter, state buffers below
-// 1 GiB (k_block_sl addresses a whole buffer through one descriptor)
+// 1 GiB (k_block addresses a whole buffer through one descriptor)
 inline bool block_supported(const FusedArgs& a) {
   const Geom& g = a.g;
   if (gs::total_elems(g) * 16 >= (int64_t)1 << 30) return false;

@@ -221,7 +221,9 @@ __device__ __forceinline__ gs::U4 philox_dev(uint32_t c0, uint32_t c1, uint64_t 
 //                  WRONG by design): bit0 no workgroup barriers, bit1 every level-0 load reads
 //                  plane 0 (L2-resident); bit2 (exact) Philox round keys 4-10 in VGPRs; bit3
 //                  (exact) the x-neighbour sums' leading s_nop restored; bit4 (exact) the
-//                  pipeline fill computes every level (no FILL skip)
+//                  pipeline fill computes every level (no FILL skip); bit5 (exact) Philox only
+//                  on lanes inside the x cone; bit6 (exact) Philox keys rebuilt on the SALU
+//                  (KV off)
 constexpr int gs_gcd(int a, int b) { return b == 0 ? a : gs_gcd(b, a % b); }
 constexpr int gs_lcm(int a, int b) { return a / gs_gcd(a, b) * b; }
 
@@ -233,7 +235,6 @@ struct FCfg {
   static constexpr int TL = TL_, ROWS = ROWS_, WAVES = WAVES_, PF = PF_;
   static constexpr bool PERIODIC = PERIODIC_, NOISE = NOISE_, SKEW = SKEW_, Q32 = Q32_;
   static constexpr int ABL = ABL_;
-  static constexpr bool KV = (ABL_ & 4) != 0;
   static constexpr int R = PF + 2;                    // level-0 ring slots
   // level-l output ring / xch buffers: 2 slots.  Skewed: level l+1 reads level l's outputs of
   // the two previous iterations (input and centre), and the levels run top-down within an
@@ -250,6 +251,13 @@ struct FCfg {
   static constexpr int WPEU =
       (sizeof(T) == 4 && ROWS == 4) ? ((WAVES == 8 || WAVES == 16) ? 4 : 3)
       : (sizeof(T) == 8 && ROWS == 4 && (WAVES == 6 || WAVES == 8)) ? 2 : 1;
+  // Philox round keys 4-10 in VGPRs (filled once per kernel) instead of rebuilt on the SALU at
+  // every draw, where the register budget has room for the 14 keys: fp32 shapes of <= 168 VGPRs
+  // (the 128-VGPR shapes would spill, the fp64 ones are near 256).  L=512 T=3, random init, the
+  // driver's window: 4x12:2s 689k -> 719k, 4x12:1s 695-698k -> 703-705k MLUPS (profiles/
+  // r4_fused_ab.txt).  ABL bit 6 turns it off (A/B), bit 2 forces it on.
+  static constexpr bool KV =
+      (ABL_ & 4) != 0 || (sizeof(T) == 4 && WPEU == 3 && (ABL_ & 64) == 0);
   // pipeline-fill level skip (fused_iter FILL periods): its second copy of the unrolled body
   // costs ~16 VGPRs, free only where the budget is 168 or 256 (WPEU 3 / 2); with 128 it spills
   // or halves the occupancy (4x8:1s: -10 % at L=512, profiles/r2_fill_skip.txt)
@@ -801,22 +809,19 @@ inline const FusedCfgEntry* fused_cfg_table(int* n) {
       {"blk8x4w16", true, false},  // 24  (T=2 only: T=3 levels do not fit the LDS)
       {"blk8x2w16l", true, false}, // 25  last level in half-quad items
       {"blk4x4w16l", true, false}, // 26  last level in half-quad items
-      // the same shapes through the SALU-lean block kernel (block.hpp SL: one buffer descriptor,
-      // per-wave load indexing, step-uniform Philox parts hoisted, branch-free boundary resets)
-      {"blk8x2w16s", true, false}, // 27
-      {"blk4x4w16s", true, false}, // 28
-      {"blk8x2w8s", true, false},  // 29
 #ifdef GS_ABLATION
-      {"4x12:2s-abl1", true, false},  // 30  no barriers
-      {"4x12:2s-abl2", true, false},  // 31  L2-resident loads
-      {"4x12:1s-abl4", true, false},  // 32  Philox keys in VGPRs (exact)
-      {"4x12:2s-abl4", true, false},  // 33  Philox keys in VGPRs (exact)
-      {"4x12:1s-abl8", true, false},  // 34  DPP sums with the s_nop (exact)
-      {"4x12:1s-abl12", true, false}, // 35  abl4 + abl8 (exact)
-      {"4x12:1s-abl16", true, false}, // 36  pipeline fill computes every level (exact)
-      {"4x8:1s-abl16", true, true},   // 37  pipeline fill computes every level (exact)
-      {"4x6:2s-abl16", true, true},   // 38  pipeline fill computes every level (exact)
-      {"4x12:1s-abl32", true, false}, // 39  Philox only on lanes in the x cone (exact)
+      {"4x12:2s-abl1", true, false},  // 27  no barriers
+      {"4x12:2s-abl2", true, false},  // 28  L2-resident loads
+      {"4x12:1s-abl4", true, false},  // 29  Philox keys in VGPRs (exact)
+      {"4x12:2s-abl4", true, false},  // 30  Philox keys in VGPRs (exact)
+      {"4x12:1s-abl8", true, false},  // 31  DPP sums with the s_nop (exact)
+      {"4x12:1s-abl12", true, false}, // 32  abl4 + abl8 (exact)
+      {"4x12:1s-abl16", true, false}, // 33  pipeline fill computes every level (exact)
+      {"4x8:1s-abl16", true, true},   // 34  pipeline fill computes every level (exact)
+      {"4x6:2s-abl16", true, true},   // 35  pipeline fill computes every level (exact)
+      {"4x12:1s-abl32", true, false}, // 36  Philox only on lanes in the x cone (exact)
+      {"4x12:2s-abl64", true, false}, // 37  Philox keys rebuilt on the SALU (exact)
+      {"4x12:1s-abl64", true, false}, // 38  Philox keys rebuilt on the SALU (exact)
 #endif
   };
   *n = (int)(sizeof(t) / sizeof(t[0]));
@@ -829,12 +834,12 @@ inline bool fused_cfg_is_block(int i) {
   return i > 0 && i < n && !strncmp(t[i].name, "blk", 3);
 }
 
-// whether block configuration i (table entries 20-29: output blocks of BY rows x BZ planes)
+// whether block configuration i (table entries 20-26: output blocks of BY rows x BZ planes)
 // holds its two level buffers in the CU's LDS at depth tl -- BCfg::FITS without instantiating
 // it; a configuration that does not fit would run the default k_fused shape under its name
-constexpr int kBlkBY[10] = {8, 4, 8, 4, 8, 8, 4, 8, 4, 8}, kBlkBZ[10] = {2, 4, 2, 4, 4, 2, 4, 2, 4, 2};
+constexpr int kBlkBY[7] = {8, 4, 8, 4, 8, 8, 4}, kBlkBZ[7] = {2, 4, 2, 4, 4, 2, 4};
 constexpr bool block_k_fits(int k, int tl, int pair_bytes) {
-  return 2 * (kBlkBZ[k] + 2 * tl) * (kBlkBY[k] + 10) * 64 * pair_bytes <= 160 * 1024;
+  return (2 * (kBlkBZ[k] + 2 * tl) * (kBlkBY[k] + 10) + 1) * 64 * pair_bytes <= 160 * 1024;
 }
 static_assert(block_k_fits(0, 3, 8) == BCfg<float, 3, 8, 2, 8, true>::FITS &&
                   block_k_fits(4, 3, 8) == BCfg<float, 3, 8, 4, 16, true>::FITS &&
@@ -843,7 +848,7 @@ static_assert(block_k_fits(0, 3, 8) == BCfg<float, 3, 8, 2, 8, true>::FITS &&
                   !block_k_fits(4, 3, 8) && block_k_fits(4, 2, 8),
               "block_cfg_fits must match BCfg::FITS");
 inline bool block_cfg_fits(int i, int tl, int pair_bytes) {
-  if (!fused_cfg_is_block(i) || i < 20 || i > 29) return true;
+  if (!fused_cfg_is_block(i) || i < 20 || i > 26) return true;
   return block_k_fits(i - 20, tl, pair_bytes);
 }
 
@@ -884,8 +889,8 @@ void run_fused_cfg(const void* s, void* d, const FusedArgs& a, const gs::Params&
       case 16: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
       case 17: FusedLaunch<FCfg<T, TL, 4, 4, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
 #ifdef GS_ABLATION
-      case 37: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
-      case 38: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 34: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 35: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
 #endif
       default: break;
     }
@@ -915,20 +920,19 @@ void run_fused_cfg(const void* s, void* d, const FusedArgs& a, const gs::Params&
       case 24: if (block_supported(a) && run_block<BCfg<T, TL, 8, 4, 16, NZ>>(s, d, a, p, st)) return; break;
       case 25: if (block_supported(a) && run_block<BCfg<T, TL, 8, 2, 16, NZ, true, true>>(s, d, a, p, st)) return; break;
       case 26: if (block_supported(a) && run_block<BCfg<T, TL, 4, 4, 16, NZ, true, true>>(s, d, a, p, st)) return; break;
-      case 27: if (block_supported(a) && run_block<BCfg<T, TL, 8, 2, 16, NZ, true, false, true>>(s, d, a, p, st)) return; break;
-      case 28: if (block_supported(a) && run_block<BCfg<T, TL, 4, 4, 16, NZ, true, false, true>>(s, d, a, p, st)) return; break;
-      case 29: if (block_supported(a) && run_block<BCfg<T, TL, 8, 2, 8, NZ, true, false, true>>(s, d, a, p, st)) return; break;
 #ifdef GS_ABLATION
-      case 30: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 1>, T>::run(s, d, a, p, st); return;
-      case 31: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 2>, T>::run(s, d, a, p, st); return;
-      case 32: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;
-      case 33: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;
-      case 34: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 8>, T>::run(s, d, a, p, st); return;
-      case 35: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 12>, T>::run(s, d, a, p, st); return;
-      case 36: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
-      case 37: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
-      case 38: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
-      case 39: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 32>, T>::run(s, d, a, p, st); return;
+      case 27: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 1>, T>::run(s, d, a, p, st); return;
+      case 28: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 2>, T>::run(s, d, a, p, st); return;
+      case 29: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;
+      case 30: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;
+      case 31: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 8>, T>::run(s, d, a, p, st); return;
+      case 32: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 12>, T>::run(s, d, a, p, st); return;
+      case 33: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 34: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 35: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 36: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 32>, T>::run(s, d, a, p, st); return;
+      case 37: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 64>, T>::run(s, d, a, p, st); return;
+      case 38: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 64>, T>::run(s, d, a, p, st); return;
 #endif
       default: break;  // 0 and 14: the default shape below
     }

@@ -29,8 +29,7 @@ int gs_set_auto_depth(gs_engine* e, int32_t on);  // let prepare() pick the dept
 int gs_plan_zplanes(gs_engine* e);               // 1 if halos are whole contiguous z planes
 int gs_fused_runs_raw(gs_engine* e, int32_t k, int32_t zlo0, int32_t zlen0, int32_t zlo1,
                       int32_t zlen1, int32_t mask, int32_t leave_room);  // timing (state unchanged)
-// variant: -1 the tuned choice, 0 all faces through k_slab, 1 z faces through k_fused, 2 the
-// same two launches concurrently (z slabs on a side stream)
+// variant: -1 the tuned choice, 0 all faces through k_slab, 1 z faces through k_fused
 int gs_shell_raw(gs_engine* e, int32_t k, int32_t sides, int32_t variant);
 int gs_advance(gs_engine* e, int64_t nsteps);
 int gs_exchange(gs_engine* e);

@@ -96,9 +96,9 @@ def main():
                 if bits:
                     for v in ((0, 1) if name == "z" else (0,)):
                         faces[f"{name}_v{v}_us"] = round(timed(("faces", bits, v)), 1)
-            # the whole shell through each variant (2: z slabs on a side stream, concurrently)
+            # the whole shell through each variant
             if (sides & 48) and (sides & 15):
-                for v in (0, 1, 2):
+                for v in (0, 1):
                     faces[f"all_v{v}_us"] = round(timed(("faces", sides, v)), 1)
             row = {"local": [a.L, a.L, nz], "k": k, "packed": a.packed, "faces": faces,
                    "one_sided": a.one_sided, "full_us": round(full, 1),

@@ -17,8 +17,7 @@ from grayscott_amd.utils.config import Settings
 
 pytestmark = pytest.mark.gpu
 
-BLOCKS = ["blk8x2w8", "blk4x4w8", "blk8x2w16", "blk4x4w16", "blk8x4w16", "blk8x2w16l", "blk4x4w16l",
-          "blk8x2w16s", "blk4x4w16s", "blk8x2w8s"]
+BLOCKS = ["blk8x2w8", "blk4x4w8", "blk8x2w16", "blk4x4w16", "blk8x4w16", "blk8x2w16l", "blk4x4w16l"]
 
 
 @pytest.fixture(scope="module", autouse=True)
