@@ -32,7 +32,7 @@ struct BlockArgs {
   Geom g;
   int64_t t;
   int32_t yb;   // local y of block row 0 (<= 0; (oy + yb) % 4 == 0: whole noise quads)
-  int32_t nby;  // blocks along y (grid = nby * ceil(nz / BZ))
+  int32_t nby;  // blocks along y (grid = nby x ceil(nz / BZ))
   int32_t gr;   // nx == 64: no lane holds the +x ghost; lane 63 adds it explicitly
 };
 
@@ -164,7 +164,7 @@ __global__ __launch_bounds__(64 * C::NW, 1) void k_block(const typename C::V2* _
   const Geom& g = a.g;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int by = blockIdx.x % a.nby, bz = blockIdx.x / a.nby;
+  const int by = blockIdx.x, bz = blockIdx.y;  // a 2D grid: no division by nby per wave
   const int y0 = a.yb + by * BY, z0 = bz * BZ;
 
   V2 kc;
@@ -353,7 +353,7 @@ bool run_block(const void* s, void* d, const FusedArgs& a0, const gs::Params& p,
   a.gr = g.nx == 64 ? 1 : 0;
   const int nbz = (g.nz + C::BZ - 1) / C::BZ;
   const FoldCoef<typename C::T> f = make_fold<typename C::T>(p);
-  k_block<C><<<(unsigned)(a.nby * nbz), 64 * C::NW, 0, st>>>(
+  k_block<C><<<dim3((unsigned)a.nby, (unsigned)nbz, 1), 64 * C::NW, 0, st>>>(
       (const typename C::V2*)s, (typename C::V2*)d, a, f, p.seed);
   return true;
   }
