@@ -96,56 +96,6 @@ __device__ __forceinline__ void for_levels(F&& f) {
 // Bit-identical to k_fused: same sum order, Philox words and resets.
 // ------------------------------------------------------------------------------------------
 
-// The step-uniform part of philox_dev<true>(c0, 0, step, seed): the words of rounds 1-3 that do
-// not depend on the lane's counter word c0.
-struct PhiloxU {
-  uint32_t x1, x2, x3, k3, x4;
-};
-
-__device__ __forceinline__ PhiloxU philox_uniform(uint64_t step, uint64_t seed) {
-  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-  const uint32_t s0 = (uint32_t)step, s1 = (uint32_t)(step >> 32);
-  PhiloxU u;
-  const uint64_t m1 = (uint64_t)kPhM1 * s0;          // round 1 (counter word 1 = 0)
-  const uint32_t u0 = (uint32_t)(m1 >> 32) ^ k0;
-  const uint32_t u1 = (uint32_t)m1;
-  u.x1 = s1 ^ k1;
-  k0 += kPhW0; k1 += kPhW1;
-  const uint64_t n0 = (uint64_t)kPhM0 * u0;          // round 2
-  u.x2 = u1 ^ k0;
-  u.x3 = (uint32_t)(n0 >> 32) ^ k1;
-  k0 += kPhW0; k1 += kPhW1;
-  u.k3 = k0;                                         // round 3
-  u.x4 = (uint32_t)n0 ^ k1;
-  return u;
-}
-
-// philox_dev<true, true>(c0, 0, step, seed, kv), given philox_uniform(step, seed)
-__device__ __forceinline__ gs::U4 philox_lane(uint32_t c0, const PhiloxU& u, const uint32_t* kv) {
-  const uint64_t m0 = (uint64_t)kPhM0 * c0;          // round 1
-  const uint32_t l2 = (uint32_t)(m0 >> 32) ^ u.x1;
-  const uint32_t l3 = (uint32_t)m0;
-  const uint64_t n1 = (uint64_t)kPhM1 * l2;          // round 2
-  uint32_t a0 = (uint32_t)(n1 >> 32) ^ u.x2;
-  uint32_t a2 = l3 ^ u.x3;
-  uint32_t a1 = (uint32_t)n1;
-  const uint64_t p0 = (uint64_t)kPhM0 * a0;          // round 3
-  const uint64_t p1 = (uint64_t)kPhM1 * a2;
-  a0 = xor3((uint32_t)(p1 >> 32), a1, u.k3);
-  a2 = (uint32_t)(p0 >> 32) ^ u.x4;
-  a1 = (uint32_t)p1;
-  uint32_t a3 = (uint32_t)p0;
-#pragma unroll
-  for (int r = 3; r < 10; ++r) {                     // rounds 4-10: round keys in VGPRs
-    const uint64_t m = (uint64_t)kPhM0 * a0;
-    const uint64_t n = (uint64_t)kPhM1 * a2;
-    const uint32_t b0 = xor3v((uint32_t)(n >> 32), a1, kv[2 * (r - 3)]);
-    const uint32_t b2 = xor3v((uint32_t)(m >> 32), a3, kv[2 * (r - 3) + 1]);
-    a0 = b0; a1 = (uint32_t)n; a2 = b2; a3 = (uint32_t)m;
-  }
-  return gs::U4{a0, a1, a2, a3};
-}
-
 // m ? b : a, bit by bit (one v_bfi_b32)
 __device__ __forceinline__ float fsel(uint32_t m, float a, float b) {
   return __uint_as_float((__float_as_uint(a) & ~m) | (__float_as_uint(b) & m));

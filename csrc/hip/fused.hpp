@@ -211,6 +211,83 @@ __device__ __forceinline__ gs::U4 philox_dev(uint32_t c0, uint32_t c1, uint64_t 
   return gs::U4{c0, c1, c2, c3};
 }
 
+// The step-uniform part of philox_dev<true>(c0, 0, step, seed): the words of rounds 1-3 that do
+// not depend on the lane's counter word c0.
+struct PhiloxU {
+  uint32_t x1, x2, x3, k3, x4;
+};
+
+__device__ __forceinline__ PhiloxU philox_uniform(uint64_t step, uint64_t seed) {
+  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+  const uint32_t s0 = (uint32_t)step, s1 = (uint32_t)(step >> 32);
+  PhiloxU u;
+  const uint64_t m1 = (uint64_t)kPhM1 * s0;          // round 1 (counter word 1 = 0)
+  const uint32_t u0 = (uint32_t)(m1 >> 32) ^ k0;
+  const uint32_t u1 = (uint32_t)m1;
+  u.x1 = s1 ^ k1;
+  k0 += kPhW0; k1 += kPhW1;
+  const uint64_t n0 = (uint64_t)kPhM0 * u0;          // round 2
+  u.x2 = u1 ^ k0;
+  u.x3 = (uint32_t)(n0 >> 32) ^ k1;
+  k0 += kPhW0; k1 += kPhW1;
+  u.k3 = k0;                                         // round 3
+  u.x4 = (uint32_t)n0 ^ k1;
+  return u;
+}
+
+// philox_dev<true, true>(c0, 0, step, seed, kv), given philox_uniform(step, seed)
+__device__ __forceinline__ gs::U4 philox_lane(uint32_t c0, const PhiloxU& u, const uint32_t* kv) {
+  const uint64_t m0 = (uint64_t)kPhM0 * c0;          // round 1
+  const uint32_t l2 = (uint32_t)(m0 >> 32) ^ u.x1;
+  const uint32_t l3 = (uint32_t)m0;
+  const uint64_t n1 = (uint64_t)kPhM1 * l2;          // round 2
+  uint32_t a0 = (uint32_t)(n1 >> 32) ^ u.x2;
+  uint32_t a2 = l3 ^ u.x3;
+  uint32_t a1 = (uint32_t)n1;
+  const uint64_t p0 = (uint64_t)kPhM0 * a0;          // round 3
+  const uint64_t p1 = (uint64_t)kPhM1 * a2;
+  a0 = xor3((uint32_t)(p1 >> 32), a1, u.k3);
+  a2 = (uint32_t)(p0 >> 32) ^ u.x4;
+  a1 = (uint32_t)p1;
+  uint32_t a3 = (uint32_t)p0;
+#pragma unroll
+  for (int r = 3; r < 10; ++r) {                     // rounds 4-10: round keys in VGPRs
+    const uint64_t m = (uint64_t)kPhM0 * a0;
+    const uint64_t n = (uint64_t)kPhM1 * a2;
+    const uint32_t b0 = xor3v((uint32_t)(n >> 32), a1, kv[2 * (r - 3)]);
+    const uint32_t b2 = xor3v((uint32_t)(m >> 32), a3, kv[2 * (r - 3) + 1]);
+    a0 = b0; a1 = (uint32_t)n; a2 = b2; a3 = (uint32_t)m;
+  }
+  return gs::U4{a0, a1, a2, a3};
+}
+
+// philox_lane with the step-uniform words held in VGPRs (u: x1, x2, x3, k3, x4), for kernels
+// that keep them live across the whole kernel (the SGPR budget has no room for them there)
+__device__ __forceinline__ gs::U4 philox_lane_v(uint32_t c0, const uint32_t* u, const uint32_t* kv) {
+  const uint64_t m0 = (uint64_t)kPhM0 * c0;          // round 1
+  const uint32_t l2 = (uint32_t)(m0 >> 32) ^ u[0];
+  const uint32_t l3 = (uint32_t)m0;
+  const uint64_t n1 = (uint64_t)kPhM1 * l2;          // round 2
+  uint32_t a0 = (uint32_t)(n1 >> 32) ^ u[1];
+  uint32_t a2 = l3 ^ u[2];
+  uint32_t a1 = (uint32_t)n1;
+  const uint64_t p0 = (uint64_t)kPhM0 * a0;          // round 3
+  const uint64_t p1 = (uint64_t)kPhM1 * a2;
+  a0 = xor3v((uint32_t)(p1 >> 32), a1, u[3]);
+  a2 = (uint32_t)(p0 >> 32) ^ u[4];
+  a1 = (uint32_t)p1;
+  uint32_t a3 = (uint32_t)p0;
+#pragma unroll
+  for (int r = 3; r < 10; ++r) {
+    const uint64_t m = (uint64_t)kPhM0 * a0;
+    const uint64_t n = (uint64_t)kPhM1 * a2;
+    const uint32_t b0 = xor3v((uint32_t)(n >> 32), a1, kv[2 * (r - 3)]);
+    const uint32_t b2 = xor3v((uint32_t)(m >> 32), a3, kv[2 * (r - 3) + 1]);
+    a0 = b0; a1 = (uint32_t)n; a2 = b2; a3 = (uint32_t)m;
+  }
+  return gs::U4{a0, a1, a2, a3};
+}
+
 // Compile-time configuration of one fused-kernel instantiation.
 //   ROWS x WAVES : rows per wave x waves per workgroup (tile height = ROWS*WAVES)
 //   PF           : level-0 prefetch distance in planes (register ring of PF+2 planes)
@@ -258,6 +335,9 @@ struct FCfg {
   // r4_fused_ab.txt).  ABL bit 6 turns it off (A/B), bit 2 forces it on.
   static constexpr bool KV =
       (ABL_ & 4) != 0 || (sizeof(T) == 4 && WPEU == 3 && (ABL_ & 64) == 0);
+  // ABL bit 7 (exact): the step-uniform Philox words of rounds 1-3 (philox_uniform) computed once
+  // per kernel and held in VGPRs, 5 per level, instead of rebuilt on the SALU at every draw
+  static constexpr bool PU = (ABL_ & 128) != 0 && KV && Q32_;
   // pipeline-fill level skip (fused_iter FILL periods): its second copy of the unrolled body
   // costs ~16 VGPRs, free only where the budget is 168 or 256 (WPEU 3 / 2); with 128 it spills
   // or halves the occupancy (4x8:1s: -10 % at L=512, profiles/r2_fill_skip.txt)
@@ -273,6 +353,7 @@ struct FusedState {
   typename C::T ar31;  // dt * noise * 2^-31 held in a VGPR (an SGPR copy spills)
   typename C::V2 kc;   // (dt F, 0) held in VGPRs (the first packed FMA's addend)
   uint32_t kv[C::KV ? 14 : 1];  // Philox round keys of rounds 4-10 (C::KV)
+  uint32_t pu[C::PU ? 5 * C::TL : 1];  // step-uniform Philox words per level (C::PU)
   V2 LD[C::R][C::ROWS];
   V2 OUT[C::NO][C::NS][C::ROWS];
   V2 A[C::TL][C::ROWS];
@@ -457,7 +538,8 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
             const uint32_t Ly4 = (uint32_t)((g.Ly + 3) >> 2);
             const uint32_t gy4 = (uint32_t)(gwrap<C>(sg.gy0 + 4 * m, g.Ly) >> 2);
             const uint32_t qu = (uint32_t)g.Lx * (gy4 + Ly4 * (uint32_t)gz);
-            blk = philox_dev<true, C::KV>(qu + sg.gx32, 0u, tstep, seed, S.kv);
+            if constexpr (C::PU) blk = philox_lane_v(qu + sg.gx32, &S.pu[5 * l], S.kv);
+            else blk = philox_dev<true, C::KV>(qu + sg.gx32, 0u, tstep, seed, S.kv);
           } else {
             const int64_t gyq = gwrap<C>(sg.gy0 + 4 * m, g.Ly);
             const uint64_t Ly4 = ((uint64_t)g.Ly + 3) >> 2;
@@ -585,6 +667,15 @@ __global__ __launch_bounds__(64 * C::WAVES, C::WPEU) void k_fused(const typename
       const uint32_t k1 = (uint32_t)(seed >> 32) + (uint32_t)r * kPhW1;
       asm volatile("v_mov_b32 %0, %1" : "=v"(S.kv[2 * (r - 3)]) : "s"(k0));
       asm volatile("v_mov_b32 %0, %1" : "=v"(S.kv[2 * (r - 3) + 1]) : "s"(k1));
+    }
+  }
+  if constexpr (C::PU) {
+#pragma unroll
+    for (int l = 0; l < TL; ++l) {
+      const PhiloxU u = philox_uniform((uint64_t)(a.t + l), seed);
+      const uint32_t w[5] = {u.x1, u.x2, u.x3, u.k3, u.x4};
+#pragma unroll
+      for (int i = 0; i < 5; ++i) asm volatile("v_mov_b32 %0, %1" : "=v"(S.pu[5 * l + i]) : "s"(w[i]));
     }
   }
   if constexpr (C::NOISE) {
@@ -822,6 +913,7 @@ inline const FusedCfgEntry* fused_cfg_table(int* n) {
       {"4x12:1s-abl32", true, false}, // 36  Philox only on lanes in the x cone (exact)
       {"4x12:2s-abl64", true, false}, // 37  Philox keys rebuilt on the SALU (exact)
       {"4x12:1s-abl64", true, false}, // 38  Philox keys rebuilt on the SALU (exact)
+      {"4x12:1s-abl128", true, false}, // 39  step-uniform Philox words in VGPRs (exact)
 #endif
   };
   *n = (int)(sizeof(t) / sizeof(t[0]));
@@ -933,6 +1025,7 @@ void run_fused_cfg(const void* s, void* d, const FusedArgs& a, const gs::Params&
       case 36: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 32>, T>::run(s, d, a, p, st); return;
       case 37: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 64>, T>::run(s, d, a, p, st); return;
       case 38: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 64>, T>::run(s, d, a, p, st); return;
+      case 39: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 128>, T>::run(s, d, a, p, st); return;
 #endif
       default: break;  // 0 and 14: the default shape below
     }
