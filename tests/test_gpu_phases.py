@@ -57,9 +57,9 @@ def test_periodic_loopback_phases():
     assert {"pack", "transport", "unpack", "fused"} <= set(r["phase_us"])
     assert r["exchange_us"] >= r["phase_us"]["transport"]
     # a 64^3 pass is short (a 14 us fused kernel): the host's RCCL group calls leave the GPU
-    # idle between passes (measured 173 us per pass vs a 135 us device critical path), so only
-    # an upper bound is exact here; the 15 % check is for the 512^3 bench below
-    assert 0.5 <= r["accounted"] <= 1.15, r
+    # idle between passes (173 and 546 us per pass on two boxes vs a ~136 us device critical
+    # path), so only the upper bound holds here; the 15 % check is for the 512^3 bench below
+    assert 0 < r["accounted"] <= 1.15, r
 
 
 def test_bench_two_ranks_reports_phases():
