@@ -300,7 +300,8 @@ __device__ __forceinline__ gs::U4 philox_lane_v(uint32_t c0, const uint32_t* u, 
 //                  (exact) the x-neighbour sums' leading s_nop restored; bit4 (exact) the
 //                  pipeline fill computes every level (no FILL skip); bit5 (exact) Philox only
 //                  on lanes inside the x cone; bit6 (exact) Philox keys rebuilt on the SALU
-//                  (KV off)
+//                  (KV off); bit7 / bit8 (exact) step-uniform Philox words in VGPRs forced
+//                  on / off (PU)
 constexpr int gs_gcd(int a, int b) { return b == 0 ? a : gs_gcd(b, a % b); }
 constexpr int gs_lcm(int a, int b) { return a / gs_gcd(a, b) * b; }
 
@@ -335,9 +336,14 @@ struct FCfg {
   // r4_fused_ab.txt).  ABL bit 6 turns it off (A/B), bit 2 forces it on.
   static constexpr bool KV =
       (ABL_ & 4) != 0 || (sizeof(T) == 4 && WPEU == 3 && (ABL_ & 64) == 0);
-  // ABL bit 7 (exact): the step-uniform Philox words of rounds 1-3 (philox_uniform) computed once
-  // per kernel and held in VGPRs, 5 per level, instead of rebuilt on the SALU at every draw
-  static constexpr bool PU = (ABL_ & 128) != 0 && KV && Q32_;
+  // The step-uniform Philox words of rounds 1-3 (philox_uniform) computed once per kernel and
+  // held in VGPRs, 5 per level, instead of rebuilt on the SALU at every draw (the SALU is
+  // shared by the CU's four SIMDs and was the co-bottleneck of the noise path).  Default on the
+  // single-prefetch KV shapes (4x12:1s: 161 VGPRs at T=3, inside the 168 budget); the 2-deep
+  // prefetch shapes would exceed it.  L=512 T=3 random init: 4x12:1s 726k -> 746k MLUPS
+  // (profiles/r4_fused_ab.txt).  ABL bit 7 forces it on, bit 8 turns it off (both exact).
+  static constexpr bool PU =
+      NOISE_ && KV && Q32_ && ((ABL_ & 128) != 0 || (PF_ == 1 && (ABL_ & 256) == 0));
   // pipeline-fill level skip (fused_iter FILL periods): its second copy of the unrolled body
   // costs ~16 VGPRs, free only where the budget is 168 or 256 (WPEU 3 / 2); with 128 it spills
   // or halves the occupancy (4x8:1s: -10 % at L=512, profiles/r2_fill_skip.txt)
@@ -913,7 +919,7 @@ inline const FusedCfgEntry* fused_cfg_table(int* n) {
       {"4x12:1s-abl32", true, false}, // 36  Philox only on lanes in the x cone (exact)
       {"4x12:2s-abl64", true, false}, // 37  Philox keys rebuilt on the SALU (exact)
       {"4x12:1s-abl64", true, false}, // 38  Philox keys rebuilt on the SALU (exact)
-      {"4x12:1s-abl128", true, false}, // 39  step-uniform Philox words in VGPRs (exact)
+      {"4x12:1s-abl256", true, false}, // 39  step-uniform Philox words on the SALU (exact)
 #endif
   };
   *n = (int)(sizeof(t) / sizeof(t[0]));
@@ -1025,7 +1031,7 @@ void run_fused_cfg(const void* s, void* d, const FusedArgs& a, const gs::Params&
       case 36: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 32>, T>::run(s, d, a, p, st); return;
       case 37: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 64>, T>::run(s, d, a, p, st); return;
       case 38: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 64>, T>::run(s, d, a, p, st); return;
-      case 39: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 128>, T>::run(s, d, a, p, st); return;
+      case 39: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 256>, T>::run(s, d, a, p, st); return;
 #endif
       default: break;  // 0 and 14: the default shape below
     }

@@ -5,5 +5,5 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/${GS_OUT:-r4ab2}
 mkdir -p $O
 cd $R
-GS_HIP_VARIANT=abl timeout -k 10 600 python scripts/tune_inproc.py --L 512 --fuse 3 --init random --warmup 6 --steps 18 --rounds 5 --sched 1 2 --cfg 4x12:1s 4x12:1s-abl128 4x12:2s 4x12:1s-abl64 --out $O/ab512.json > $O/ab512.log 2>&1
+GS_HIP_VARIANT=abl timeout -k 10 600 python scripts/tune_inproc.py --L 512 --fuse 3 --init random --warmup 6 --steps 18 --rounds 5 --sched 1 2 --cfg 4x12:1s 4x12:1s-abl256 4x12:2s 4x12:1s-abl64 --out $O/ab512.json > $O/ab512.log 2>&1
 echo "exit $?"
