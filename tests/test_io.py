@@ -90,6 +90,40 @@ def test_fp64_and_multiple_blocks(tmp_path):
         np.testing.assert_array_equal(r.read("X", 0, (2, 1, 0), (2, 3, 4)), full[2:4, 1:4, :])
 
 
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_block_minmax_vectorised(tmp_path, dtype):
+    """The writer's block min / max characteristics (SSE2 folds, OpenMP chunks above 2M
+    elements) equal numpy's for lengths that do not fill the vector lanes, with NaNs that must
+    not win (the scalar rule `v < a ? v : a`) and a leading NaN that does."""
+    rng = np.random.default_rng(3)
+    cases = []
+    for n in (1, 2, 7, 17, 33, 1000, 65537, (1 << 21) + 5):
+        a = (rng.random(n) * 200 - 100).astype(dtype)
+        if n > 2:
+            a[n // 2] = np.nan
+            a[-1] = -250.0  # the extreme in the scalar tail
+        cases.append(a)
+    lead = (rng.random(40) - 0.5).astype(dtype)
+    lead[0] = np.nan
+    cases.append(lead)
+    p = str(tmp_path / "mm.bp")
+    w = BP4Writer(p, "MinMax", 0, 1)
+    for i, a in enumerate(cases):
+        w.define_variable(f"X{i}", dtype, (a.size,), (0,), (a.size,))
+    w.begin_step()
+    for i, a in enumerate(cases):
+        w.put(f"X{i}", a)
+    w.write_metadata([w.end_step()])
+    w.close()
+    with BP4Reader(p) as r:
+        vs = r.variables(0)
+        for i, a in enumerate(cases[:-1]):
+            b = vs[f"X{i}"].blocks[0]
+            assert b.vmin == np.nanmin(a) and b.vmax == np.nanmax(a), (a.size, b.vmin, b.vmax)
+        b = vs[f"X{len(cases) - 1}"].blocks[0]
+        assert np.isnan(b.vmin) and np.isnan(b.vmax)
+
+
 def _walk_data_file(path):
     """Parse every process group of a data subfile; returns [(step, nvars, [var names])]."""
     with open(path, "rb") as fh:
