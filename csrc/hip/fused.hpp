@@ -301,7 +301,7 @@ __device__ __forceinline__ gs::U4 philox_lane_v(uint32_t c0, const uint32_t* u, 
 //                  pipeline fill computes every level (no FILL skip); bit5 (exact) Philox only
 //                  on lanes inside the x cone; bit6 (exact) Philox keys rebuilt on the SALU
 //                  (KV off); bit7 / bit8 (exact) step-uniform Philox words in VGPRs forced
-//                  on / off (PU)
+//                  on / off (PU); bit9 (exact) Philox blocks drawn before the barrier
 constexpr int gs_gcd(int a, int b) { return b == 0 ? a : gs_gcd(b, a % b); }
 constexpr int gs_lcm(int a, int b) { return a / gs_gcd(a, b) * b; }
 
@@ -348,6 +348,17 @@ struct FCfg {
   // costs ~16 VGPRs, free only where the budget is 168 or 256 (WPEU 3 / 2); with 128 it spills
   // or halves the occupancy (4x8:1s: -10 % at L=512, profiles/r2_fill_skip.txt)
   static constexpr bool FILLSKIP = (WPEU == 3 || WPEU == 2) && !(ABL_ & 16);
+  // ABL bit 9 (exact): every level's Philox block of the iteration drawn before the workgroup
+  // barrier (three independent chains interleaved, overlapping the barrier wait) instead of at
+  // the top of each level's branch (4-row tiles, the PU form)
+  // (bit 10: only the top level's block, the first computed in the skewed order; bits 9 + 10:
+  // the top two levels')
+  static constexpr int HOISTN =
+      !(PU && ROWS_ == 4) ? 0
+      : ((ABL_ & 1536) == 1536) ? (TL_ < 2 ? TL_ : 2)
+      : (ABL_ & 512) ? TL_ : (ABL_ & 1024) ? 1 : 0;
+  static constexpr bool HOIST = HOISTN > 0;
+  static constexpr bool hoisted(int l) { return HOISTN > 0 && l >= TL_ - HOISTN; }
   static constexpr int YSTEP = (RT - 2 * TL) & ~3;        // output rows per tile
   // rows of output level L = l + 1 that some stored output depends on: [l + 1, hi(l)]
   static constexpr int need_hi(int l) { return 2 * TL + YSTEP - 2 - l; }
@@ -479,6 +490,18 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
       S.LD[(IR + C::PF) % C::R][j] = bload(r, sg.voff + j * sg.pitchb, (V2*)nullptr);
     sg.ldp += sg.pzb;
   }
+  gs::U4 pre[TL];  // hoisted blocks (C::HOIST); unused otherwise
+  if constexpr (C::HOIST) {
+    const uint32_t Ly4 = (uint32_t)((g.Ly + 3) >> 2);
+    const uint32_t gy4 = (uint32_t)(gwrap<C>(sg.gy0, g.Ly) >> 2);
+#pragma unroll
+    for (int l = TL - C::HOISTN; l < TL; ++l) {
+      const int q = C::SKEW ? p - (2 * l + 1) : p - l - 1;
+      const int64_t gz = gwrap<C>(g.oz + q, g.Lz);
+      const uint32_t qu = (uint32_t)g.Lx * (gy4 + Ly4 * (uint32_t)gz);
+      pre[l] = philox_lane_v(qu + sg.gx32, &S.pu[5 * l], S.kv);
+    }
+  }
   if constexpr (C::SKEW) {
 #pragma unroll
     for (int l = 0; l < TL; ++l) {
@@ -544,7 +567,8 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
             const uint32_t Ly4 = (uint32_t)((g.Ly + 3) >> 2);
             const uint32_t gy4 = (uint32_t)(gwrap<C>(sg.gy0 + 4 * m, g.Ly) >> 2);
             const uint32_t qu = (uint32_t)g.Lx * (gy4 + Ly4 * (uint32_t)gz);
-            if constexpr (C::PU) blk = philox_lane_v(qu + sg.gx32, &S.pu[5 * l], S.kv);
+            if (C::hoisted(l)) blk = pre[l];
+            else if constexpr (C::PU) blk = philox_lane_v(qu + sg.gx32, &S.pu[5 * l], S.kv);
             else blk = philox_dev<true, C::KV>(qu + sg.gx32, 0u, tstep, seed, S.kv);
           } else {
             const int64_t gyq = gwrap<C>(sg.gy0 + 4 * m, g.Ly);
@@ -920,6 +944,9 @@ inline const FusedCfgEntry* fused_cfg_table(int* n) {
       {"4x12:2s-abl64", true, false}, // 37  Philox keys rebuilt on the SALU (exact)
       {"4x12:1s-abl64", true, false}, // 38  Philox keys rebuilt on the SALU (exact)
       {"4x12:1s-abl256", true, false}, // 39  step-uniform Philox words on the SALU (exact)
+      {"4x12:1s-abl512", true, false}, // 40  Philox blocks of all levels before the barrier (exact)
+      {"4x12:1s-abl1024", true, false}, // 41  the top level's Philox block before the barrier (exact)
+      {"4x12:1s-abl1536", true, false}, // 42  the top two levels' Philox blocks before the barrier
 #endif
   };
   *n = (int)(sizeof(t) / sizeof(t[0]));
@@ -1032,6 +1059,9 @@ void run_fused_cfg(const void* s, void* d, const FusedArgs& a, const gs::Params&
       case 37: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 64>, T>::run(s, d, a, p, st); return;
       case 38: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 64>, T>::run(s, d, a, p, st); return;
       case 39: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 256>, T>::run(s, d, a, p, st); return;
+      case 40: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 512>, T>::run(s, d, a, p, st); return;
+      case 41: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 1024>, T>::run(s, d, a, p, st); return;
+      case 42: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 1536>, T>::run(s, d, a, p, st); return;
 #endif
       default: break;  // 0 and 14: the default shape below
     }
