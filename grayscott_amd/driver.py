@@ -156,6 +156,9 @@ def run(settings: Settings, out=sys.stdout) -> dict:
         if do_ckpt:
             t1 = time.perf_counter()
             with timer.phase("checkpoint"):
+                # output steps before the checkpoint's are committed first (output_queue > 1
+                # keeps several in flight): a restart from it rewrites only its own step
+                stream.commit_through(step - 1)
                 if ckpt is not None:
                     ckpt.start(step, sim, snap)
                 else:

@@ -16,10 +16,14 @@ gathers the per-rank step metadata over the control plane and writes md.0 / md.i
 GPU->host copy uses the compaction kernel (no full-buffer D2H as in the reference, D1/K14).
 
 ``async_output`` (default true): a step is written behind the simulation -- device snapshot and
-D2H on an I/O stream, the data write on a host thread; ``flush`` (called by the next
-``write_step`` and by ``close``) joins it and commits its metadata, so a step is complete in
-the file once the following step starts or the stream is closed.  ``async_output = false``
-writes each step before ``write_step`` returns.
+D2H on an I/O stream, the data write on a host thread.  Up to ``output_queue`` (default 2) steps
+are in flight: ``write_step`` first commits the oldest ones (joins its data write, gathers and
+writes its metadata) until fewer are pending, so step n is complete in the file once step
+n + output_queue starts (or the stream is closed), and the main thread's own per-step work
+(metadata gather, the next snapshot) overlaps the previous step's data write instead of
+following it.  Snapshots above 1 GiB per rank keep one step in flight (the pinned host
+buffers are per queued step; such steps are write-bound).  ``async_output = false`` writes
+each step before ``write_step`` returns.
 
 Restart (``append_after_step``): the output history is kept -- the existing file's steps up to
 the restart step stay, later ones (written after the checkpoint by the failed run) are cut off,
@@ -28,6 +32,7 @@ GrayScott.jl:77-78, implies).
 """
 from __future__ import annotations
 
+import collections
 import os
 import shutil
 from typing import Optional
@@ -131,7 +136,8 @@ class SimulationOutput:
         self.w.define_variable("V", dtype, (Lz, Ly, Lx), (oz, oy, ox), (nz, ny, nx))
         self.steps_written = 0
         self.async_io = bool(getattr(settings, "async_output", True))
-        self._pending = None
+        self.queue = max(1, int(getattr(settings, "output_queue", 2)))
+        self._pending = collections.deque()  # data-write jobs of uncommitted steps, in order
 
     def define_attribute(self, name, value) -> None:
         if self.ctx.rank == 0:
@@ -151,18 +157,21 @@ class SimulationOutput:
     def write_step(self, step: int, sim):
         """IO.jl:82-96.  With ``async_output`` (default) the step is written behind the
         simulation: device snapshot + D2H on an I/O stream, data write on a host thread; the
-        collective metadata gather of step n happens on the main thread at step n+1 (or at
-        close), so no collective ever runs off the main thread.  Returns the snapshot
-        ``(u, v, wait)`` it writes from (None when synchronous), so an asynchronous checkpoint
-        of the same step can share it; the caller must have finished every other reader of
-        the previous snapshot (the host buffers are reused)."""
+        collective metadata gather of step n happens on the main thread when step
+        n + queue is written (or at close), in step order, so no collective ever runs off the
+        main thread.  Returns the snapshot ``(u, v, wait)`` it writes from (None when
+        synchronous), so an asynchronous checkpoint of the same step can share it; the caller
+        must have finished every other reader of that snapshot before the output step that
+        reuses its buffers (``queue`` steps later)."""
         if not self.async_io:
             u, v = sim.get_fields()
             self.write_fields(step, u, v)
             self.last_step = step
             return None
-        self.flush()
-        snap = sim.snapshot_fields("output")
+        depth = self.queue if _snapshot_bytes(sim) <= (1 << 30) else 1
+        while len(self._pending) >= depth:
+            self._commit_oldest()
+        snap = sim.snapshot_fields("output", depth=depth)
         u, v, wait = snap
 
         def job():
@@ -173,26 +182,45 @@ class SimulationOutput:
             self.w.put("V", v)
             return self.w.end_step()
 
-        self._pending = worker("gs-async-output").submit(job)
+        self._pending.append((step, worker("gs-async-output").submit(job)))
         self.last_step = step
         return snap
 
-    def flush(self) -> None:
-        """Finish the in-flight asynchronous step: wait for its data write, gather the
-        per-rank metadata blobs and let rank 0 append them to the index."""
-        job, self._pending = self._pending, None
-        if job is None:
-            return
+    def _commit_oldest(self) -> None:
+        """Finish the oldest in-flight step: wait for its data write, gather the per-rank
+        metadata blobs and let rank 0 append them to the index (rank 0's metadata writes touch
+        md.0 / md.idx only, so they may run while a later step's data write is in flight)."""
+        _, job = self._pending.popleft()
         blob = job.result()
         blobs = self.ctx.gather_object(blob, dst=0)
         if self.ctx.rank == 0:
             self.w.write_metadata(blobs)
         self.steps_written += 1
 
+    def flush(self) -> None:
+        """Commit every in-flight asynchronous step."""
+        while self._pending:
+            self._commit_oldest()
+
+    def commit_through(self, step: int) -> None:
+        """Commit the in-flight steps up to ``step``.  The driver calls it with the step before
+        a checkpoint's: once that checkpoint is committed, every earlier output step is in the
+        file, so a restart from it only has to rewrite the checkpoint step itself."""
+        while self._pending and self._pending[0][0] <= step:
+            self._commit_oldest()
+
     def close(self) -> None:
         self.flush()
         self.w.close()
         self.ctx.barrier()
+
+
+def _snapshot_bytes(sim) -> int:
+    """Bytes of one rank's ghost-free (u, v) snapshot."""
+    n = 1
+    for d in sim.local_shape:
+        n *= int(d)
+    return 2 * n * np.dtype(_NP.get(str(getattr(sim, "dtype", "float32")), np.float32)).itemsize
 
 
 class _Worker:

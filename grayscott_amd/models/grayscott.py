@@ -329,33 +329,42 @@ class GrayScott:
         u, v = self.get_fields_device()
         return u.numpy(), v.numpy()
 
-    def snapshot_fields(self, slot: str = "output"):
+    def snapshot_fields(self, slot: str = "output", depth: int = 1):
         """Asynchronous ghost-stripped copy of u, v for output: the compaction
         kernel runs in stream order on the compute stream, the D2H copy into pinned host
         buffers on a separate I/O stream, so stepping continues while the copy (and the file
         write that follows it) is in flight.  Returns ``(u, v, wait)``: numpy views of the host
         buffers and a callable that blocks until they are filled.
 
-        Each ``slot`` (one per consumer: "output", "checkpoint") has its own device and host
-        buffers, reused by that slot's next call: the consumer must be done with them (its
-        write joined) before snapshotting the same slot again.  The device buffers are not
-        overwritten before the previous D2H copy out of them has finished (the compute stream
-        waits for it), so consumers of different slots never race."""
+        Each ``slot`` (one per consumer: "output", "checkpoint") has one pair of device buffers
+        and a ring of ``depth`` host buffer pairs, used in turn: the consumer must be done with
+        a snapshot (its write joined) before the ``depth``-th next call of the same slot reuses
+        its host buffers (the output stream keeps up to ``depth`` steps in flight).  The device
+        buffers are not overwritten before the previous D2H copy out of them has finished (the
+        compute stream waits for it), so consumers of different slots never race."""
         if self.backend != "hip":
             u, v = self.get_fields()
             return u, v, lambda: None
         tdt = _TORCH_DTYPES[self.dtype]
+        depth = max(1, int(depth))
         if getattr(self, "_snaps", None) is None:
             self._snaps = {}
             self._io_stream = torch.cuda.Stream(self.device)
-        if slot not in self._snaps:
-            dev = [torch.empty(self.local_shape, dtype=tdt, device=self.device) for _ in range(2)]
-            host = [torch.empty(self.local_shape, dtype=tdt, pin_memory=True) for _ in range(2)]
-            self._snaps[slot] = [dev, host, None]
-        dev, host, prev_done = self._snaps[slot]
+        st = self._snaps.get(slot)
+        if st is None or len(st["host"]) != depth:
+            if st is not None and st["done"] is not None:
+                st["done"].synchronize()  # the old ring's last copy has landed
+            st = self._snaps[slot] = {
+                "dev": [torch.empty(self.local_shape, dtype=tdt, device=self.device)
+                        for _ in range(2)],
+                "host": [[torch.empty(self.local_shape, dtype=tdt, pin_memory=True)
+                          for _ in range(2)] for _ in range(depth)],
+                "next": 0, "done": None}
+        dev, host = st["dev"], st["host"][st["next"]]
+        st["next"] = (st["next"] + 1) % depth
         cur = torch.cuda.current_stream(self.device)
-        if prev_done is not None:
-            cur.wait_event(prev_done)  # the previous D2H out of dev[] has finished
+        if st["done"] is not None:
+            cur.wait_event(st["done"])  # the previous D2H out of dev[] has finished
         self.engine.extract(dev[0].data_ptr(), dev[1].data_ptr())
         ready = torch.cuda.Event()
         ready.record(cur)
@@ -365,7 +374,7 @@ class GrayScott:
             host[0].copy_(dev[0], non_blocking=True)
             host[1].copy_(dev[1], non_blocking=True)
             done.record(self._io_stream)
-        self._snaps[slot][2] = done
+        st["done"] = done
         return host[0].numpy(), host[1].numpy(), done.synchronize
 
     def set_fields(self, u, v) -> None:

@@ -205,25 +205,46 @@ def test_vtk_schema_extent():
     assert 'Extent="0 64 0 64 0 64"' in vtk_schema(64)
 
 
-def test_async_output_matches_sync(tmp_path):
-    """async_output (snapshot + background data write, metadata gathered one step later) writes
-    the same steps and bytes as the synchronous path."""
+def _async_output_vs_sync(tmp_path, backend, L, queues):
     from grayscott_amd import driver
 
     out = {}
-    for mode in (False, True):
-        s = Settings(L=20, steps=12, plotgap=3, noise=0.1, F=0.02, k=0.048, dt=1.0, Du=0.2,
-                     Dv=0.1, precision="Float32", backend="CPU", async_output=mode,
-                     output=str(tmp_path / f"gs_{mode}.bp"))
+    for mode in [False] + list(queues):
+        s = Settings(L=L, steps=12, plotgap=3, noise=0.1, F=0.02, k=0.048, dt=1.0, Du=0.2,
+                     Dv=0.1, precision="Float32", backend=backend, async_output=bool(mode),
+                     output_queue=int(mode) or 1, output=str(tmp_path / f"gs_{mode}.bp"))
         driver.run(s, out=open(os.devnull, "w"))
         with BP4Reader(s.output) as r:
             out[mode] = [(int(r.read("step", i)), r.read("U", i), r.read("V", i))
                          for i in range(r.steps)]
-    assert len(out[True]) == len(out[False]) == 4
-    for (sa, ua, va), (sb, ub, vb) in zip(out[False], out[True]):
-        assert sa == sb
-        np.testing.assert_array_equal(ua, ub)
-        np.testing.assert_array_equal(va, vb)
+    for q in queues:
+        assert len(out[q]) == len(out[False]) == 4
+        for (sa, ua, va), (sb, ub, vb) in zip(out[False], out[q]):
+            assert sa == sb
+            np.testing.assert_array_equal(ua, ub)
+            np.testing.assert_array_equal(va, vb)
+
+
+def test_async_output_matches_sync(tmp_path):
+    """async_output (snapshot + background data write, metadata committed when the step
+    `output_queue` steps later is written) writes the same steps and bytes as the synchronous
+    path, for one to three steps in flight."""
+    _async_output_vs_sync(tmp_path, "CPU", 20, (1, 2, 3))
+
+
+@pytest.mark.gpu
+def test_async_output_queue_gpu(tmp_path):
+    """The output queue on the HIP path: a ring of pinned host snapshot buffers behind one
+    device staging pair; every queued step's bytes equal the synchronous writer's."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _async_output_vs_sync(tmp_path, "AMDGPU", 64, (1, 2, 3))
+
+
+def test_output_queue_is_a_setting():
+    from grayscott_amd.utils.config import EXTENSION_KEYS
+    assert Settings().output_queue == 2 and "output_queue" in EXTENSION_KEYS
 
 
 def _async_vs_sync(tmp_path, backend, L, steps, plotgap, freqs):
