@@ -111,18 +111,22 @@ __device__ __forceinline__ PairT<double>::type bload(__amdgpu_buffer_rsrc_t r, i
   return PairT<double>::type{__longlong_as_double(((long long)v.y << 32) | v.x),
                              __longlong_as_double(((long long)v.w << 32) | v.z)};
 }
+// AUX: the store's cache policy (gfx950: 1 sc0, 2 nt, 16 sc1; sc1 = device scope, written
+// through the XCD's L2)
+template <int AUX = 0>
 __device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, int voff, PairT<float>::type c) {
   gs_u2 v;
   v.x = __float_as_uint(c.x);
   v.y = __float_as_uint(c.y);
-  __builtin_amdgcn_raw_buffer_store_b64(v, r, voff, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b64(v, r, voff, 0, AUX);
 }
+template <int AUX = 0>
 __device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, int voff, PairT<double>::type c) {
   const unsigned long long a = (unsigned long long)__double_as_longlong(c.x);
   const unsigned long long b = (unsigned long long)__double_as_longlong(c.y);
   gs_u4 v;
   v.x = (unsigned)a; v.y = (unsigned)(a >> 32); v.z = (unsigned)b; v.w = (unsigned)(b >> 32);
-  __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, 0, AUX);
 }
 
 // a ^ b ^ c in one gfx950 instruction (the compiler does not form v_bitop3 from xor chains)
@@ -301,7 +305,8 @@ __device__ __forceinline__ gs::U4 philox_lane_v(uint32_t c0, const uint32_t* u, 
 //                  pipeline fill computes every level (no FILL skip); bit5 (exact) Philox only
 //                  on lanes inside the x cone; bit6 (exact) Philox keys rebuilt on the SALU
 //                  (KV off); bit7 / bit8 (exact) step-uniform Philox words in VGPRs forced
-//                  on / off (PU); bit9 (exact) Philox blocks drawn before the barrier
+//                  on / off (PU); bit9 (exact) Philox blocks drawn before the barrier; bits 11 /
+//                  12 (exact) nt / sc1 output stores
 constexpr int gs_gcd(int a, int b) { return b == 0 ? a : gs_gcd(b, a % b); }
 constexpr int gs_lcm(int a, int b) { return a / gs_gcd(a, b) * b; }
 
@@ -358,6 +363,9 @@ struct FCfg {
       : ((ABL_ & 1536) == 1536) ? (TL_ < 2 ? TL_ : 2)
       : (ABL_ & 512) ? TL_ : (ABL_ & 1024) ? 1 : 0;
   static constexpr bool HOIST = HOISTN > 0;
+  // ABL bits 11 / 12 (exact): the output stores non-temporal (nt) / device-scope (sc1, written
+  // through L2, so the kernel-end release has no dirty L2 lines to write back)
+  static constexpr int STORE_AUX = ((ABL_ & 2048) ? 2 : 0) | ((ABL_ & 4096) ? 16 : 0);
   static constexpr bool hoisted(int l) { return HOISTN > 0 && l >= TL_ - HOISTN; }
   static constexpr int YSTEP = (RT - 2 * TL) & ~3;        // output rows per tile
   // rows of output level L = l + 1 that some stored output depends on: [l + 1, hi(l)]
@@ -541,7 +549,7 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
       if (!need && l + 1 == TL && !((sg.skip >> l) & 1)) {
         const __amdgpu_buffer_rsrc_t w = plane_rsrc(sg.stp, 0);
 #pragma unroll
-        for (int j = 0; j < ROWS; ++j) bstore(w, (int)0x80000000, in[j]);
+        for (int j = 0; j < ROWS; ++j) bstore<C::STORE_AUX>(w, (int)0x80000000, in[j]);
       }
     }
     if (need && !((sg.skip >> l) & 1)) {  // wave-uniform
@@ -607,7 +615,7 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
 #pragma unroll
         for (int j = 0; j < ROWS; ++j) {
           const int off = (j >= sg.srow0 && j < sg.srow1) ? sg.svoff + j * sg.pitchb : (int)0x80000000;
-          bstore(w, off, res[j]);
+          bstore<C::STORE_AUX>(w, off, res[j]);
         }
       }
     }
@@ -947,6 +955,9 @@ inline const FusedCfgEntry* fused_cfg_table(int* n) {
       {"4x12:1s-abl512", true, false}, // 40  Philox blocks of all levels before the barrier (exact)
       {"4x12:1s-abl1024", true, false}, // 41  the top level's Philox block before the barrier (exact)
       {"4x12:1s-abl1536", true, false}, // 42  the top two levels' Philox blocks before the barrier
+      {"4x12:1s-abl2048", true, false}, // 43  non-temporal output stores (exact)
+      {"4x12:1s-abl4096", true, false}, // 44  device-scope (write-through) output stores (exact)
+      {"4x12:1s-abl6144", true, false}, // 45  both (exact)
 #endif
   };
   *n = (int)(sizeof(t) / sizeof(t[0]));
@@ -1062,6 +1073,9 @@ void run_fused_cfg(const void* s, void* d, const FusedArgs& a, const gs::Params&
       case 40: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 512>, T>::run(s, d, a, p, st); return;
       case 41: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 1024>, T>::run(s, d, a, p, st); return;
       case 42: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 1536>, T>::run(s, d, a, p, st); return;
+      case 43: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 2048>, T>::run(s, d, a, p, st); return;
+      case 44: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 4096>, T>::run(s, d, a, p, st); return;
+      case 45: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 6144>, T>::run(s, d, a, p, st); return;
 #endif
       default: break;  // 0 and 14: the default shape below
     }
