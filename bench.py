@@ -177,6 +177,7 @@ def profile_phases(sim, ctx, passes: int):
     summary = {
         "passes": rows[0]["passes"], "steps_per_pass": rows[0]["depth"],
         "transport": rows[0]["transport"], "overlapped": rows[0]["overlapped"],
+        "chained": rows[0].get("chained", False),
         "pass_us": round(max(r["pass_us"] for r in rows), 2),
         "phase_us": {k: round(max(r["phase_us"].get(k, 0.0) for r in rows), 2) for k in names},
         "exchange_us": round(max(r["exchange_us"] for r in rows), 2),

@@ -50,6 +50,25 @@ def default_fuse(backend: str, domain: CartDomain, dtype: str = "float32") -> in
     return max(1, min(t, nx, ny, nz))
 
 
+
+def critical_path(ph: dict, xch: float, per_pass: dict, chained: bool) -> float:
+    """Critical path of one pass (us) from its median phase times ``ph``, the exchange span
+    ``xch`` and the share of passes each phase ran in (``per_pass``):
+      * chained overlapped passes (engine.h advance_chained): inner_p waits for shell_{p-1},
+        shell_p for exchange_p and inner_{p-1}, so the steady-state period is
+        max(inner, exchange + shell);
+      * one overlapped pass at a time: max(inner, exchange) + shell;
+      * otherwise the phases run in sequence: exchange + fused + step.
+    A phase that runs in some passes only (the boundary refill after a depth change) counts
+    with its share of the passes."""
+    bc = ph.get("bc", 0.0) * min(1.0, per_pass.get("bc", 0.0))
+    if "inner" in ph or "shell" in ph:
+        inner, shell = ph.get("inner", 0.0), ph.get("shell", 0.0)
+        if chained:
+            return max(inner, xch + shell) + bc
+        return max(inner, xch) + shell + bc
+    return xch + ph.get("fused", 0.0) + ph.get("step", 0.0) + bc
+
 class GrayScott:
     """One rank's Gray-Scott state and stepping engine."""
 
@@ -256,8 +275,10 @@ class GrayScott:
         device (csrc/include/gs/phase.h): median microseconds per pass of pack,
         transport, unpack, inner, shell, fused, step and bc, the halo exchange's span and the
         window's time per pass.  Derived: ``critical_us`` -- the pass's critical path from the
-        parts (overlapped: max(inner, exchange) + shell + bc; otherwise their sum; bc weighted
-        by the share of passes that refill the boundary) -- and
+        parts (one overlapped pass: max(inner, exchange) + shell; chained overlapped passes,
+        engine.h advance_chained, whose shell of pass p runs beside the inner part of pass p:
+        the steady-state period max(inner, exchange + shell); otherwise the sum; plus bc
+        weighted by the share of passes that refill the boundary) -- and
         ``accounted`` = critical_us / pass_us; ``bytes_per_neighbour`` and the achieved
         ``link_GBps`` (bytes to the busiest neighbour / the exchange's data time: transport, plus
         the pack for IPC, whose pack kernel stores straight into the peers)."""
@@ -268,24 +289,19 @@ class GrayScott:
             self.engine.advance(int(steps))
         finally:
             r = self.engine.prof_stop()
-        ph = r["phase_us"]
-        xch = r["exchange_us"]
-        # a phase that runs in some passes only (the boundary refill after a depth change)
-        # counts with its share of the passes
-        bc = ph.get("bc", 0.0) * min(1.0, r["per_pass"].get("bc", 0.0))
-        if "inner" in ph or "shell" in ph:
-            crit = max(ph.get("inner", 0.0), xch) + ph.get("shell", 0.0) + bc
-        else:
-            crit = xch + ph.get("fused", 0.0) + ph.get("step", 0.0) + bc
+        chained = passes >= 2 and self.engine.chained(depth)
+        crit = critical_path(r["phase_us"], r["exchange_us"], r["per_pass"], chained)
         r["critical_us"] = crit
         r["accounted"] = crit / r["pass_us"] if r["pass_us"] > 0 else None
         nb = self.halo_bytes()
         r["bytes_per_neighbour"] = {str(k): v for k, v in sorted(nb.items())}
+        ph = r["phase_us"]
         data_us = ph.get("transport", 0.0) + (ph.get("pack", 0.0) if self.transport == "ipc" else 0.0)
         r["link_GBps"] = (float(f"{max(nb.values()) / (data_us * 1e3):.4g}")
                           if nb and data_us > 0 else None)
         r["transport"] = self.transport
         r["overlapped"] = bool(self.overlapped)
+        r["chained"] = bool(chained)
         r["depth"] = depth
         return r
 

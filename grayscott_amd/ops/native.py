@@ -75,6 +75,8 @@ def _declare(lib) -> None:
     lib.gs_set_loopback.restype = c_int
     lib.gs_overlapped.argtypes = [c_void_p, c_int32]
     lib.gs_overlapped.restype = c_int
+    lib.gs_chained.argtypes = [c_void_p, c_int32]
+    lib.gs_chained.restype = c_int
     lib.gs_depth.argtypes = [c_void_p]
     lib.gs_depth.restype = c_int
     lib.gs_set_auto_depth.argtypes = [c_void_p, c_int32]
@@ -267,6 +269,9 @@ class Engine:
 
     def overlapped(self, k: int) -> bool:
         return bool(self.lib.gs_overlapped(self.h, int(k)))
+
+    def chained(self, k: int) -> bool:
+        return bool(self.lib.gs_chained(self.h, int(k)))
 
     def set_auto_depth(self, on: bool):
         self._chk(self.lib.gs_set_auto_depth(self.h, 1 if on else 0), "set_auto_depth")

@@ -114,3 +114,26 @@ def test_driver_perf_log_uses_stream_ordered_compute_timer(tmp_path):
     assert summ["timers"]["compute"]["clock"] == "host"
     assert abs(summ["compute_s"] - sum(r["compute_s"] for r in steps)) < 1e-9
     assert res["steps"] == 12
+
+
+def test_critical_path_models():
+    """The three pass schedules' critical paths (models/grayscott.py critical_path): sequential
+    parts add up; one overlapped pass hides the exchange behind the inner part and then runs the
+    shell; chained passes (engine.h advance_chained) run shell_p beside inner_p, so the period is
+    max(inner, exchange + shell) -- the recurrence c_p = max(c_{p-1}, e_{p-1}) + I,
+    e_p = max(e_{p-1} + X, c_{p-1}) + S, simulated here."""
+    from grayscott_amd.models.grayscott import critical_path
+    seq = {"pack": 5.0, "transport": 20.0, "unpack": 4.0, "fused": 100.0, "bc": 10.0}
+    assert critical_path(seq, 29.0, {"bc": 0.5}, False) == pytest.approx(29 + 100 + 5)
+    ov = {"inner": 80.0, "shell": 25.0}
+    assert critical_path(ov, 50.0, {}, False) == pytest.approx(105.0)
+    assert critical_path(ov, 90.0, {}, False) == pytest.approx(115.0)
+    for inner, xch, shell in ((80.0, 50.0, 25.0), (80.0, 70.0, 25.0), (40.0, 10.0, 5.0)):
+        c = e = 0.0
+        ends = []
+        for _ in range(200):
+            c, e = max(c, e) + inner, max(e + xch, c) + shell
+            ends.append(e)
+        period = (ends[-1] - ends[-101]) / 100
+        assert critical_path({"inner": inner, "shell": shell}, xch, {}, True) == \
+            pytest.approx(period)
