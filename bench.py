@@ -160,6 +160,20 @@ def golden_check(sim, settings, dom, nsteps: int, init_seed):
     return err if err == err else float("inf")
 
 
+def parallelism_label(dims, transport: str, overlapped: bool) -> str:
+    """``spatial-z-slabs 1x1x8 (ipc plane halos, overlapped)``, ``spatial-3d 2x2x2 (rccl packed
+    halos)``, ``spatial-3d 1x1x1``: the process grid, and with neighbours the halo transport
+    (z slabs exchange contiguous ghost planes in place, other grids packed faces / edges /
+    corners) and whether the exchange overlaps the inner update."""
+    dstr = "x".join(str(int(d)) for d in dims)
+    if all(int(d) == 1 for d in dims):
+        return f"spatial-3d {dstr}"
+    zslab = int(dims[0]) == 1 and int(dims[1]) == 1
+    kind = "plane" if zslab else "packed"
+    tail = ", overlapped" if overlapped else ""
+    return f"spatial-{'z-slabs' if zslab else '3d'} {dstr} ({transport} {kind} halos{tail})"
+
+
 def profile_phases(sim, ctx, passes: int):
     """Per-phase device timing of ``passes`` passes of this data path, run after
     the timed region (csrc/include/gs/phase.h: hipEvents in stream order on the compute and
@@ -328,7 +342,6 @@ def run(args) -> int:
     cells = float(args.L) ** 3
     mlups = cells * args.steps / elapsed / 1e6
     if ctx.rank == 0:
-        dstr = "x".join(str(d) for d in dom.dims)
         ref_grid = None
         if tuning:
             bal = dims_create(ctx.world_size)
@@ -360,8 +373,7 @@ def run(args) -> int:
                 "L": args.L,
                 "global_batch": 1,
                 "seq_len": args.L,
-                "parallelism": (f"spatial-z-slabs {dstr} ({sim.transport} plane halos, overlapped)"
-                                if sim.overlapped else f"spatial-3d {dstr}"),
+                "parallelism": parallelism_label(dom.dims, sim.transport, sim.overlapped),
                 "dims": dom.dims,
                 "local_extent": dom.proc_sizes,
                 "fuse_steps": sim.depth, "ghost_width": sim.H,

@@ -110,3 +110,15 @@ def test_spawn_local_fail_fast(tmp_path):
     rc = spawn_local(2, [sys.executable, "-c", prog], grace=2.0)
     assert rc == 3
     assert time.monotonic() - t0 < 60
+
+
+def test_parallelism_label():
+    """The JSON line's config.parallelism names the grid, and with neighbours the halo kind
+    (in-place planes for z slabs, packed otherwise), the transport and the overlap."""
+    import bench
+    assert bench.parallelism_label([1, 1, 1], "none", False) == "spatial-3d 1x1x1"
+    assert bench.parallelism_label([1, 1, 8], "ipc", True) == \
+        "spatial-z-slabs 1x1x8 (ipc plane halos, overlapped)"
+    assert bench.parallelism_label([2, 2, 2], "rccl", False) == "spatial-3d 2x2x2 (rccl packed halos)"
+    assert bench.parallelism_label([2, 2, 1], "ipc", True) == \
+        "spatial-3d 2x2x1 (ipc packed halos, overlapped)"
