@@ -136,7 +136,7 @@ class SimulationOutput:
         self.w.define_variable("V", dtype, (Lz, Ly, Lx), (oz, oy, ox), (nz, ny, nx))
         self.steps_written = 0
         self.async_io = bool(getattr(settings, "async_output", True))
-        self.queue = max(1, int(getattr(settings, "output_queue", 2)))
+        self.queue = min(4, max(1, int(getattr(settings, "output_queue", 2))))  # 1..4
         self._pending = collections.deque()  # data-write jobs of uncommitted steps, in order
 
     def define_attribute(self, name, value) -> None:

@@ -19,8 +19,8 @@ Extension keys (not in the reference, all optional, documented in README):
   "tune": self-check and time the candidate grids / fuse depths, parallel/autotune.py),
   ``overlap`` ("auto"|"on"|"off": overlap the halo exchange with the inner-plane update),
   ``async_output`` (bool, default true: output steps are written behind the simulation),
-  ``output_queue`` (int, default 2: output steps in flight behind the simulation -- snapshot
-  buffers per rank; 1 when one step's snapshot exceeds 1 GiB),
+  ``output_queue`` (int 1-4, default 2: output steps in flight behind the simulation --
+  snapshot buffers per rank; 1 when one step's snapshot exceeds 1 GiB),
   ``async_checkpoint`` (bool, default true: checkpoint data is written behind the simulation and
   committed -- metadata, atomic rename -- at the next output/checkpoint event or at the end).
 """
