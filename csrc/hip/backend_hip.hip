@@ -814,6 +814,11 @@ class HipBackend final : public gs::Backend {
     }
     const auto t0 = std::chrono::steady_clock::now();
     int sleep_us = 20;
+    // Timed regions end in this wait, so its detection latency adds to every measured window:
+    // the first kSpinS seconds poll back to back (a yield between queries: ~1-2 us latency);
+    // only a longer wait backs off to sleeps of up to 160 us (previously from the first poll,
+    // which could report a 1 ms multi-rank window up to ~0.2 ms late).
+    constexpr double kSpinS = 0.05;
     for (;;) {
       const hipError_t a = hipStreamQuery(stream_);
       const hipError_t b = hipStreamQuery(comm_stream_);
@@ -836,8 +841,12 @@ class HipBackend final : public gs::Backend {
         throw std::runtime_error("halo exchange watchdog: device work not finished after " +
                                  std::to_string(timeout_s) + " s (GS_COMM_TIMEOUT)");
       }
+      if (el < kSpinS) {
+        std::this_thread::yield();
+        continue;
+      }
       std::this_thread::sleep_for(std::chrono::microseconds(sleep_us));
-      if (sleep_us < 100) sleep_us *= 2;  // bounded latency: timed regions end in this wait
+      if (sleep_us < 100) sleep_us *= 2;
     }
   }
 
