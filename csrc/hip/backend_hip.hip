@@ -452,7 +452,7 @@ class HipBackend final : public gs::Backend {
       for (int i = 0; i < nt; ++i)
         if ((sizeof(T) == 4 ? tab[i].f32 : tab[i].f64) && i != dflt && !strstr(tab[i].name, "-abl") &&
             (blk_ok || !gsk::fused_cfg_is_block(i)) &&
-            gsk::block_cfg_fits(i, n, (int)sizeof(V2)))
+            gsk::block_cfg_fits(i, n, (int)sizeof(V2)) && gsk::fused_cfg_applies(i, g_, n))
           cfgs.push_back(i);
     }
     const int nsched = pt.zlen1 > 0 ? 1 : 3;  // two z-runs always use schedule 0

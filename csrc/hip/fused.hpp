@@ -61,6 +61,10 @@ struct FusedArgs {
   // the small-grid block kernel may serve this launch (Backend::fused(), and the autotuner's
   // timing of it): its level-0 x ghosts are then the engine's ensure_bc values (block.hpp)
   int32_t allow_block;
+  // folded x strip (FCfg::FOLD): tiles [0, ntxf * nty) are the full 64-column tiles; the last
+  // strip's narrow tiles (<= 32 - 2T outputs wide) run two per wave as nfold = ceil(nty / 2)
+  // units -- lanes 0-31 y-tile 2f, lanes 32-63 y-tile 2f + 1 (idle past the last one)
+  int32_t ntxf, nfold;
 };
 
 template <typename T> struct PairT;
@@ -311,13 +315,18 @@ constexpr int gs_gcd(int a, int b) { return b == 0 ? a : gs_gcd(b, a % b); }
 constexpr int gs_lcm(int a, int b) { return a / gs_gcd(a, b) * b; }
 
 template <typename T_, int TL_, int ROWS_, int WAVES_, int PF_, bool PERIODIC_, bool NOISE_,
-          bool SKEW_ = false, bool Q32_ = true, int ABL_ = 0>
+          bool SKEW_ = false, bool Q32_ = true, int ABL_ = 0, bool FOLD_ = false>
 struct FCfg {
   using T = T_;
   using V2 = typename PairT<T>::type;
   static constexpr int TL = TL_, ROWS = ROWS_, WAVES = WAVES_, PF = PF_;
   static constexpr bool PERIODIC = PERIODIC_, NOISE = NOISE_, SKEW = SKEW_, Q32 = Q32_;
   static constexpr int ABL = ABL_;
+  // the last x strip folded into half-wave tiles (FusedArgs::ntxf ..): non-periodic, 32-bit
+  // noise counter (its lane part absorbs the upper half's y offset)
+  static constexpr bool FOLD = FOLD_;
+  static_assert(!FOLD_ || (Q32_ && !PERIODIC_ && ROWS_ == 4),
+                "folded strips need Q32, a non-periodic grid and 4-row waves");
   static constexpr int R = PF + 2;                    // level-0 ring slots
   // level-l output ring / xch buffers: 2 slots.  Skewed: level l+1 reads level l's outputs of
   // the two previous iterations (input and centre), and the levels run top-down within an
@@ -391,11 +400,13 @@ struct FusedSeg {
   int skip;                  // bit l: this wave's rows are outside level l+1's cone
   int voff, svoff, pitchb;
   int srow0, srow1;
+  int soff[4];               // FOLD: per-lane store offset of each row (out of range: masked)
   int pzb;                   // bytes per storage plane
   const char* ldp;           // source plane of the next prefetch (p + PF)
   char* stp;                 // destination plane of this iteration's last-level output
   int64_t gx, gxu, gy0;
   uint32_t gx32;             // Q32 noise counter: lane part
+  int gdy;                   // folded tile: this lane's y offset from gy0 (0 or ystep)
   bool edge;
 };
 
@@ -603,7 +614,7 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
           const bool xout = sg.gxu < 0 || sg.gxu >= g.Lx;
 #pragma unroll
           for (int j = 0; j < ROWS; ++j) {
-            const int64_t gyj = sg.gy0 + j;
+            const int64_t gyj = sg.gy0 + j + (C::FOLD ? sg.gdy : 0);
             if (zout || xout || gyj < 0 || gyj >= g.Ly) res[j] = V2{bu, (T)0};
           }
         }
@@ -614,7 +625,9 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
         const __amdgpu_buffer_rsrc_t w = plane_rsrc(sg.stp, q >= sg.z0 ? sg.pzb : 0);
 #pragma unroll
         for (int j = 0; j < ROWS; ++j) {
-          const int off = (j >= sg.srow0 && j < sg.srow1) ? sg.svoff + j * sg.pitchb : (int)0x80000000;
+          int off;
+          if constexpr (C::FOLD) off = sg.soff[j];  // per lane (a folded pair's halves differ)
+          else off = (j >= sg.srow0 && j < sg.srow1) ? sg.svoff + j * sg.pitchb : (int)0x80000000;
           bstore<C::STORE_AUX>(w, off, res[j]);
         }
       }
@@ -746,26 +759,54 @@ __global__ __launch_bounds__(64 * C::WAVES, C::WPEU) void k_fused(const typename
       const int z0 = a.zlo[run] + (zv - rv0);
       const int z1 = z0 + (zv1 - zv);
       u += zv1 - zv;
-      const int tx = tile % a.ntx, ty = tile / a.ntx;
+      int tx, ty, xw = 64, dy = 0;  // x width of the tile in lanes; this lane's y offset
+      bool live = true;             // false: the idle upper half of an unpaired folded tile
+      if (C::FOLD && tile >= a.ntxf * a.nty) {
+        // folded strip unit: lanes 0-31 y-tile ty, lanes 32-63 y-tile ty + 1 (pairs only)
+        const int f = tile - a.ntxf * a.nty;
+        tx = a.ntxf;
+        ty = 2 * f;
+        xw = 32;
+        if (sg.lane >= 32) {
+          if (ty + 1 < a.nty) dy = a.ystep;
+          else live = false;
+        }
+      } else {
+        const int ntxe = C::FOLD ? a.ntxf : a.ntx;  // full tiles per row of tiles
+        tx = tile % ntxe;
+        ty = tile / ntxe;
+      }
       const int X0 = tx * a.xstep - TL;
       const int Y0 = a.ybase + ty * a.ystep - TL;
-      const int x = X0 + sg.lane;
+      const int x = X0 + (C::FOLD ? (sg.lane & (xw - 1)) : sg.lane);
       const int ylo = Y0 + sg.wave * ROWS;
-      // lane byte offset inside a plane (row ylo); negative values are out of range
-      sg.voff = ((ylo + g.H) * g.px + x + g.xo) * (int)sizeof(typename C::V2);
+      // lane byte offset inside a plane (row ylo + dy); negative values are out of range
+      sg.voff = ((ylo + dy + g.H) * g.px + x + g.xo) * (int)sizeof(typename C::V2);
       sg.gxu = g.ox + x;
       sg.gx = gwrap<C>(sg.gxu, g.Lx);
       sg.gy0 = g.oy + ylo;
-      sg.gx32 = (uint32_t)sg.gx;
-      const int ox1 = min(X0 + TL + a.xstep, a.mx1);
+      sg.gdy = dy;
+      // Q32 counter gx + Lx * (gy/4 + Ly4 * gz): the upper half's dy (a multiple of 4) joins the
+      // lane part
+      sg.gx32 = (uint32_t)sg.gx + (uint32_t)g.Lx * (uint32_t)(dy >> 2);
+      const int ox1 = min(X0 + TL + (xw == 64 ? a.xstep : 32 - 2 * TL), a.mx1);
       const int oy0 = max(Y0 + TL, a.my0), oy1 = min(Y0 + TL + a.ystep, a.my1);
-      const bool xin = x >= max(X0 + TL, a.mx0) && x < ox1;
+      const bool xin = live && x >= max(X0 + TL, a.mx0) && x < ox1;
       sg.svoff = xin ? sg.voff : (int)0x80000000;  // masked lanes store out of range
       sg.srow0 = max(oy0 - ylo, 0);
       sg.srow1 = min(oy1 - ylo, ROWS);
+      if constexpr (C::FOLD) {
+        // the lane's own y-tile (Y0 + dy): its store rows, folded into per-row offsets once
+        const int oy0l = max(Y0 + dy + TL, a.my0), oy1l = min(Y0 + dy + TL + a.ystep, a.my1);
+        const int r0 = max(oy0l - ylo - dy, 0), r1 = min(oy1l - ylo - dy, ROWS);
+#pragma unroll
+        for (int j = 0; j < ROWS; ++j)
+          sg.soff[j] = (xin && j >= r0 && j < r1) ? sg.voff + j * sg.pitchb : (int)0x80000000;
+      }
+      const int yext = WAVES * ROWS + (xw == 32 ? a.ystep : 0);
       sg.edge = a.bcfix &&
-          (g.ox + X0 < 0 || g.ox + X0 + 64 > g.Lx || g.oy + Y0 < 0 ||
-           g.oy + Y0 + WAVES * ROWS > g.Ly || g.oz + z0 - TL < 0 || g.oz + z1 + TL > g.Lz);
+          (g.ox + X0 < 0 || g.ox + X0 + xw > g.Lx || g.oy + Y0 < 0 ||
+           g.oy + Y0 + yext > g.Ly || g.oz + z0 - TL < 0 || g.oz + z1 + TL > g.Lz);
       sg.z0 = z0;
 #pragma unroll
       for (int l = 0; l < TL; ++l)
@@ -806,6 +847,19 @@ __global__ __launch_bounds__(64 * C::WAVES, C::WPEU) void k_fused(const typename
 // ------------------------------------------------------------------------------------------
 inline int& fused_sched_slot();
 
+// Folded last x strip (FCfg::FOLD): when the last x strip of tiles holds <= 32 - 2T outputs,
+// its y-tiles run two per wave (lanes 0-31 tile 2f, lanes 32-63 tile 2f + 1) and the strip
+// costs half its tiles.  L=256 T=3: 5 x 7 = 35 tiles -> 4 x 7 + 4 = 32 units (one more z-chunk
+// per tile fits the 256 workgroup slots); L=128: 3 x 4 -> 2 x 4 + 2.
+template <class C>
+inline void fold_strip(FusedArgs& a) {
+  const int rem = a.g.nx - (a.ntx - 1) * a.xstep;  // outputs of the last strip (1..xstep)
+  if (a.ntx < 2 || rem > 32 - 2 * C::TL) return;
+  a.ntxf = a.ntx - 1;
+  a.nfold = (a.nty + 1) / 2;
+  a.ntiles = a.ntxf * a.nty + a.nfold;
+}
+
 template <class C, typename T>
 struct FusedLaunch {
   static int occupancy() {
@@ -828,6 +882,9 @@ struct FusedLaunch {
     a.ntx = (a.g.nx + a.xstep - 1) / a.xstep;
     a.nty = (a.g.ny - a.ybase + a.ystep - 1) / a.ystep;
     a.ntiles = a.ntx * a.nty;
+    a.ntxf = a.ntx;
+    a.nfold = 0;
+    if constexpr (C::FOLD) fold_strip<C>(a);
     a.units = (int64_t)a.ntiles * a.nzv;
     static int cus = 0;
     if (!cus) {
@@ -938,30 +995,42 @@ inline const FusedCfgEntry* fused_cfg_table(int* n) {
       {"blk8x4w16", true, false},  // 24  (T=2 only: T=3 levels do not fit the LDS)
       {"blk8x2w16l", true, false}, // 25  last level in half-quad items
       {"blk4x4w16l", true, false}, // 26  last level in half-quad items
+      {"4x12:1sf", true, false},   // 27  the last x strip folded into half-wave tiles (FCfg::FOLD)
 #ifdef GS_ABLATION
-      {"4x12:2s-abl1", true, false},  // 27  no barriers
-      {"4x12:2s-abl2", true, false},  // 28  L2-resident loads
-      {"4x12:1s-abl4", true, false},  // 29  Philox keys in VGPRs (exact)
-      {"4x12:2s-abl4", true, false},  // 30  Philox keys in VGPRs (exact)
-      {"4x12:1s-abl8", true, false},  // 31  DPP sums with the s_nop (exact)
-      {"4x12:1s-abl12", true, false}, // 32  abl4 + abl8 (exact)
-      {"4x12:1s-abl16", true, false}, // 33  pipeline fill computes every level (exact)
-      {"4x8:1s-abl16", true, true},   // 34  pipeline fill computes every level (exact)
-      {"4x6:2s-abl16", true, true},   // 35  pipeline fill computes every level (exact)
-      {"4x12:1s-abl32", true, false}, // 36  Philox only on lanes in the x cone (exact)
-      {"4x12:2s-abl64", true, false}, // 37  Philox keys rebuilt on the SALU (exact)
-      {"4x12:1s-abl64", true, false}, // 38  Philox keys rebuilt on the SALU (exact)
-      {"4x12:1s-abl256", true, false}, // 39  step-uniform Philox words on the SALU (exact)
-      {"4x12:1s-abl512", true, false}, // 40  Philox blocks of all levels before the barrier (exact)
-      {"4x12:1s-abl1024", true, false}, // 41  the top level's Philox block before the barrier (exact)
-      {"4x12:1s-abl1536", true, false}, // 42  the top two levels' Philox blocks before the barrier
-      {"4x12:1s-abl2048", true, false}, // 43  non-temporal output stores (exact)
-      {"4x12:1s-abl4096", true, false}, // 44  device-scope (write-through) output stores (exact)
-      {"4x12:1s-abl6144", true, false}, // 45  both (exact)
+      {"4x12:2s-abl1", true, false},  // 28  no barriers
+      {"4x12:2s-abl2", true, false},  // 29  L2-resident loads
+      {"4x12:1s-abl4", true, false},  // 30  Philox keys in VGPRs (exact)
+      {"4x12:2s-abl4", true, false},  // 31  Philox keys in VGPRs (exact)
+      {"4x12:1s-abl8", true, false},  // 32  DPP sums with the s_nop (exact)
+      {"4x12:1s-abl12", true, false}, // 33  abl4 + abl8 (exact)
+      {"4x12:1s-abl16", true, false}, // 34  pipeline fill computes every level (exact)
+      {"4x8:1s-abl16", true, true},   // 35  pipeline fill computes every level (exact)
+      {"4x6:2s-abl16", true, true},   // 36  pipeline fill computes every level (exact)
+      {"4x12:1s-abl32", true, false}, // 37  Philox only on lanes in the x cone (exact)
+      {"4x12:2s-abl64", true, false}, // 38  Philox keys rebuilt on the SALU (exact)
+      {"4x12:1s-abl64", true, false}, // 39  Philox keys rebuilt on the SALU (exact)
+      {"4x12:1s-abl256", true, false}, // 40  step-uniform Philox words on the SALU (exact)
+      {"4x12:1s-abl512", true, false}, // 41  Philox blocks of all levels before the barrier (exact)
+      {"4x12:1s-abl1024", true, false}, // 42  the top level's Philox block before the barrier (exact)
+      {"4x12:1s-abl1536", true, false}, // 43  the top two levels' Philox blocks before the barrier
+      {"4x12:1s-abl2048", true, false}, // 44  non-temporal output stores (exact)
+      {"4x12:1s-abl4096", true, false}, // 45  device-scope (write-through) output stores (exact)
+      {"4x12:1s-abl6144", true, false}, // 46  both (exact)
 #endif
   };
   *n = (int)(sizeof(t) / sizeof(t[0]));
   return t;
+}
+
+// whether a config is worth timing for a launch of k steps over g: the folded-strip tile
+// (FCfg::FOLD) equals 4x12:1s unless the last x strip fits half a wave
+inline bool fused_cfg_applies(int i, const Geom& g, int k) {
+  int n = 0;
+  const FusedCfgEntry* t = fused_cfg_table(&n);
+  if (i < 0 || i >= n || strcmp(t[i].name, "4x12:1sf") != 0) return true;
+  const int xstep = 64 - 2 * k;
+  const int ntx = (g.nx + xstep - 1) / xstep;
+  return ntx >= 2 && g.nx - (ntx - 1) * xstep <= 32 - 2 * k;
 }
 
 inline bool fused_cfg_is_block(int i) {
@@ -1025,8 +1094,8 @@ void run_fused_cfg(const void* s, void* d, const FusedArgs& a, const gs::Params&
       case 16: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
       case 17: FusedLaunch<FCfg<T, TL, 4, 4, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
 #ifdef GS_ABLATION
-      case 34: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
-      case 35: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 35: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 36: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
 #endif
       default: break;
     }
@@ -1056,26 +1125,27 @@ void run_fused_cfg(const void* s, void* d, const FusedArgs& a, const gs::Params&
       case 24: if (block_supported(a) && run_block<BCfg<T, TL, 8, 4, 16, NZ>>(s, d, a, p, st)) return; break;
       case 25: if (block_supported(a) && run_block<BCfg<T, TL, 8, 2, 16, NZ, true, true>>(s, d, a, p, st)) return; break;
       case 26: if (block_supported(a) && run_block<BCfg<T, TL, 4, 4, 16, NZ, true, true>>(s, d, a, p, st)) return; break;
+      case 27: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 0, true>, T>::run(s, d, a, p, st); return;
 #ifdef GS_ABLATION
-      case 27: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 1>, T>::run(s, d, a, p, st); return;
-      case 28: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 2>, T>::run(s, d, a, p, st); return;
-      case 29: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;
-      case 30: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;
-      case 31: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 8>, T>::run(s, d, a, p, st); return;
-      case 32: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 12>, T>::run(s, d, a, p, st); return;
-      case 33: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
-      case 34: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
-      case 35: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
-      case 36: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 32>, T>::run(s, d, a, p, st); return;
-      case 37: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 64>, T>::run(s, d, a, p, st); return;
-      case 38: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 64>, T>::run(s, d, a, p, st); return;
-      case 39: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 256>, T>::run(s, d, a, p, st); return;
-      case 40: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 512>, T>::run(s, d, a, p, st); return;
-      case 41: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 1024>, T>::run(s, d, a, p, st); return;
-      case 42: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 1536>, T>::run(s, d, a, p, st); return;
-      case 43: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 2048>, T>::run(s, d, a, p, st); return;
-      case 44: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 4096>, T>::run(s, d, a, p, st); return;
-      case 45: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 6144>, T>::run(s, d, a, p, st); return;
+      case 28: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 1>, T>::run(s, d, a, p, st); return;
+      case 29: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 2>, T>::run(s, d, a, p, st); return;
+      case 30: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;
+      case 31: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;
+      case 32: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 8>, T>::run(s, d, a, p, st); return;
+      case 33: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 12>, T>::run(s, d, a, p, st); return;
+      case 34: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 35: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 36: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 37: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 32>, T>::run(s, d, a, p, st); return;
+      case 38: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 64>, T>::run(s, d, a, p, st); return;
+      case 39: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 64>, T>::run(s, d, a, p, st); return;
+      case 40: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 256>, T>::run(s, d, a, p, st); return;
+      case 41: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 512>, T>::run(s, d, a, p, st); return;
+      case 42: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 1024>, T>::run(s, d, a, p, st); return;
+      case 43: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 1536>, T>::run(s, d, a, p, st); return;
+      case 44: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 2048>, T>::run(s, d, a, p, st); return;
+      case 45: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 4096>, T>::run(s, d, a, p, st); return;
+      case 46: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 6144>, T>::run(s, d, a, p, st); return;
 #endif
       default: break;  // 0 and 14: the default shape below
     }

@@ -76,6 +76,24 @@ def test_headline_pinned_tiles_match_golden(cfg, sched, L):
     assert err < 2e-5, (err, choice)
 
 
+@pytest.mark.parametrize("L,fuse,sched", [(256, 3, 1), (256, 3, 2), (128, 3, 2), (128, 2, 1),
+                                           (192, 3, 0)])
+def test_folded_strip_matches_golden_and_plain_tile(L, fuse, sched):
+    """4x12:1sf (fused.hpp FCfg::FOLD): the last x strip's narrow tiles run two per wave (lanes
+    0-31 one y-tile, 32-63 the next).  Against the golden model, and bit for bit against the
+    same tile without folding (every tile choice computes the same bits).  The last strip
+    holds 24 outputs at L=256 T=3, 12 at L=128 T=3, 8 at L=128 T=2 and 18 at L=192 T=3 (<= 32 - 2T:
+    all fold); schedules 0, 1 and 2."""
+    env = {"GS_FUSED_CFG": "4x12:1sf", "GS_FUSED_SCHED": str(sched)}
+    err, choice = _run(L, "Float32", fuse, 2 * fuse, env=env)
+    assert err < 2e-5, (err, choice)
+    err2, choice2 = _run(L, "Float32", fuse, 2 * fuse,
+                         env={"GS_FUSED_CFG": "4x12:1s", "GS_FUSED_SCHED": str(sched)})
+    d1 = [w for w in choice.split() if len(w) == 40][0]
+    d2 = [w for w in choice2.split() if len(w) == 40][0]
+    assert d1 == d2, (choice, choice2)
+
+
 def test_headline_fp64_t2_matches_golden():
     """fp64 at T=2 (its default depth), L=256, autotuned tile."""
     err, choice = _run(256, "Float64", 2, 6)
