@@ -9,11 +9,13 @@ i.e. the
 VALU issue time per pass up to a constant -- fused.hpp FusedLaunch::run's own chunk choice.
 
   python scripts/tile_model.py --n 512 512 512 --T 3
+
+The folded last strip (4x12f, fused.hpp FCfg::FOLD) is listed where it applies (e.g. L=256).
 """
 import argparse
 
 
-def model(nx, ny, nz, T, rows, waves, wg_per_cu, cus=256, oy=0):
+def model(nx, ny, nz, T, rows, waves, wg_per_cu, cus=256, oy=0, fold=False):
     rt = rows * waves
     ystep = (rt - 2 * T) & ~3
     xstep = 64 - 2 * T
@@ -21,6 +23,11 @@ def model(nx, ny, nz, T, rows, waves, wg_per_cu, cus=256, oy=0):
     ntx = -(-nx // xstep)
     nty = (ny - ybase + ystep - 1) // ystep
     ntiles = ntx * nty
+    # folded last x strip (fused.hpp FCfg::FOLD): its tiles run two per wave when the strip
+    # holds <= 32 - 2T outputs
+    folded = fold and ntx >= 2 and nx - (ntx - 1) * xstep <= 32 - 2 * T
+    if folded:
+        ntiles = (ntx - 1) * nty + (nty + 1) // 2
     # rows computed per level l (waves whose rows touch [l+1, need_hi(l)]): k_fused's skip rule
     comp = 0
     for l in range(T):
@@ -29,7 +36,7 @@ def model(nx, ny, nz, T, rows, waves, wg_per_cu, cus=256, oy=0):
     useful_rows = T * ystep
     y_yield = useful_rows / comp
     x_yield = xstep / 64
-    cover = (nx * ny) / (ntx * xstep * nty * ystep)
+    cover = (nx * ny) / (((ntx - 1) * xstep + (xstep / 2 if folded else xstep)) * nty * ystep)
     per_useful = 1 / (x_yield * y_yield * cover)
     slots = wg_per_cu * cus
     M = max(1, slots // 8)
@@ -43,7 +50,8 @@ def model(nx, ny, nz, T, rows, waves, wg_per_cu, cus=256, oy=0):
     cost, nch, rounds = best
     # VALU time per pass ~ makespan x cells a CU computes per pipeline iteration (VALU-bound CU)
     t = cost * rt * wg_per_cu
-    return dict(tile=f"{rows}x{waves}", wg_per_cu=wg_per_cu, ntiles=ntiles, ystep=ystep,
+    return dict(tile=f"{rows}x{waves}" + ("f" if folded else ""), wg_per_cu=wg_per_cu,
+                ntiles=ntiles, ystep=ystep,
                 x_yield=round(x_yield, 3), y_yield=round(y_yield, 3), cover=round(cover, 3),
                 levels_per_useful=round(per_useful, 3), nch=nch, rounds=rounds,
                 busy_cus=round(min(1.0, ntiles * nch / (rounds * slots)), 3), makespan=cost,
@@ -58,6 +66,9 @@ def main():
     # (rows, waves, workgroups per CU as the register / LDS budget allows, fp32)
     shapes = [(4, 8, 2), (4, 12, 1), (4, 16, 1), (8, 4, 2), (4, 6, 2)]
     rows = [model(*a.n, a.T, r, w, k) for r, w, k in shapes]
+    f = model(*a.n, a.T, 4, 12, 1, fold=True)
+    if f["tile"].endswith("f"):
+        rows.append(f)
     base = next(r["time_units"] for r in rows if r["tile"] == "4x12")
     for r in rows:
         r["rel_time"] = round(r["time_units"] / base, 3)
