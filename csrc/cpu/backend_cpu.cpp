@@ -3,6 +3,9 @@
 // solver (reference: Simulation_CPU.jl:14-133, Threads.@threads over z) and the golden
 // model the gfx950 kernels are tested against.  Same Philox noise stream as the GPU.
 #include <emmintrin.h>
+#if defined(__x86_64__)
+#include <immintrin.h>
+#endif
 #include <omp.h>
 #include <string.h>
 
@@ -15,6 +18,80 @@ namespace {
 
 using gs::Box;
 using gs::Geom;
+
+// Philox4x32-10 blocks of counters (q_i, q_i >> 32, step, step >> 32), key `seed`, for a row of
+// cells (the noise cache of CpuBackend::step).  The AVX2 form runs eight counters per vector:
+// _mm256_mul_epu32 gives the 32x32 -> 64-bit products of the even 32-bit lanes, the odd lanes
+// go through a 64-bit shift, and blends reassemble the products' low / high words.  Integer
+// arithmetic only, so it equals gs::philox4x32_10 bit for bit (tests/test_noise.py checks);
+// chosen at run time when the CPU has AVX2 (the library is built for baseline x86-64).
+void noise_blocks_scalar(const uint64_t* q, int n, uint64_t step, uint64_t seed, gs::U4* out) {
+  for (int i = 0; i < n; ++i)
+    out[i] = gs::philox4x32_10((uint32_t)q[i], (uint32_t)(q[i] >> 32), (uint32_t)step,
+                               (uint32_t)(step >> 32), seed);
+}
+
+#if defined(__x86_64__)
+__attribute__((target("avx2"))) void noise_blocks_avx2(const uint64_t* q, int n, uint64_t step,
+                                                       uint64_t seed, gs::U4* out) {
+  const __m256i m0 = _mm256_set1_epi32((int)0xD2511F53u), m1 = _mm256_set1_epi32((int)0xCD9E8D57u);
+  int i = 0;
+  for (; i + 8 <= n; i += 8) {
+    alignas(32) uint32_t lo[8], hi[8];
+    for (int k = 0; k < 8; ++k) {
+      lo[k] = (uint32_t)q[i + k];
+      hi[k] = (uint32_t)(q[i + k] >> 32);
+    }
+    __m256i c0 = _mm256_load_si256((const __m256i*)lo), c1 = _mm256_load_si256((const __m256i*)hi);
+    __m256i c2 = _mm256_set1_epi32((int)(uint32_t)step), c3 = _mm256_set1_epi32((int)(uint32_t)(step >> 32));
+    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    for (int r = 0; r < 10; ++r) {
+      const __m256i e0 = _mm256_mul_epu32(c0, m0), o0 = _mm256_mul_epu32(_mm256_srli_epi64(c0, 32), m0);
+      const __m256i e1 = _mm256_mul_epu32(c2, m1), o1 = _mm256_mul_epu32(_mm256_srli_epi64(c2, 32), m1);
+      const __m256i lo0 = _mm256_blend_epi32(e0, _mm256_slli_epi64(o0, 32), 0xAA);
+      const __m256i hi0 = _mm256_blend_epi32(_mm256_srli_epi64(e0, 32), o0, 0xAA);
+      const __m256i lo1 = _mm256_blend_epi32(e1, _mm256_slli_epi64(o1, 32), 0xAA);
+      const __m256i hi1 = _mm256_blend_epi32(_mm256_srli_epi64(e1, 32), o1, 0xAA);
+      const __m256i n0 = _mm256_xor_si256(_mm256_xor_si256(hi1, c1), _mm256_set1_epi32((int)k0));
+      const __m256i n2 = _mm256_xor_si256(_mm256_xor_si256(hi0, c3), _mm256_set1_epi32((int)k1));
+      c0 = n0;
+      c1 = lo1;
+      c2 = n2;
+      c3 = lo0;
+      k0 += 0x9E3779B9u;
+      k1 += 0xBB67AE85u;
+    }
+    alignas(32) uint32_t w[4][8];
+    _mm256_store_si256((__m256i*)w[0], c0);
+    _mm256_store_si256((__m256i*)w[1], c1);
+    _mm256_store_si256((__m256i*)w[2], c2);
+    _mm256_store_si256((__m256i*)w[3], c3);
+    for (int k = 0; k < 8; ++k) out[i + k] = gs::U4{w[0][k], w[1][k], w[2][k], w[3][k]};
+  }
+  noise_blocks_scalar(q + i, n - i, step, seed, out + i);
+}
+#endif
+
+// 1: the AVX2 form, 0: scalar (gs_noise_blocks' `impl`, -1: the one the step uses)
+bool cpu_has_avx2() {
+#if defined(__x86_64__)
+  static const bool yes = __builtin_cpu_supports("avx2");
+  return yes;
+#else
+  return false;
+#endif
+}
+
+void noise_blocks(const uint64_t* q, int n, uint64_t step, uint64_t seed, gs::U4* out, int impl = -1) {
+#if defined(__x86_64__)
+  if (impl == 1 || (impl < 0 && cpu_has_avx2())) {
+    noise_blocks_avx2(q, n, step, seed, out);
+    return;
+  }
+#endif
+  (void)impl;
+  noise_blocks_scalar(q, n, step, seed, out);
+}
 
 // One row of fp32 cell updates, two cells (u0 v0 u1 v1) per SSE2 vector.  The operations and
 // their order are those of gs::gs_update on each cell -- plain IEEE adds and multiplies (no FMA:
@@ -122,6 +199,7 @@ class CpuBackend final : public gs::Backend {
 #pragma omp parallel
     {
       gs::U4* cache = new gs::U4[R.nx > 0 ? R.nx : 1];
+      uint64_t* qrow = new uint64_t[R.nx > 0 ? R.nx : 1];
       float* rrow = new float[R.nx > 0 ? R.nx : 1];
 #pragma omp for schedule(static)
       for (int z = R.z0; z < R.z0 + R.nz; ++z) {
@@ -131,11 +209,15 @@ class CpuBackend final : public gs::Backend {
           int64_t gy = g.oy + y;
           if (gy < 0) gy += g.Ly; else if (gy >= g.Ly) gy -= g.Ly;
           if (noise && (y == R.y0 || (gy & 3) == 0)) {
+            // gs::noise_block's counters for the row, then the blocks eight at a time
+            const uint64_t Ly4 = ((uint64_t)g.Ly + 3) >> 2;
+            const uint64_t qy = (uint64_t)g.Lx * ((uint64_t)(gy >> 2) + Ly4 * (uint64_t)gz);
             for (int x = R.x0; x < R.x0 + R.nx; ++x) {
               int64_t gx = g.ox + x;
               if (gx < 0) gx += g.Lx; else if (gx >= g.Lx) gx -= g.Lx;
-              cache[x - R.x0] = gs::noise_block(gx, gy >> 2, gz, g.Lx, g.Ly, (uint64_t)t, seed);
+              qrow[x - R.x0] = (uint64_t)gx + qy;
             }
+            noise_blocks(qrow, R.nx, (uint64_t)t, seed, cache);
           }
           const int64_t base = 2 * gs::lin(g, 0, y, z);
           if constexpr (sizeof(T) == 4) {
@@ -162,6 +244,7 @@ class CpuBackend final : public gs::Backend {
         }
       }
       delete[] cache;
+      delete[] qrow;
       delete[] rrow;
     }
   }
@@ -270,6 +353,15 @@ gs::Backend* gs_make_backend(int32_t dtype, const gs::Geom& g, const gs::Params&
   if (dtype == gs::kF32) return new CpuBackend<float>(g, p, b0, b1, send, recv);
   if (dtype == gs::kF64) return new CpuBackend<double>(g, p, b0, b1, send, recv);
   throw std::runtime_error("unsupported dtype");
+}
+
+// Philox blocks of counters q[0, n) (gs::noise_block's (q, step, seed) stream) into out (4 words
+// each): impl 0 scalar, 1 AVX2 (-1 when the CPU lacks it), -1 the form the CPU step uses.
+extern "C" int gs_noise_blocks(const uint64_t* q, int32_t n, uint64_t step, uint64_t seed,
+                               uint32_t* out, int32_t impl) {
+  if (impl == 1 && !cpu_has_avx2()) return -1;
+  noise_blocks(q, n, step, seed, reinterpret_cast<gs::U4*>(out), impl);
+  return 0;
 }
 
 // OpenMP threads of the CPU backend in this process: n > 0 sets them, any n returns the

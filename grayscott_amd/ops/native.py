@@ -456,6 +456,22 @@ def peer_access_matrix():
     return [[int(buf[i * n + j]) for j in range(n)] for i in range(n)]
 
 
+def noise_blocks(q, step: int, seed: int, impl: int = -1):
+    """Philox4x32-10 blocks of counters ``q`` (uint64: (q, q >> 32, step, step >> 32), key
+    ``seed``) as an (n, 4) uint32 array, by the CPU backend's row routine: ``impl`` 0 scalar,
+    1 AVX2 (None when the CPU lacks it), -1 the form its step uses."""
+    import numpy as np
+    lib = load("core")
+    lib.gs_noise_blocks.argtypes = [c_void_p, c_int32, ctypes.c_uint64, ctypes.c_uint64,
+                                    c_void_p, c_int32]
+    lib.gs_noise_blocks.restype = c_int
+    qa = np.ascontiguousarray(np.asarray(q, dtype=np.uint64))
+    out = np.zeros((qa.size, 4), dtype=np.uint32)
+    rc = lib.gs_noise_blocks(qa.ctypes.data, qa.size, int(step), int(seed), out.ctypes.data,
+                             int(impl))
+    return None if rc != 0 else out
+
+
 def cpu_threads(n: int = 0) -> int:
     """OpenMP threads of the CPU backend in this process: ``n > 0`` sets them; returns the
     current maximum."""

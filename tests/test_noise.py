@@ -66,3 +66,20 @@ def test_native_block_equals_reference_layout():
         blk = native.noise_block(gx, gy >> 2, gz, Lx, Ly, step, 1234)
         w = ref.noise((Lx, Ly, 200), (gx, gy, gz), (1, 1, 1), step, 1234, dtype=np.float64)
         assert np.int32(np.uint32(blk[gy & 3])) * 2.0 ** -31 == w[0, 0, 0]
+
+
+@pytest.mark.parametrize("impl", [0, 1])
+def test_cpu_row_blocks_equal_reference_philox(impl):
+    """The CPU step's row routine (backend_cpu.cpp noise_blocks: scalar, and the AVX2 form that
+    runs eight counters per vector) equals the independent Python Philox4x32-10 for counters
+    below and above 2^32, steps above 2^32 and row lengths that leave a scalar tail."""
+    rng = np.random.default_rng(11)
+    q = np.concatenate([rng.integers(0, 2**32, 21, dtype=np.uint64),
+                        rng.integers(2**32, 2**40, 16, dtype=np.uint64)])
+    for step, seed in ((3, 0x5EED6A5C), (2**33 + 5, 2**63 + 12345)):
+        got = native.noise_blocks(q, step, seed, impl)
+        if got is None:
+            pytest.skip("no AVX2 on this CPU")
+        for i, qi in enumerate(q.tolist()):
+            want = ref.philox4x32_10(qi & 0xFFFFFFFF, qi >> 32, step & 0xFFFFFFFF, step >> 32, seed)
+            assert tuple(int(w) for w in got[i]) == tuple(int(w) for w in want), (i, impl)
