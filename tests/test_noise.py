@@ -83,3 +83,27 @@ def test_cpu_row_blocks_equal_reference_philox(impl):
         for i, qi in enumerate(q.tolist()):
             want = ref.philox4x32_10(qi & 0xFFFFFFFF, qi >> 32, step & 0xFFFFFFFF, step >> 32, seed)
             assert tuple(int(w) for w in got[i]) == tuple(int(w) for w in want), (i, impl)
+
+
+def test_cpu_step_flushes_denormals_but_restores_the_callers_fp_mode():
+    """The CPU solver flushes denormals inside its parallel step region (backend_cpu.cpp: MXCSR
+    FTZ + DAZ, a ~100x slowdown avoided on the reference example) and restores the calling
+    thread's mode afterwards: numpy on the main thread keeps IEEE denormals."""
+    from grayscott_amd.models.grayscott import GrayScott
+    from grayscott_amd.parallel.decomp import init_domain
+    from grayscott_amd.utils.config import Settings
+
+    s = Settings(L=12, precision="Float32", noise=0.0, F=0.02, k=0.048, dt=1.0, Du=0.2, Dv=0.1,
+                 backend="CPU")
+    sim = GrayScott(s, init_domain(12, 1, 0))
+    sim.init_fields()
+    u = np.full(sim.local_shape, 0.5, np.float32)
+    v = np.full(sim.local_shape, 1e-39, np.float32)  # denormal v everywhere
+    sim.set_fields(u, v)
+    sim.iterate(1)
+    _, v1 = sim.get_fields()
+    sim.close()
+    tiny = np.finfo(np.float32).tiny
+    assert not ((v1 != 0) & (np.abs(v1) < tiny)).any()  # no denormal survives the step
+    d = np.float32(1e-39)
+    assert d != 0 and d * np.float32(1.0) == d  # the main thread still computes denormals
