@@ -34,12 +34,19 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 T_START = time.perf_counter()
 _JSON_FD = 1  # the original stdout (main() points fd 1 at stderr for the run)
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+
+# What a failure record can report: the phase the run is in and the data-path tuning rows
+# finished so far (rank 0).  One JSON line per job, whatever happens (_emit_once).
+_PROGRESS = {"phase": "start", "rows": []}
+_EMIT = threading.Lock()
+_EMITTED = [False, True]  # printed, and whether that line reported success
 
 
 def parse_args(argv):
@@ -67,22 +74,155 @@ def parse_args(argv):
     ap.add_argument("--tune-budget", type=float, default=float(os.environ.get("GS_TUNE_BUDGET_S",
                                                                                 "180")),
                     help="seconds for the multi-rank data-path tuning (checks + timing)")
+    ap.add_argument("--deadline", type=float,
+                    default=float(os.environ.get("GS_BENCH_DEADLINE_S", "540")),
+                    help="seconds from start after which every rank gives up: rank 0 prints a "
+                         "JSON line with status 'timeout' (the phase it was in, the tuning rows "
+                         "finished) and the job exits 124 (0 = off)")
     ap.add_argument("--timeout", type=float, default=0.0,
-                    help="self-launched jobs: kill all ranks after this many seconds (0 = off)")
+                    help="self-launched jobs: kill all ranks after this many seconds (default: "
+                         "the deadline + 60 s)")
     return ap.parse_args(argv)
+
+
+def _metric_name(args) -> str:
+    return (f"MLUPS (cell-updates/sec, whole node) at L={args.L} "
+            f"{'fp32' if args.precision.lower() in ('float32', 'fp32') else 'fp64'}")
+
+
+def failure_record(args, status: str, n_gpus: int, **extra) -> dict:
+    """The one JSON line of a job that produced no measurement: the contract's keys with
+    ``value`` null, ``status`` ("timeout", "rank_failed", "error"), the phase the job was in
+    and the data-path tuning rows it finished."""
+    fp32 = args.precision.lower() in ("float32", "fp32")
+    rec = {"metric": _metric_name(args), "value": None, "unit": "MLUPS", "n_gpus": n_gpus,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": None,
+           "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+           "dtype": "fp32" if fp32 else "fp64",
+           "data": "synthetic: random-init u, v ~ U[0,1) on device" if args.init == "random"
+                   else "synthetic: reference seed-cube init",
+           "config": {"model": "gray-scott-3d-7pt", "L": args.L, "global_batch": 1,
+                      "seq_len": args.L, "parallelism": f"spatial-3d ({n_gpus} ranks)"},
+           "status": status, "phase": _PROGRESS["phase"],
+           "data_path_tuning": list(_PROGRESS["rows"]),
+           "wall_s": round(time.perf_counter() - T_START, 2)}
+    rec.update(extra)
+    return rec
+
+
+def _emit_once(rec: dict) -> bool:
+    """Write the job's JSON line (at most once per process)."""
+    with _EMIT:
+        if _EMITTED[0]:
+            return False
+        _EMITTED[0] = True
+        _EMITTED[1] = rec.get("status") == "ok"
+        os.write(_JSON_FD, (json.dumps(rec) + "\n").encode())
+        return True
+
+
+def _progress_row(row: dict) -> None:
+    """A finished data-path tuning row (rank 0): kept for a failure record and appended to
+    GS_BENCH_PROGRESS (set by a self-launching parent, which reports it if the job dies)."""
+    _PROGRESS["rows"].append(row)
+    path = os.environ.get("GS_BENCH_PROGRESS")
+    if path:
+        try:
+            with open(path, "a") as f:
+                f.write(json.dumps(row) + "\n")
+        except OSError:
+            pass
+
+
+def start_deadline(args, rank: int, world: int) -> None:
+    """Every rank: once ``args.deadline`` seconds have passed since start, rank 0 prints the
+    failure record (status "timeout") and every rank exits 124 at once -- a first-contact stall
+    on a fresh node (RCCL bootstrap, a peer that never joins, a device wait) yields a
+    parseable line inside the driver's own limit instead of nothing."""
+    if not args.deadline or args.deadline <= 0:
+        return
+
+    def fire():
+        left = args.deadline - (time.perf_counter() - T_START)
+        if left > 0:
+            time.sleep(left)
+        if _EMITTED[0]:
+            # the result line is out: only the teardown is left, give it a minute, then end
+            # with the status of the line already printed
+            time.sleep(60)
+            os._exit(0 if _EMITTED[1] else 1)
+        if rank == 0:
+            _emit_once(failure_record(args, "timeout", world, deadline_s=args.deadline))
+        print(f"bench.py: rank {rank}: deadline of {args.deadline:g} s reached in phase "
+              f"{_PROGRESS['phase']!r}; exiting", file=sys.stderr, flush=True)
+        sys.stderr.flush()
+        os._exit(124)
+
+    threading.Thread(target=fire, name="bench-deadline", daemon=True).start()
+
+
+def self_launch(args, argv, ngpus: int) -> int:
+    """``--gpus N`` without a launcher: run the N ranks here (parallel/launch.py), forward rank
+    0's JSON line, and if the job ended without one (a rank failed, the job's time limit),
+    print a failure record naming the failing rank and the tuning rows rank 0 streamed to
+    GS_BENCH_PROGRESS."""
+    import tempfile
+
+    from grayscott_amd.parallel.launch import spawn_local
+
+    timeout = args.timeout or ((args.deadline + 60.0) if args.deadline > 0 else None)
+    with tempfile.TemporaryDirectory(prefix="gs_bench_") as tmp:
+        out_path = os.path.join(tmp, "rank0.out")
+        prog = os.path.join(tmp, "progress.jsonl")
+        info: dict = {}
+        with open(out_path, "w") as out0:
+            rc = spawn_local(ngpus, [sys.executable, os.path.abspath(__file__)] + argv,
+                             timeout=timeout, cwd=ROOT, rank0_stdout=out0, info=info,
+                             extra_env={"GS_BENCH_PROGRESS": prog})
+        with open(out_path) as f:
+            text = f.read()
+        lines = [l for l in text.splitlines() if l.startswith("{")]
+        if lines:
+            line = lines[-1]
+            if rc != 0:
+                try:
+                    rec = json.loads(line)
+                except ValueError:
+                    rec = None
+                if isinstance(rec, dict) and rec.get("value") is None:
+                    # rank 0's own failure record: name the first rank this parent saw fail
+                    if info.get("failed_rank") not in (None, 0):
+                        rec["status"] = "rank_failed"
+                    rec["failed_rank"] = info.get("failed_rank")
+                    rec["exit_codes"] = info.get("codes")
+                    line = json.dumps(rec)
+            sys.stdout.write(line + "\n")
+            sys.stdout.flush()
+            return rc
+        rows = []
+        if os.path.exists(prog):
+            with open(prog) as f:
+                rows = [json.loads(l) for l in f if l.strip()]
+        _PROGRESS["rows"] = rows
+        _PROGRESS["phase"] = "unknown (no line from rank 0)"
+        status = "timeout" if info.get("timed_out") else "rank_failed"
+        rec = failure_record(args, status, ngpus, failed_rank=info.get("failed_rank"),
+                             exit_codes=info.get("codes"))
+        sys.stdout.write(json.dumps(rec) + "\n")
+        sys.stdout.flush()
+        return rc if rc else 1
 
 
 def main(argv=None) -> int:
     argv = list(sys.argv[1:] if argv is None else argv)
     args = parse_args(argv)
-    from grayscott_amd.parallel.launch import launcher_env, spawn_local
+    from grayscott_amd.parallel.launch import launcher_env
 
-    _, world, _ = launcher_env()
+    rank, world, _ = launcher_env()
     ngpus = args.gpus if args.gpus is not None else world
     if ngpus > 1 and world == 1:
         # self-launch: one worker per GPU, before anything initialises HIP in this process
-        return spawn_local(ngpus, [sys.executable, os.path.abspath(__file__)] + argv,
-                           timeout=args.timeout or None, cwd=ROOT)
+        return self_launch(args, argv, ngpus)
     # a blocked halo wait or control-plane collective becomes an error after this long (the
     # driver's own limit is minutes; a hung rank must not eat it)
     os.environ.setdefault("GS_COMM_TIMEOUT", "120")
@@ -95,9 +235,15 @@ def main(argv=None) -> int:
     sys.stdout.flush()
     _JSON_FD = os.dup(1)
     os.dup2(2, 1)
+    start_deadline(args, rank, world)
     try:
         return run(args)
-    except BaseException:
+    except BaseException as ex:
+        if rank == 0 and not isinstance(ex, (KeyboardInterrupt, SystemExit)):
+            # (with several ranks the cause may be a peer that failed first: a self-launching
+            # parent adds the first failing rank it saw)
+            _emit_once(failure_record(args, "error", world,
+                                      error=f"rank 0: {type(ex).__name__}: {ex}"[:400]))
         if world > 1:
             # one failed rank ends the job now instead of leaving its peers blocked
             import traceback
@@ -182,7 +328,11 @@ def profile_phases(sim, ctx, passes: int):
     rank's pass time, exchange span and critical path; ``accounted`` is the smallest share of a
     rank's measured pass time that its parts explain."""
     prof = sim.phase_profile(passes * max(1, int(sim.depth)))
-    rows = ctx.gather_object(prof)
+    return summarize_profiles(ctx.gather_object(prof))
+
+
+def summarize_profiles(rows):
+    """The ``phases`` entry from every rank's GrayScott.phase_profile (rank 0; None elsewhere)."""
     if not rows:
         return None
     names = sorted(set().union(*(r["phase_us"] for r in rows)))
@@ -222,16 +372,32 @@ def profile_reference_grid(settings, ctx, args, dims, row, passes: int):
     env = dict(row.get("env", {}))
     if not row.get("inplace_halos", True):
         env["GS_INPLACE_HALO"] = "0"
+    sim, prof, err = None, None, None
     with _env(env):
-        dom = init_domain(args.L, ctx.world_size, ctx.rank, periodic=False, dims=dims)
-        sim = GrayScott(s, dom, ctx)
         try:
+            dom = init_domain(args.L, ctx.world_size, ctx.rank, periodic=False, dims=dims)
+            sim = GrayScott(s, dom, ctx)
             sim.init_fields()
             sim.randomize_fields(seed=2024)
             sim.iterate(4 * max(1, int(sim.depth)))
-            out = profile_phases(sim, ctx, passes)
-        finally:
-            sim.close()
+            prof = sim.phase_profile(passes * max(1, int(sim.depth)))
+        except Exception as ex:  # agreed below: a rank failing alone never strands the others
+            err = f"rank {ctx.rank}: {type(ex).__name__}: {ex}"[:200]
+        # every rank gets here whatever failed locally, and all agree before any collective
+        # that needs every rank's result (the gather below, the IPC close barrier)
+        ok = ctx.allreduce(0.0 if err else 1.0, "min") > 0
+        if sim is not None:
+            try:
+                sim.synchronize()
+            except Exception as ex:
+                err = err or f"rank {ctx.rank}: {ex}"[:200]
+        ctx.barrier()  # no rank frees buffers its peers may still write (IPC)
+        if sim is not None:
+            sim.close(barrier=False)
+    if not ok:
+        errs = [e for e in ctx.allgather_object(err) if e]
+        return {"error": "; ".join(errs)[:400]} if ctx.rank == 0 else None
+    out = summarize_profiles(ctx.gather_object(prof))
     if out is not None:
         out["summary"]["dims"] = list(dims)
     return out
@@ -253,6 +419,7 @@ def run(args) -> int:
     backend, _ = load_backend_and_lang(settings)
     ctx = init_from_env("hip" if backend == "hip" else "cpu")
     dims = choose_dims(args.L, ctx.world_size, args.decomposition, backend)
+    _PROGRESS["phase"] = "data-path tuning"
     tuning = None
     t_tune = time.perf_counter()
     if ctx.world_size > 1:
@@ -265,12 +432,14 @@ def run(args) -> int:
             cands = [(dims, args.fuse)]
         log = (lambda m: print(f"bench.py: {m}", file=sys.stderr, flush=True))
         tuning = tune_data_path(settings, ctx, args.L, backend, cands=cands, log=log,
-                                budget_s=args.tune_budget)
+                                budget_s=args.tune_budget,
+                                on_row=_progress_row if ctx.rank == 0 else None)
         dims = tuning["dims"]
         settings.fuse_steps = tuning["fuse"]
         settings.transport, settings.overlap = tuning["transport"], tuning["overlap"]
         os.environ.update(tuning["env"])
     tuning_s = time.perf_counter() - t_tune
+    _PROGRESS["phase"] = "set-up of the chosen data path"
     dom = init_domain(args.L, ctx.world_size, ctx.rank, periodic=False, dims=dims)
     sim = GrayScott(settings, dom, ctx, use_fused=not args.no_fused_kernel)
     sim.init_fields()
@@ -289,13 +458,20 @@ def run(args) -> int:
         if backend == "hip":
             torch.cuda.synchronize()
 
+    _PROGRESS["phase"] = "warm-up"
     sim.iterate(args.warmup)
     sync()
-    if (os.environ.get("GS_RAISE_AT_STEP") is not None and
-            int(os.environ.get("GS_FAIL_RANK", "-1")) in (-1, ctx.rank)):
-        raise RuntimeError(f"injected failure on rank {ctx.rank} (GS_RAISE_AT_STEP)")
+    if int(os.environ.get("GS_FAIL_RANK", "-1")) in (-1, ctx.rank):
+        if os.environ.get("GS_RAISE_AT_STEP") is not None:
+            raise RuntimeError(f"injected failure on rank {ctx.rank} (GS_RAISE_AT_STEP)")
+        if os.environ.get("GS_STALL_AT_STEP") is not None:
+            # a rank that stops answering (the deadline's test): peers block in the barrier
+            print(f"bench.py: rank {ctx.rank} stalls (GS_STALL_AT_STEP)", file=sys.stderr,
+                  flush=True)
+            time.sleep(1e6)
     ctx.barrier()
     sync()
+    _PROGRESS["phase"] = "timed region"
     t0 = time.perf_counter()
     sim.iterate(args.steps)
     sync()
@@ -306,6 +482,7 @@ def run(args) -> int:
     stats = sim.global_stats()
     world_info = ctx.gather_object(sim.device_info())
     phases = None
+    _PROGRESS["phase"] = "phase profile"
     if args.profile_passes > 0:
         # outside the timed region: the state it advances is reset by the golden check
         t_prof = time.perf_counter()
@@ -319,16 +496,15 @@ def run(args) -> int:
                 phases["reference_grid"] = None
                 if rows:
                     r = min(rows, key=lambda r: r["ms_per_step"])
-                    try:
-                        # the same construction the tuning timed for this row
-                        phases["reference_grid"] = profile_reference_grid(
-                            settings, ctx, args, bal, r, args.profile_passes)
-                    except Exception as ex:  # recorded; the headline is already measured
-                        phases["reference_grid"] = {"error": str(ex)[:200]}
+                    # the same construction the tuning timed for this row; a failure is
+                    # agreed by all ranks and recorded (the headline is already measured)
+                    phases["reference_grid"] = profile_reference_grid(
+                        settings, ctx, args, bal, r, args.profile_passes)
             from grayscott_amd.ops import native
             phases["peer_access"] = native.peer_access_matrix() if ctx.rank == 0 else None
         phases["profile_s"] = round(time.perf_counter() - t_prof, 2)
     if do_golden:
+        _PROGRESS["phase"] = "golden check"
         t_chk = time.perf_counter()
         err = golden_check(sim, settings, dom, args.check_steps,
                            2024 if args.init == "random" else None)
@@ -401,7 +577,9 @@ def run(args) -> int:
             rec["phases"] = phases
         if ref_grid is not None and ctx.world_size == 8 and ref_grid["dims"] == [2, 2, 2]:
             rec["config3_2x2x2"] = ref_grid
-        os.write(_JSON_FD, (json.dumps(rec) + "\n").encode())
+        rec["status"] = "ok" if check.get("golden_ok", True) else "golden_check_failed"
+        _emit_once(rec)
+    _PROGRESS["phase"] = "teardown"
     sim.close()
     ctx.finalize()
     return 0 if check.get("golden_ok", True) else 1

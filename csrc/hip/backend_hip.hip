@@ -46,7 +46,7 @@ extern template bool launch_shell<double>(const void*, void*, const Geom&, const
 #define NCCL_CHECK(expr)                                                                  \
   do {                                                                                    \
     ncclResult_t _r = (expr);                                                             \
-    if (_r != ncclSuccess)                                                                \
+    if (_r != ncclSuccess && _r != ncclInProgress)                                        \
       throw std::runtime_error(std::string("RCCL error: ") + ncclGetErrorString(_r) +      \
                                " (" #expr ")");                                           \
   } while (0)
@@ -360,7 +360,7 @@ class HipBackend final : public gs::Backend {
       NCCL_CHECK(ncclRecv(buf_[b] + gs::box_start(g_, m.box),
                           (size_t)gs::box_cells(m.box) * sizeof(V2), ncclUint8, m.peer, comm_, xs_));
     }
-    NCCL_CHECK(ncclGroupEnd());
+    group_end();
     return true;
   }
 
@@ -579,7 +579,7 @@ class HipBackend final : public gs::Backend {
     HIP_CHECK(hipDeviceGetPCIBusId(out + sizeof(h), kIpcPciBytes - 1, dev_));
     int khz = 0;
     HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev_));
-    const double to = getenv("GS_COMM_TIMEOUT") ? atof(getenv("GS_COMM_TIMEOUT")) : 900.0;
+    const double to = gs::comm_timeout_s();
     ipc_ticks_ = (uint64_t)(std::max(1.0, to) * (double)std::max(khz, 1) * 1000.0);
     const double emu = gs::debug_knobs().ipc_emulate_us;  // modelling only (gs/debug.h)
     ipc_emulate_ticks_ = (uint64_t)(std::max(0.0, emu) * (double)std::max(khz, 1) / 1000.0);
@@ -795,7 +795,7 @@ class HipBackend final : public gs::Backend {
       NCCL_CHECK(ncclRecv(recv_ + m.offset, (size_t)gs::box_cells(m.box) * sizeof(V2), ncclUint8,
                           m.peer, comm_, xs_));
     }
-    NCCL_CHECK(ncclGroupEnd());
+    group_end();
     return true;
   }
 
@@ -831,7 +831,7 @@ class HipBackend final : public gs::Backend {
       if (b != hipErrorNotReady) HIP_CHECK(b);
       ncclResult_t async = ncclSuccess;
       if (comm_) NCCL_CHECK(ncclCommGetAsyncError(comm_, &async));
-      if (async != ncclSuccess) {
+      if (async != ncclSuccess && async != ncclInProgress) {
         abort_comm();
         throw std::runtime_error(std::string("RCCL asynchronous error: ") + ncclGetErrorString(async));
       }
@@ -896,6 +896,13 @@ class HipBackend final : public gs::Backend {
     out3[0] = n; out3[1] = r; out3[2] = d;
   }
 
+  // The communicator is created non-blocking (config.blocking = 0) and its set-up is polled
+  // under GS_COMM_TIMEOUT: a peer that never joins, or a bootstrap / topology stall on a fresh
+  // node, becomes an error (the communicator aborted, the transport chain moves on) instead of
+  // a process blocked inside ncclCommInitRank for the rest of the job.  Every later call on a
+  // non-blocking communicator may also return ncclInProgress -- the first send / receive to a
+  // peer sets up its connection asynchronously -- so each group end is completed the same way
+  // (group_end) before anything else is enqueued behind it.
   void init_comm(const ncclUniqueId& id, int nranks, int rank) {
     SharedComm& sc = shared_comm();
     if (sc.comm && sc.nranks == nranks && sc.rank == rank) {
@@ -904,8 +911,57 @@ class HipBackend final : public gs::Backend {
       return;
     }
     rank_ = rank;
-    NCCL_CHECK(ncclCommInitRank(&comm_, nranks, id, rank));
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    ncclComm_t c = nullptr;
+    const ncclResult_t r = ncclCommInitRankConfig(&c, nranks, id, rank, &cfg);
+    if (r != ncclSuccess && r != ncclInProgress) {
+      if (c) ncclCommAbort(c);
+      throw std::runtime_error(std::string("RCCL error: ") + ncclGetErrorString(r) +
+                               " (ncclCommInitRankConfig)");
+    }
+    comm_ = c;
+    complete(c, "communicator set-up (ncclCommInitRankConfig)");
     if (!sc.comm) sc = SharedComm{comm_, nranks, rank};  // kept for the process lifetime
+  }
+
+  // Wait for a non-blocking communicator's pending operation (set-up, a group's connection
+  // set-up) under GS_COMM_TIMEOUT; on an error or timeout abort the communicator and throw.
+  void complete(ncclComm_t c, const char* what) {
+    const double to = gs::comm_timeout_s();
+    const auto t0 = std::chrono::steady_clock::now();
+    int sleep_us = 10;
+    for (;;) {
+      ncclResult_t st = ncclSuccess;
+      const ncclResult_t q = ncclCommGetAsyncError(c, &st);
+      if (q != ncclSuccess) st = q;
+      if (st == ncclSuccess) return;
+      if (st != ncclInProgress) {
+        abort_comm();
+        throw std::runtime_error(std::string("RCCL error: ") + ncclGetErrorString(st) + " in " +
+                                 what);
+      }
+      const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (el > to) {
+        abort_comm();
+        throw std::runtime_error(std::string("RCCL ") + what + " did not complete within " +
+                                 std::to_string(to) + " s (GS_COMM_TIMEOUT): a peer never joined "
+                                 "or the node's topology set-up stalled");
+      }
+      std::this_thread::sleep_for(std::chrono::microseconds(sleep_us));
+      if (sleep_us < 1000) sleep_us *= 2;
+    }
+  }
+
+  // ncclGroupEnd on the non-blocking communicator: in steady state the group is enqueued before
+  // it returns; the first exchange with a peer returns ncclInProgress while the connection is
+  // made, and completes here, so the stream order of later work is unchanged
+  void group_end() {
+    const ncclResult_t r = ncclGroupEnd();
+    if (r == ncclSuccess) return;
+    if (r != ncclInProgress)
+      throw std::runtime_error(std::string("RCCL error: ") + ncclGetErrorString(r) + " (ncclGroupEnd)");
+    complete(comm_, "point-to-point connection set-up (ncclGroupEnd)");
   }
 
  private:

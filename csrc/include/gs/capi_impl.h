@@ -96,12 +96,10 @@ int gs_exchange(gs_engine* e) { GS_TRY(e->eng->exchange()) }
 int64_t gs_get_step(gs_engine* e) { return e->eng->step(); }
 int gs_set_step(gs_engine* e, int64_t t) { GS_TRY(e->eng->set_step(t)) }
 int gs_current_buffer(gs_engine* e) { return e->eng->cur(); }
-// Waits for all queued work.  GS_COMM_TIMEOUT (seconds, default 900) bounds the wait when a
-// device transport is active: a hung or failed halo exchange becomes an error, not a hang.
-int gs_sync(gs_engine* e) {
-  static const double timeout = getenv("GS_COMM_TIMEOUT") ? atof(getenv("GS_COMM_TIMEOUT")) : 900.0;
-  GS_TRY(e->eng->backend()->wait_all(timeout))
-}
+// Waits for all queued work.  GS_COMM_TIMEOUT (seconds, default 900; read at every call) bounds
+// the wait when a device transport is active: a hung or failed halo exchange becomes an error,
+// not a hang.
+int gs_sync(gs_engine* e) { GS_TRY(e->eng->backend()->wait_all(gs::comm_timeout_s())) }
 int gs_extract(gs_engine* e, void* u, void* v) {
   GS_TRY(e->eng->backend()->extract(e->eng->cur(), u, v))
 }
@@ -128,9 +126,8 @@ int gs_phase_count(void) { return gs::kNumPhases; }
 const char* gs_phase_name(int32_t i) { return gs::phase_name(i); }
 int gs_prof_start(gs_engine* e, int32_t max_records) { GS_TRY(e->eng->prof_start(max_records)) }
 int gs_prof_stop(gs_engine* e, double* out) {
-  static const double timeout = getenv("GS_COMM_TIMEOUT") ? atof(getenv("GS_COMM_TIMEOUT")) : 900.0;
   try {
-    return e->eng->prof_stop(out, timeout);
+    return e->eng->prof_stop(out, gs::comm_timeout_s());
   } catch (const std::exception& ex) {
     g_gs_err = ex.what();
     return -1;

@@ -27,6 +27,15 @@ namespace gs {
 
 enum DType : int32_t { kF32 = 0, kF64 = 1 };
 
+// Seconds a blocked communication step (RCCL set-up, a halo exchange, a device wait) may take
+// before it becomes an error: GS_COMM_TIMEOUT, read at every call so a caller that changes it
+// for one engine (the data-path tuner's candidates) is obeyed.  Default 900.
+inline double comm_timeout_s() {
+  const char* e = getenv("GS_COMM_TIMEOUT");
+  const double v = e ? atof(e) : 900.0;
+  return v > 0.0 ? v : 900.0;
+}
+
 // Transport callback: exchange the packed send buffer into the receive buffer.
 // Returns 0 on success.
 typedef int (*TransportFn)(void* user);

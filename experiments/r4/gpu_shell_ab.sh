@@ -1,7 +1,7 @@
 # Round 4: (1) shell changes (x/y-only k_slab <= 256 VGPRs; variant 2 = z slabs beside the x/y
 # slabs on a side stream) + padded-row boundary fill + the SALU-lean block kernel (k_block_sl):
 # correctness tests, the 256^3 shell splits, L=64 block A/B and bench, the driver's N=1 command;
-# (2) the fused-kernel A/B (scripts/r4/gpu_ab.sh).
+# (2) the fused-kernel A/B (experiments/r4/gpu_ab.sh).
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/${GS_OUT:-r4shell}
@@ -14,5 +14,5 @@ timeout -k 10 200 python bench.py --L 64 --steps 2000 --warmup 200 > $O/n1_L64.j
 timeout -k 10 300 python scripts/bench_overlap_split.py --packed --one-sided --L 256 --nz 256 --k 3 2 --out $O/split_onesided.json > $O/split.log 2>&1 &&
 timeout -k 10 300 python scripts/bench_overlap_split.py --packed --L 256 --nz 256 --k 3 --out $O/split_allsides.json >> $O/split.log 2>&1 &&
 timeout -k 10 150 python bench.py --steps 20 --warmup 5 > $O/n1.json 2> $O/n1.err &&
-GS_OUT=r4ab bash scripts/r4/gpu_ab.sh
+GS_OUT=r4ab bash experiments/r4/gpu_ab.sh
 echo "exit $?"

@@ -25,6 +25,10 @@ from ..parallel.halo import TorchTransport
 from ..utils.config import Settings, load_backend_and_lang, parse_precision
 
 _TORCH_DTYPES = {"float32": torch.float32, "float64": torch.float64}
+# set (identically on every rank: the chain's outcome is agreed) once RCCL failed its set-up or
+# trial exchange in this process's "auto" transport chain: later engines skip it instead of
+# paying its GS_COMM_TIMEOUT again (the data-path tuner builds a dozen engines)
+_RCCL_FAILED = [False]
 _NP_DTYPES = {"float32": np.float32, "float64": np.float64}
 
 
@@ -74,7 +78,7 @@ class GrayScott:
 
     def __init__(self, settings: Settings, domain: CartDomain, ctx: Optional[DistContext] = None,
                  fuse: Optional[int] = None, transport: Optional[str] = None,
-                 use_fused: bool = True, loopback: bool = False):
+                 use_fused: bool = True, loopback: bool = False, skip_rccl: bool = False):
         self.settings = settings
         self.domain = domain
         self.ctx = ctx or DistContext()
@@ -122,6 +126,9 @@ class GrayScott:
             raise ValueError(f"overlap must be auto | on | off, not {ov!r}")
         self.engine.set_overlap(-1 if ov == "auto" else (1 if ov in ("on", "true", "1") else 0))
         self.transport = "none"
+        # the data-path tuner's candidates after RCCL failed to set up on this node: the "auto"
+        # transport chain starts after it (parallel/autotune.py)
+        self._skip_rccl = bool(skip_rccl)
         if loopback:
             # single-GPU test mode: the periodic wraps onto this rank go through RCCL
             # send/recv-to-self, exercising the multi-rank data path (engine.h set_loopback)
@@ -138,8 +145,8 @@ class GrayScott:
         kind = (kind or "auto").lower()
         if kind == "auto":
             chain = ["rccl", "torch", "host"] if self.backend == "hip" else ["torch"]
-            if os.environ.get("GS_TUNE_SKIP_RCCL") == "1" and self.backend == "hip":
-                chain = ["torch", "host"]  # RCCL failed to set up earlier in this job (tuning)
+            if (self._skip_rccl or _RCCL_FAILED[0]) and self.backend == "hip":
+                chain = ["torch", "host"]  # RCCL failed to set up earlier in this job
             errors = []
             for k in chain:
                 try:
@@ -154,6 +161,8 @@ class GrayScott:
                     errors.append(f"{k}: {ex}")
                     ok = self.ctx.allreduce(0.0, "min") if self.ctx.is_distributed else 0.0
                 if ok <= 0:
+                    if k == "rccl":
+                        _RCCL_FAILED[0] = True
                     # a transport that set up but failed its trial (on any rank) must not stay
                     # behind the next one: abort its communicator / unmap its peers first
                     self.engine.drop_transport()
@@ -453,12 +462,15 @@ class GrayScott:
         return {"mean_u": tot[0] / n, "min_u": mn[0], "max_u": mx[0],
                 "mean_v": tot[1] / n, "min_v": mn[1], "max_v": mx[1]}
 
-    def close(self) -> None:
+    def close(self, barrier: bool = True) -> None:
+        """Free the engine.  With the IPC transport every rank drains its streams and meets the
+        others at a barrier first (peers store into this rank's landing buffer until their last
+        exchange); ``barrier=False``: the caller has already done both on every rank."""
         if getattr(self, "_snaps", None):
             self._io_stream.synchronize()  # no D2H copy may still read the snapshot buffers
             self._snaps = None
         if getattr(self, "engine", None) is not None:
-            if self.transport == "ipc":
+            if self.transport == "ipc" and barrier:
                 # peers store into this rank's landing buffer and flags until their last
                 # exchange has finished: every rank drains its streams before any rank frees
                 try:

@@ -32,7 +32,7 @@ from .decomp import choose_dims, dims_create, init_domain
 
 
 def selfcheck(ctx, backend: str, dims, fuse: int, transport: str, overlap: str, L: int = 64,
-              steps: int = 15, precision: str = "Float32"):
+              steps: int = 15, precision: str = "Float32", skip_rccl: bool = False):
     """Run the exact data path (decomposition, transport, in-place halos, overlap, fuse depth,
     precision) on a small grid from the benchmarks' random init and compare with the
     numpy/torch golden model computed by every rank.  Returns ``(ok, max_abs_err,
@@ -40,7 +40,8 @@ def selfcheck(ctx, backend: str, dims, fuse: int, transport: str, overlap: str, 
 
     A rank that fails locally (set-up, a device wait that timed out, ...) still makes the same
     collectives as the others -- its error is reported as an infinite difference -- so the
-    ranks' collective sequences never diverge."""
+    ranks' collective sequences never diverge.  ``skip_rccl``: the "auto" transport chain starts
+    after RCCL (it failed to set up earlier on this node)."""
     import numpy as np
 
     from ..models.grayscott import GrayScott
@@ -55,7 +56,7 @@ def selfcheck(ctx, backend: str, dims, fuse: int, transport: str, overlap: str, 
                      noise=0.1, backend="AMDGPU" if backend == "hip" else "CPU", seed=77,
                      transport=transport, overlap=overlap)
         dom = init_domain(L, ctx.world_size, ctx.rank, periodic=False, dims=dims)
-        sim = GrayScott(s, dom, ctx, fuse=min(fuse, min(dom.proc_sizes)))
+        sim = GrayScott(s, dom, ctx, fuse=min(fuse, min(dom.proc_sizes)), skip_rccl=skip_rccl)
         try:
             sim.init_fields()
             sim.randomize_fields(seed=5)
@@ -124,7 +125,7 @@ def candidates(L: int, nprocs: int, backend: str) -> List[Tuple]:
 
 
 def time_data_path(settings, ctx, L: int, dims, fuse: int, steps: int = 30, warmup: int = 6,
-                   seed: int = 2024):
+                   seed: int = 2024, skip_rccl: bool = False):
     """(seconds for ``steps`` steps of the real problem on this data path (max over ranks),
     whether its passes overlap the halo exchange)."""
     import torch
@@ -134,7 +135,7 @@ def time_data_path(settings, ctx, L: int, dims, fuse: int, steps: int = 30, warm
     s = copy.copy(settings)
     s.fuse_steps = int(fuse)
     dom = init_domain(L, ctx.world_size, ctx.rank, periodic=False, dims=dims)
-    sim = GrayScott(s, dom, ctx)
+    sim = GrayScott(s, dom, ctx, skip_rccl=skip_rccl)
     try:
         sim.init_fields()
         sim.randomize_fields(seed=seed)
@@ -160,7 +161,7 @@ def time_data_path(settings, ctx, L: int, dims, fuse: int, steps: int = 30, warm
 def tune_data_path(settings, ctx, L: int, backend: str,
                    cands: Optional[Sequence[Tuple]] = None,
                    steps: int = 120, warmup: int = 12, log=None,
-                   budget_s: Optional[float] = None) -> Dict:
+                   budget_s: Optional[float] = None, on_row=None) -> Dict:
     """Self-check and time every candidate ``(dims, fuse[, overlap[, env]])``; returns
     ``{"dims", "fuse", "transport", "overlap", "inplace_halos", "env", "table"}`` for the fastest
     correct one (identical on every rank; ``env`` must be set for the run that uses it).
@@ -170,11 +171,14 @@ def tune_data_path(settings, ctx, L: int, backend: str,
     least two are always tried.  Once one candidate's transport passed its check, later
     candidates do not retry the fallback transports: a failure there is the path's own.
 
-    Fail fast per transport: once a pinned transport (IPC) fails a candidate's check -- a peer
-    wait that timed out, a mapping error, a mismatch -- every later candidate pinned to it is
-    skipped (``"skipped": "ipc failed: <reason>"``), so a node whose cross-device IPC
-    misbehaves pays its timeout once, not once per IPC row.  Likewise, once RCCL failed to set
-    up, later candidates' fallback chains start after it (``GS_TUNE_SKIP_RCCL``)."""
+    Fail fast per transport: once a pinned transport (IPC) fails a candidate's check with a
+    transport-level error on some rank -- a peer wait that timed out, a mapping or set-up
+    error -- every later candidate pinned to it is skipped (``"skipped": "ipc failed:
+    <reason>"``), so a node whose cross-device IPC misbehaves pays its timeout once, not once
+    per IPC row.  A numerical mismatch is the candidate's own (its grid, overlap mode or tile):
+    later rows on the same transport are still tried.  Likewise, once RCCL failed to set up,
+    later candidates' fallback chains start after it (``skip_rccl``).  ``on_row(row)`` is
+    called with every finished table row (bench.py streams them for a failure report)."""
     from ..models.grayscott import default_fuse
 
     cands = list(cands) if cands is not None else candidates(L, ctx.world_size, backend)
@@ -183,12 +187,18 @@ def tune_data_path(settings, ctx, L: int, backend: str,
     t_start = time.perf_counter()
     proven = None  # transport that passed a check on this node
     failed: Dict[str, str] = {}  # pinned transport -> why it failed on this node
+
+    def finish(row):
+        table.append(row)
+        if on_row is not None:
+            on_row(row)
+
     for ci, cand in enumerate(cands):
         over = budget_s is not None and time.perf_counter() - t_start > budget_s
         if ci >= 2 and ctx.allreduce(1.0 if over else 0.0, "max") > 0:
-            table.append({"dims": list(cand[0]), "fuse": cand[1],
-                          "overlap_req": cand[2] if len(cand) > 2 else settings.overlap,
-                          "skipped": "budget"})
+            finish({"dims": list(cand[0]), "fuse": cand[1],
+                    "overlap_req": cand[2] if len(cand) > 2 else settings.overlap,
+                    "skipped": "budget"})
             continue
         dims, fuse = cand[0], cand[1]
         ov0 = cand[2] if len(cand) > 2 else settings.overlap
@@ -209,7 +219,7 @@ def tune_data_path(settings, ctx, L: int, backend: str,
             # (every rank holds the same `failed`: it is built from agreed results only)
             row["skipped"] = f"{tr0} failed: {failed[tr0]}"
             row["ok"] = False
-            table.append(row)
+            finish(row)
             continue
         chosen = None
         attempts = [(settings.transport, ov0, {}),
@@ -223,15 +233,15 @@ def tune_data_path(settings, ctx, L: int, backend: str,
             # a fixed transport: no fallback chain; a peer that never signals ends its device
             # waits after 20 s instead of GS_COMM_TIMEOUT
             attempts = [(tr0, ov0, {"GS_COMM_TIMEOUT": "20"})]
-        if "rccl" in failed:
-            # the fallback chain of "auto" starts after RCCL (its set-up failed before)
-            attempts = [(tr, ov, {**extra, "GS_TUNE_SKIP_RCCL": "1"}) for tr, ov, extra in attempts]
+        # the fallback chain of "auto" starts after RCCL once its set-up failed on this node
+        skip_rccl = "rccl" in failed
         for tr, ov, extra in attempts:
             env = {**env0, **extra}
             with _env(env):
                 # selfcheck never raises and makes the same collectives on every rank
                 ok, err, used, text = selfcheck(ctx, backend, dims, f, tr, ov,
-                                                precision=settings.precision)
+                                                precision=settings.precision,
+                                                skip_rccl=skip_rccl)
             if not ok:
                 # reported in the bench JSON (data_path_tuning): why a transport failed
                 row.setdefault("check_errors", []).append(
@@ -239,7 +249,10 @@ def tune_data_path(settings, ctx, L: int, backend: str,
             ok = ctx.allreduce(1.0 if ok else 0.0, "min") > 0
             # agreed failure reasons (every rank the same): rank 0's text, or the mismatch
             why = ctx.broadcast_object((text or f"max |err| {err:.3g} vs golden")[:120], src=0)
-            if not ok and tr0:
+            # a transport-level failure: some rank raised (set-up, mapping, a wait that timed
+            # out); a pure mismatch raised nowhere (selfcheck's error text stays None)
+            raised = ctx.allreduce(1.0 if text else 0.0, "max") > 0
+            if not ok and tr0 and raised:
                 failed[tr0] = why
             if not ok and "rccl" in why.lower() and ("init" in why.lower() or
                                                      "unique" in why.lower()):
@@ -251,25 +264,26 @@ def tune_data_path(settings, ctx, L: int, backend: str,
                 break
         if chosen is None:
             row.update(ok=False)
-            table.append(row)
+            finish(row)
             continue
         s = copy.copy(settings)
         s.transport, s.overlap = chosen[0], chosen[1]
         with _env(chosen[2]):
             try:
-                el, ovd = time_data_path(s, ctx, L, dims, f, steps=steps, warmup=warmup)
+                el, ovd = time_data_path(s, ctx, L, dims, f, steps=steps, warmup=warmup,
+                                         skip_rccl=skip_rccl)
                 ran = 1.0
             except Exception as ex:  # e.g. out of memory at the real size: skip this path
                 el, ovd, ran = float("inf"), False, 0.0
                 row["error"] = str(ex)[:200]
         if ctx.allreduce(ran, "min") <= 0:
             row.update(ok=False)
-            table.append(row)
+            finish(row)
             continue
         row.update(ok=True, transport=chosen[0], overlap=chosen[1], overlapped=ovd,
                    inplace_halos=chosen[2].get("GS_INPLACE_HALO") != "0",
                    ms_per_step=round(1e3 * el / steps, 4), steps=steps)
-        table.append(row)
+        finish(row)
         if log is not None and ctx.rank == 0:
             log(f"data path {row}")
         if best is None or el < best[0]:

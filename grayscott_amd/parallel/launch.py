@@ -72,7 +72,8 @@ def worker_env(rank: int, nprocs: int, port: int, base: Optional[Dict[str, str]]
 def spawn_local(nprocs: int, cmd: Sequence[str], *, port: Optional[int] = None,
                 extra_env: Optional[Dict[str, str]] = None, timeout: Optional[float] = None,
                 grace: float = 30.0, cwd: Optional[str] = None,
-                rank0_stdout=None, others_stdout=None, poll: float = 0.05) -> int:
+                rank0_stdout=None, others_stdout=None, poll: float = 0.05,
+                info: Optional[dict] = None) -> int:
     """Run ``cmd`` as ``nprocs`` local ranks and return the job's exit status.
 
     Rank 0's stdout goes to ``rank0_stdout`` (default: this process's stdout); the other ranks'
@@ -80,7 +81,9 @@ def spawn_local(nprocs: int, cmd: Sequence[str], *, port: Optional[int] = None,
     a result line.  stderr is inherited.  The status is 0 only if every rank exited 0; otherwise
     it is the first failure's code (negative signal numbers mapped to 128 + signal).  A rank
     still running ``grace`` seconds after another failed, or when ``timeout`` expires, is
-    terminated (SIGTERM, then SIGKILL 10 s later) -- each by the PID this call started."""
+    terminated (SIGTERM, then SIGKILL 10 s later) -- each by the PID this call started.
+    ``info`` (a dict, filled in): ``failed_rank`` (the first rank seen failing, or None),
+    ``timed_out`` (the ``timeout`` ended the job) and ``codes`` (every rank's exit status)."""
     port = port or free_port()
     out0 = rank0_stdout if rank0_stdout is not None else sys.stdout
     outn = others_stdout if others_stdout is not None else sys.stderr
@@ -97,27 +100,37 @@ def spawn_local(nprocs: int, cmd: Sequence[str], *, port: Optional[int] = None,
                                           stdout=out0 if r == 0 else outn))
         t0 = time.monotonic()
         first_fail: Optional[int] = None
+        failed_rank: Optional[int] = None
+        timed_out = False
         fail_time = None
         while True:
             codes = [p.poll() for p in procs]
             if all(c is not None for c in codes):
                 break
-            for c in codes:
+            for r, c in enumerate(codes):
                 if c not in (None, 0) and first_fail is None:
                     first_fail = _status(c)
+                    failed_rank = r
                     fail_time = time.monotonic()
             now = time.monotonic()
             if ((fail_time is not None and now - fail_time > grace) or
                     (timeout is not None and now - t0 > timeout)):
                 if first_fail is None:
                     first_fail = 124  # timeout(1)'s status
+                    timed_out = True
                 _terminate(procs)
                 break
             time.sleep(poll)
         codes = [p.wait() for p in procs]
         if first_fail is None:
-            bad = [_status(c) for c in codes if c != 0]
-            first_fail = bad[0] if bad else 0
+            bad = [(r, _status(c)) for r, c in enumerate(codes) if c != 0]
+            if bad:
+                failed_rank, first_fail = bad[0]
+            else:
+                first_fail = 0
+        if info is not None:
+            info.update(failed_rank=failed_rank, timed_out=timed_out,
+                        codes=[_status(c) for c in codes])
         return first_fail
     except BaseException:
         _terminate(procs)

@@ -93,7 +93,45 @@ def test_bench_self_launch_propagates_failure():
                        cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode != 0
     assert "injected failure on rank 1" in r.stderr
-    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+    # one parseable line all the same: no value, the status and the failing rank
+    d = _last_json(r.stdout)
+    assert KEYS <= set(d)
+    assert d["value"] is None and d["status"] == "rank_failed" and d["failed_rank"] == 1
+
+
+def _no_launcher_env(**extra):
+    env = dict(os.environ, OMP_NUM_THREADS="1", **extra)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    return env
+
+
+@pytest.mark.parametrize("launch", ["self", "torchrun"])
+def test_bench_deadline_stalled_rank(launch):
+    """A rank that stops answering (GS_STALL_AT_STEP on rank 1) while rank 0 waits in a
+    collective: every rank gives up at the job's deadline, well before the control plane's
+    own timeout, and stdout still carries exactly one parseable line (status "timeout", the
+    phase rank 0 was in)."""
+    import time
+    env = _no_launcher_env(GS_COMM_TIMEOUT="300", GS_STALL_AT_STEP="0", GS_FAIL_RANK="1")
+    args = ["bench.py", "--gpus", "2", "--backend", "CPU", "--L", "16", "--steps", "2",
+            "--warmup", "1", "--decomposition", "balanced", "--deadline", "25"]
+    if launch == "torchrun":
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
+               "2", "--master-addr", "127.0.0.1", "--master-port", str(free_port())] + args
+    else:
+        cmd = [sys.executable] + args
+    t0 = time.monotonic()
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240, env=env)
+    took = time.monotonic() - t0
+    assert r.returncode != 0
+    assert took < 150, took
+    d = _last_json(r.stdout)
+    assert KEYS <= set(d)
+    assert d["value"] is None and d["status"] == "timeout" and d["deadline_s"] == 25
+    assert d["phase"] == "warm-up"  # rank 0 waits for rank 1 in the barrier after it
+    # the tuning rows finished before the stall are in the record
+    assert len(d["data_path_tuning"]) == 1 and d["data_path_tuning"][0]["ok"]
 
 
 def test_spawn_local_fail_fast(tmp_path):
