@@ -12,6 +12,10 @@
 //   ipc_system_stores 0 (default); 1: the IPC pack stores every peer-bound message with system
 //                   coherence, as it always does for a peer on another GPU (tests of that path
 //                   on one GPU).
+//   cpu_ftz         1 (default): the CPU solver flushes fp32 denormals in its step region
+//                   (MXCSR FTZ + DAZ; ~100x faster where the reference example's v field
+//                   passes through them); 0: IEEE denormals, the reference's and the GPU's
+//                   fp32 behaviour bit for bit (exact-parity runs).  fp64 never flushes.
 #pragma once
 
 #include <string.h>
@@ -23,6 +27,7 @@ struct DebugKnobs {
   int philox_generic = 0;
   double ipc_emulate_us = 0.0;
   int ipc_system_stores = 0;
+  int cpu_ftz = 1;
 };
 
 inline DebugKnobs& debug_knobs() {
@@ -38,6 +43,7 @@ inline int debug_set(const char* name, double value) {
   else if (!strcmp(name, "philox_generic")) k.philox_generic = value != 0.0 ? 1 : 0;
   else if (!strcmp(name, "ipc_emulate_us")) k.ipc_emulate_us = value > 0.0 ? value : 0.0;
   else if (!strcmp(name, "ipc_system_stores")) k.ipc_system_stores = value != 0.0 ? 1 : 0;
+  else if (!strcmp(name, "cpu_ftz")) k.cpu_ftz = value != 0.0 ? 1 : 0;
   else return -1;
   return 0;
 }

@@ -43,6 +43,9 @@ from ..parallel.dist import DistContext
 from .bp4 import BP4Writer
 
 _NP = {"float32": np.float32, "float64": np.float64}
+# pinned (page-locked) host memory the asynchronous output ring may hold per rank: the queue
+# depth is cut to what fits (a 512^3 fp32 rank's 1 GiB snapshot: one step in flight)
+PINNED_RING_BYTES = 1 << 30
 
 
 def vtk_schema(L) -> str:
@@ -168,7 +171,10 @@ class SimulationOutput:
             self.write_fields(step, u, v)
             self.last_step = step
             return None
-        depth = self.queue if _snapshot_bytes(sim) <= (1 << 30) else 1
+        # the ring of pinned host snapshots is bounded in bytes, not in steps: at most
+        # PINNED_RING_BYTES per rank (queue x snapshot), so an 8-rank node pins <= 8 GiB for
+        # output whatever the sub-domain size (one step in flight beyond that)
+        depth = max(1, min(self.queue, PINNED_RING_BYTES // max(1, _snapshot_bytes(sim))))
         while len(self._pending) >= depth:
             self._commit_oldest()
         snap = sim.snapshot_fields("output", depth=depth)

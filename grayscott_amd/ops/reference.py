@@ -246,13 +246,20 @@ def noise_torch(L, step: int, seed: int, dtype=None, device="cpu"):
 
 def run_torch(L, nsteps: int, F=0.02, k=0.048, dt=1.0, Du=0.2, Dv=0.1, noise_amp=0.0, seed=0,
               dtype=None, device="cpu", init_seed=None, init_lo=0.0, init_hi=1.0, u0=None,
-              v0=None):
+              v0=None, arith: str = "storage"):
     """``run`` as device-resident PyTorch (non-periodic reference boundary): from
-    the reference init, the benchmarks' random init (``init_seed``) or given (u0, v0); every
-    operation in ``dtype`` (default float32).  Returns (u, v) tensors on ``device``."""
+    the reference init, the benchmarks' random init (``init_seed``) or given (u0, v0).
+
+    ``arith``: "storage" -- every operation in ``dtype`` (default float32); "julia" -- the
+    reference's own Float32 arithmetic (``_step_julia``): Float32 storage, but the Laplacian,
+    ``F * (1.0 - u)``, the noise term and the Euler update in Float64 (the Float64 literals
+    promote them), the neighbour sum, ``u * v^2`` and ``(F + k) * v`` in Float32, rounded to
+    Float32 on store.  Returns (u, v) tensors on ``device``."""
     import torch
     import torch.nn.functional as Fn
     dtype = dtype or torch.float32
+    if arith not in ("storage", "julia"):
+        raise ValueError(f"arith must be storage | julia, not {arith!r}")
     if isinstance(L, int):
         L = (L, L, L)
     if u0 is not None:
@@ -268,6 +275,10 @@ def run_torch(L, nsteps: int, F=0.02, k=0.048, dt=1.0, Du=0.2, Dv=0.1, noise_amp
         return ((p[1:-1, 1:-1, :-2] + p[1:-1, 1:-1, 2:]) + (p[1:-1, :-2, 1:-1] + p[1:-1, 2:, 1:-1])
                 + (p[:-2, 1:-1, 1:-1] + p[2:, 1:-1, 1:-1]))
 
+    if arith == "julia":
+        for t in range(nsteps):
+            u, v = _step_julia(u, v, t, F, k, dt, Du, Dv, noise_amp, seed, L)
+        return u, v
     for t in range(nsteps):
         su = nsum(Fn.pad(u, (1, 1, 1, 1, 1, 1), mode="constant", value=bc_u(t)))
         sv = nsum(Fn.pad(v, (1, 1, 1, 1, 1, 1), mode="constant", value=0.0))
@@ -278,3 +289,44 @@ def run_torch(L, nsteps: int, F=0.02, k=0.048, dt=1.0, Du=0.2, Dv=0.1, noise_amp
         dv = (Dv / 6.0) * sv - Dv * v + uvv - (F + k) * v
         u, v = u + du * dt, v + dv * dt
     return u, v
+
+
+def _step_julia(u, v, t, F, k, dt, Du, Dv, noise_amp, seed, L):
+    """One step with the reference's mixed precision for T = Float32, evaluated in Julia's
+    order (src/simulation/Simulation_CPU.jl:82-109, Common.jl:13-18):
+
+      params       Du, Dv, F, K, noise, dt = convert(Float32, ...)              (:82-87)
+      laplacian    l = x[i-1] + x[i+1] + x[j-1] + x[j+1] + x[k-1] + x[k+1]       Float32, left
+                       - 6.0 * x[i,j,k]                                           to right, then
+                   l / 6.0                                                        Float64
+      du = Du * lap_u - u * v^2 + F * (1.0 - u) + noise * rand(Uniform(-1, 1))  Float64
+                   (u * v^2 is Float32: v^2 = v * v, then u * that)
+      dv = Dv * lap_v + u * v^2 - (F + K) * v                                    Float64
+                   ((F + K) * v is Float32)
+      u_temp = u + du * dt ; v_temp = v + dv * dt                                Float64, stored
+                                                                                 as Float32
+    The uniform draw is this framework's Philox stream (the reference's ``rand`` is not
+    reproducible), exact in Float64.  ``u``, ``v``: float32 tensors; returns float32 tensors."""
+    import torch
+    import torch.nn.functional as Fn
+    f32 = np.float32
+    Du32, Dv32, F32, K32 = float(f32(Du)), float(f32(Dv)), float(f32(F)), float(f32(k))
+    n32, dt32 = float(f32(noise_amp)), float(f32(dt))
+    FK32 = float(f32(F32) + f32(K32))  # F + K in Float32
+
+    def lap(x, bc):
+        p = Fn.pad(x, (1, 1, 1, 1, 1, 1), mode="constant", value=bc)
+        s = p[1:-1, 1:-1, :-2] + p[1:-1, 1:-1, 2:]      # Float32, Julia's left-to-right order
+        s = s + p[1:-1, :-2, 1:-1]
+        s = s + p[1:-1, 2:, 1:-1]
+        s = s + p[:-2, 1:-1, 1:-1]
+        s = s + p[2:, 1:-1, 1:-1]
+        return (s.double() - 6.0 * x.double()) / 6.0     # promoted by the 6.0 literals
+
+    lu, lv = lap(u, bc_u(t)), lap(v, 0.0)
+    uvv = (u * (v * v)).double()                         # u * v^2 in Float32
+    du = Du32 * lu - uvv + F32 * (1.0 - u.double())
+    if noise_amp != 0:
+        du = du + n32 * noise_torch(L, t, seed, torch.float64, u.device)
+    dv = Dv32 * lv + uvv - (FK32 * v).double()           # (F + K) * v in Float32
+    return (u.double() + du * dt32).float(), (v.double() + dv * dt32).float()

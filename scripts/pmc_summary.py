@@ -7,25 +7,46 @@ import sys
 from collections import defaultdict
 
 
+def _key(name: str) -> str:
+    """Kernel name without its parameter list (the template arguments are kept: they tell the
+    fused kernel's configurations apart)."""
+    name = name.strip()
+    if name.startswith("void "):
+        name = name[5:]
+    depth = 0
+    for i, ch in enumerate(name):
+        if ch == "<":
+            depth += 1
+        elif ch == ">":
+            depth -= 1
+        elif ch == "(" and depth == 0:
+            return name[:i]
+    return name
+
+
 def main(root):
     acc = defaultdict(lambda: defaultdict(float))
+    vals = defaultdict(lambda: defaultdict(list))
     cnt = defaultdict(lambda: defaultdict(int))
     for f in glob.glob(os.path.join(root, "g*", "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                k = row["Kernel_Name"].split("(")[0][:70]
+                k = _key(row["Kernel_Name"])
                 acc[k][row["Counter_Name"]] += float(row["Counter_Value"])
                 cnt[k][row["Counter_Name"]] += 1
+                vals[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
     durs = defaultdict(list)
     for f in glob.glob(os.path.join(root, "stats", "**", "*kernel_stats.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                durs[row["Name"].split("(")[0][:70]] = [int(row["Calls"]), float(row["AverageNs"])]
+                durs[_key(row["Name"])] = [int(row["Calls"]), float(row["AverageNs"])]
     for k, d in acc.items():
         print(f"== {k}  calls/avg_ns={durs.get(k)}")
         for c in sorted(d):
             n = max(1, cnt[k][c])
-            print(f"   {c:28s} per-dispatch {d[c] / n * (1 if 'SQ_' not in c else 1):.4g}")
+            v = sorted(vals[k][c])
+            med = v[len(v) // 2] if v else 0.0
+            print(f"   {c:28s} per-dispatch mean {d[c] / n:.4g}  median {med:.4g}  (n={n})")
 
 
 if __name__ == "__main__":

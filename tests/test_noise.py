@@ -107,3 +107,26 @@ def test_cpu_step_flushes_denormals_but_restores_the_callers_fp_mode():
     assert not ((v1 != 0) & (np.abs(v1) < tiny)).any()  # no denormal survives the step
     d = np.float32(1e-39)
     assert d != 0 and d * np.float32(1.0) == d  # the main thread still computes denormals
+
+
+def test_cpu_ftz_knob_keeps_ieee_denormals(debug_knob):
+    """Debug knob cpu_ftz = 0: the CPU solver keeps IEEE denormals (the reference's and the
+    GPU's fp32 behaviour) for exact-parity runs; fp64 never flushes."""
+    from grayscott_amd.models.grayscott import GrayScott
+    from grayscott_amd.parallel.decomp import init_domain
+    from grayscott_amd.utils.config import Settings
+
+    tiny = {"Float32": np.finfo(np.float32).tiny, "Float64": np.finfo(np.float64).tiny}
+    for prec, knob in (("Float32", 0), ("Float64", 1)):
+        debug_knob("cpu_ftz", knob, "core")
+        dt = np.float32 if prec == "Float32" else np.float64
+        s = Settings(L=12, precision=prec, noise=0.0, F=0.02, k=0.048, dt=1.0, Du=0.2, Dv=0.1,
+                     backend="CPU")
+        sim = GrayScott(s, init_domain(12, 1, 0))
+        sim.init_fields()
+        sim.set_fields(np.full(sim.local_shape, 0.5, dt),
+                       np.full(sim.local_shape, 4 * tiny[prec] / 2 ** 10, dt))  # denormal v
+        sim.iterate(1)
+        _, v1 = sim.get_fields()
+        sim.close()
+        assert ((v1 != 0) & (np.abs(v1) < tiny[prec])).any(), prec  # denormals survive

@@ -41,3 +41,16 @@ def test_torch_run_matches_numpy_run():
     d = ref.run(L, 5, noise_amp=0.0, dtype=np.float64)
     e = ref.run_torch(L, 5, noise_amp=0.0, dtype=torch.float64)
     assert np.abs(d[0] - e[0].numpy()).max() < 1e-13
+
+
+def test_julia_semantics_oracle_sits_between_fp32_and_fp64():
+    """The reference's mixed Float32 arithmetic (run_torch arith="julia") is closer to a
+    Float64 run than the all-Float32 oracle is, and differs from it by rounding only."""
+    a = ref.run_torch(24, 40, noise_amp=0.1, seed=9, arith="julia")
+    b = ref.run_torch(24, 40, noise_amp=0.1, seed=9)
+    c = ref.run(24, 40, noise_amp=0.1, seed=9, dtype=np.float64)
+    dj = max(float(np.abs(x.numpy() - y).max()) for x, y in zip(a, c))
+    df = max(float(np.abs(x.numpy() - y).max()) for x, y in zip(b, c))
+    assert a[0].dtype == torch.float32
+    assert dj < df < 1e-5
+    assert 0 < max(float((x - y).abs().max()) for x, y in zip(a, b)) < 1e-5
