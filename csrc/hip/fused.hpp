@@ -315,7 +315,7 @@ constexpr int gs_gcd(int a, int b) { return b == 0 ? a : gs_gcd(b, a % b); }
 constexpr int gs_lcm(int a, int b) { return a / gs_gcd(a, b) * b; }
 
 template <typename T_, int TL_, int ROWS_, int WAVES_, int PF_, bool PERIODIC_, bool NOISE_,
-          bool SKEW_ = false, bool Q32_ = true, int ABL_ = 0, bool FOLD_ = false>
+          bool SKEW_ = false, bool Q32_ = true, int ABL_ = 0, bool FOLD_ = false, int OPT_ = 0>
 struct FCfg {
   using T = T_;
   using V2 = typename PairT<T>::type;
@@ -325,6 +325,27 @@ struct FCfg {
   // the last x strip folded into half-wave tiles (FusedArgs::ntxf ..): non-periodic, 32-bit
   // noise counter (its lane part absorbs the upper half's y offset)
   static constexpr bool FOLD = FOLD_;
+  // fp64 x-neighbour pair sums through LDS instead of DPP: the DP ALU has no wave-shift DPP (only
+  // row_newbcast), so a lane shift of a double is two 32-bit v_mov_b32_dpp -- eight VALU per
+  // cell-level for the (u, v) pair's two neighbours.  With LX each wave stores its rows once per
+  // level (ds_write_b128) and reads both neighbours back (2 x ds_read_b128): LDS instructions
+  // instead of VALU, latency hidden by the plane pipeline (the sums feed the next plane's partial
+  // sum).  Same association, (left + right) + s, and the padding lanes read 0 like bound_ctrl:
+  // bit-identical.  Candidate "<shape>x" of the fp64 autotuner.
+  static constexpr bool LX = (OPT_ & 1) != 0;
+  static_assert(!LX || sizeof(T_) == 8, "LDS x-sums are for fp64 (fp32 fuses the DPP into the add)");
+  // Neighbour-only synchronisation of the skewed pipeline's LDS row exchange (OPT bit 1) instead
+  // of one workgroup barrier per plane: a wave reads only its up / down partner's rows, so after
+  // publishing its own rows it bumps its LDS sequence word and waits until both partners' words
+  // reach the same iteration.  The waves of a workgroup drift by up to an iteration per
+  // neighbour instead of meeting at one s_barrier (whose wait lines up every wave's stalls).
+  // RAW: a partner's rows of iteration i are written before its word reaches i (one wave's LDS
+  // instructions execute in order); WAR: slot i % 2 is rewritten at i + 2, after the partner has
+  // published i + 1, i.e. finished its reads of i.  The wrap-around partners (wave 0's up, the
+  // last wave's down) exchange tile-halo rows that never reach an output, so they are not waited
+  // for.  Bit-identical.
+  static constexpr bool NSYNC = (OPT_ & 2) != 0;
+  static_assert(!NSYNC || SKEW_, "neighbour sync replaces the skewed pipeline's single barrier");
   static_assert(!FOLD_ || (Q32_ && !PERIODIC_ && ROWS_ == 4),
                 "folded strips need Q32, a non-periodic grid and 4-row waves");
   static constexpr int R = PF + 2;                    // level-0 ring slots
@@ -408,6 +429,10 @@ struct FusedSeg {
   uint32_t gx32;             // Q32 noise counter: lane part
   int gdy;                   // folded tile: this lane's y offset from gy0 (0 or ystep)
   bool edge;
+  void* xl;                  // FCfg::LX: this wave's LDS rows (ROWS x 66 pairs, pads 0 / 65 zero)
+  int* seq;                  // FCfg::NSYNC: the workgroup's per-wave sequence words (LDS)
+  int it;                    // FCfg::NSYNC: pipeline iterations run by this workgroup so far
+  bool wait_up, wait_dn;     // FCfg::NSYNC: whether this wave waits for its up / down partner
 };
 
 template <class C>
@@ -466,13 +491,30 @@ __device__ __forceinline__ typename C::V2 cell_update(typename C::V2& A, typenam
                                                       typename C::V2 c, typename C::V2 ym,
                                                       typename C::V2 yp, const FoldCoef<typename C::T>& f,
                                                       typename C::T ar31, typename C::V2 kc,
-                                                      uint32_t w) {
+                                                      uint32_t w, typename C::V2 xs = {}) {
   using T = typename C::T;
   using V2 = typename C::V2;
   const V2 s = A + in;
   const V2 yz = (ym + yp) + c;
   constexpr bool nop = (C::ABL & 8) != 0;
-  A = V2{lane_pair_sum_add<nop>(in.x, yz.x), lane_pair_sum_add<nop>(in.y, yz.y)};
+  if constexpr (C::LX) A = V2{xs.x + yz.x, xs.y + yz.y};  // xs = left + right (LDS, FCfg::LX)
+  else A = V2{lane_pair_sum_add<nop>(in.x, yz.x), lane_pair_sum_add<nop>(in.y, yz.y)};
+  if constexpr (sizeof(T) == 8) {
+    // fp64 has no packed arithmetic: the vector form below would compute uvv twice (4 v_mul_f64)
+    // and, with kc in VGPRs as the first FMA's accumulator, copy it first (v_mov_b64 + v_fmac).
+    // The same expression tree, scalarised: uvv = (cu cv) cv once; v's first term is dt uvv
+    // (kc.y = 0: fma(dt, uvv, 0) rounds like the product); three-operand FMAs.  Bit-identical.
+    const T uvv = (c.x * c.y) * c.y;
+    V2 P;
+    P.x = __builtin_fma(f.kd.x, uvv, kc.x);
+    P.y = f.kd.y * uvv;
+    P.x = __builtin_fma(f.ks.x, s.x, P.x);
+    P.y = __builtin_fma(f.ks.y, s.y, P.y);
+    P.x = __builtin_fma(f.kcc.x, c.x, P.x);
+    P.y = __builtin_fma(f.kcc.y, c.y, P.y);
+    if constexpr (C::NOISE) P.x = __builtin_fma(ar31, (T)(int32_t)w, P.x);
+    return P;
+  }
   // uvv in both halves: (cu cv, cv cv) then (cu cv cv, cu cv cv)
   const V2 t = c * c.yy;
   const V2 uvv = t.xx * c.yy;
@@ -528,7 +570,25 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
       xch[l][IS][sg.wave][0][sg.lane] = in[0];
       xch[l][IS][sg.wave][1][sg.lane] = in[ROWS - 1];
     }
-    if constexpr (!(C::ABL & 1)) __syncthreads();
+    if constexpr (C::NSYNC) {
+      // publish this iteration's rows, then wait for the partners' (see FCfg::NSYNC)
+      const int it = ++sg.it;
+      asm volatile("" ::: "memory");
+      __hip_atomic_store(&sg.seq[sg.wave], it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      // bounded: a scheduling bug must end in wrong numbers (caught by the bitwise tests), never
+      // in a wave that spins forever
+      for (int spins = 0; spins < (1 << 22); ++spins) {
+        const int a = sg.wait_up ? __hip_atomic_load(&sg.seq[sg.wup], __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_WORKGROUP) : it;
+        const int b = sg.wait_dn ? __hip_atomic_load(&sg.seq[sg.wdn], __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_WORKGROUP) : it;
+        if (a >= it && b >= it) break;
+        __builtin_amdgcn_s_sleep(0);
+      }
+      asm volatile("" ::: "memory");
+    } else if constexpr (!(C::ABL & 1)) {
+      __syncthreads();
+    }
   }
 #pragma unroll
   for (int li = 0; li < TL; ++li) {
@@ -566,6 +626,14 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
     if (need && !((sg.skip >> l) & 1)) {  // wave-uniform
       const V2 up = lds_load2(&xch[l][IS][sg.wup][1][sg.lane]);
       const V2 dn = lds_load2(&xch[l][IS][sg.wdn][0][sg.lane]);
+      V2* xl = (V2*)sg.xl;
+      if constexpr (C::LX) {
+        // this wave's input rows out to LDS and the x neighbours back (one wave: LDS executes
+        // its instructions in order, so no barrier; the asm keeps the compiler's order)
+#pragma unroll
+        for (int j = 0; j < ROWS; ++j) xl[j * 66 + sg.lane + 1] = in[j];
+        asm volatile("" ::: "memory");
+      }
       const int64_t gz = gwrap<C>(g.oz + q, g.Lz);
       const uint64_t tstep = (uint64_t)(a.t + l);
       V2 res[ROWS];
@@ -604,9 +672,15 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
           const V2 ym = j == 0 ? up : in[j - 1];
           const V2 yp = j == ROWS - 1 ? dn : in[j + 1];
           const uint32_t w = k == 0 ? blk.x : (k == 1 ? blk.y : (k == 2 ? blk.z : blk.w));
-          res[j] = cell_update<C>(S.A[l][j], in[j], Cc[j], ym, yp, f, S.ar31, S.kc, w);
+          V2 xs{};
+          if constexpr (C::LX) {
+            const V2 xa = xl[j * 66 + sg.lane], xb = xl[j * 66 + sg.lane + 2];
+            xs = V2{xa.x + xb.x, xa.y + xb.y};
+          }
+          res[j] = cell_update<C>(S.A[l][j], in[j], Cc[j], ym, yp, f, S.ar31, S.kc, w, xs);
         }
       }
+      if constexpr (C::LX) asm volatile("" ::: "memory");
       if (l + 1 < TL) {
         if (sg.edge) {
           const T bu = (T)gs::bc_u(a.t + l + 1);
@@ -659,10 +733,29 @@ __global__ __launch_bounds__(64 * C::WAVES, C::WPEU) void k_fused(const typename
   constexpr int ROWS = C::ROWS, WAVES = C::WAVES, TL = C::TL;
   static_assert(ROWS % 4 == 0, "rows per wave must hold whole noise quads");
   __shared__ typename C::V2 xch[TL][C::NS][WAVES][2][64];  // [level][ring][wave][row][lane]
+  __shared__ typename C::V2 xrow[C::LX ? WAVES * ROWS * 66 : 1];  // FCfg::LX rows, 1-lane pads
   const Geom& g = a.g;
   FusedSeg sg;
   sg.lane = threadIdx.x & 63;
   sg.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  sg.xl = nullptr;
+  __shared__ int seqw[C::NSYNC ? WAVES : 1];
+  sg.seq = seqw;
+  sg.it = 0;
+  sg.wait_up = sg.wave > 0;
+  sg.wait_dn = sg.wave < WAVES - 1;
+  if constexpr (C::NSYNC) {
+    if (sg.lane == 0) seqw[sg.wave] = 0;
+    __syncthreads();  // once: every word initialised before any wave polls
+  }
+  if constexpr (C::LX) {
+    typename C::V2* w = xrow + sg.wave * ROWS * 66;
+    if (sg.lane < ROWS) {  // the pads read by lanes 0 / 63: 0, as DPP's bound_ctrl gives
+      w[sg.lane * 66] = typename C::V2{(T)0, (T)0};
+      w[sg.lane * 66 + 65] = typename C::V2{(T)0, (T)0};
+    }
+    sg.xl = w;
+  }
   sg.wup = sg.wave == 0 ? WAVES - 1 : sg.wave - 1;
   sg.wdn = sg.wave == WAVES - 1 ? 0 : sg.wave + 1;
   sg.skip = 0;
@@ -996,38 +1089,47 @@ inline const FusedCfgEntry* fused_cfg_table(int* n) {
       {"blk8x2w16l", true, false}, // 25  last level in half-quad items
       {"blk4x4w16l", true, false}, // 26  last level in half-quad items
       {"4x12:1sf", true, false},   // 27  the last x strip folded into half-wave tiles (FCfg::FOLD)
+      {"4x8:1sx", false, true},    // 28  fp64: x-neighbour sums through LDS (FCfg::LX)
+      {"4x6:2sx", false, true},    // 29  fp64: x-neighbour sums through LDS (FCfg::LX)
+      {"4x8:1x", false, true},     // 30  fp64: x-neighbour sums through LDS, unskewed
+      {"4x12:1sn", true, false},   // 31  neighbour-only LDS sync instead of the barrier (NSYNC)
+      {"4x12:1sfn", true, false},  // 32  folded last strip + neighbour-only sync
+      {"4x12:2sn", true, false},   // 33  2-plane prefetch + neighbour-only sync
+      {"4x8:1sxn", false, true},   // 34  fp64: LDS x-sums + neighbour-only sync
+      {"4x8:1sn", false, true},    // 35  fp64: neighbour-only sync
 #ifdef GS_ABLATION
-      {"4x12:2s-abl1", true, false},  // 28  no barriers
-      {"4x12:2s-abl2", true, false},  // 29  L2-resident loads
-      {"4x12:1s-abl4", true, false},  // 30  Philox keys in VGPRs (exact)
-      {"4x12:2s-abl4", true, false},  // 31  Philox keys in VGPRs (exact)
-      {"4x12:1s-abl8", true, false},  // 32  DPP sums with the s_nop (exact)
-      {"4x12:1s-abl12", true, false}, // 33  abl4 + abl8 (exact)
-      {"4x12:1s-abl16", true, false}, // 34  pipeline fill computes every level (exact)
-      {"4x8:1s-abl16", true, true},   // 35  pipeline fill computes every level (exact)
-      {"4x6:2s-abl16", true, true},   // 36  pipeline fill computes every level (exact)
-      {"4x12:1s-abl32", true, false}, // 37  Philox only on lanes in the x cone (exact)
-      {"4x12:2s-abl64", true, false}, // 38  Philox keys rebuilt on the SALU (exact)
-      {"4x12:1s-abl64", true, false}, // 39  Philox keys rebuilt on the SALU (exact)
-      {"4x12:1s-abl256", true, false}, // 40  step-uniform Philox words on the SALU (exact)
-      {"4x12:1s-abl512", true, false}, // 41  Philox blocks of all levels before the barrier (exact)
-      {"4x12:1s-abl1024", true, false}, // 42  the top level's Philox block before the barrier (exact)
-      {"4x12:1s-abl1536", true, false}, // 43  the top two levels' Philox blocks before the barrier
-      {"4x12:1s-abl2048", true, false}, // 44  non-temporal output stores (exact)
-      {"4x12:1s-abl4096", true, false}, // 45  device-scope (write-through) output stores (exact)
-      {"4x12:1s-abl6144", true, false}, // 46  both (exact)
+      {"4x12:2s-abl1", true, false},  // 36  no barriers
+      {"4x12:2s-abl2", true, false},  // 37  L2-resident loads
+      {"4x12:1s-abl4", true, false},  // 38  Philox keys in VGPRs (exact)
+      {"4x12:2s-abl4", true, false},  // 39  Philox keys in VGPRs (exact)
+      {"4x12:1s-abl8", true, false},  // 40  DPP sums with the s_nop (exact)
+      {"4x12:1s-abl12", true, false}, // 41  abl4 + abl8 (exact)
+      {"4x12:1s-abl16", true, false}, // 42  pipeline fill computes every level (exact)
+      {"4x8:1s-abl16", true, true},   // 43  pipeline fill computes every level (exact)
+      {"4x6:2s-abl16", true, true},   // 44  pipeline fill computes every level (exact)
+      {"4x12:1s-abl32", true, false}, // 45  Philox only on lanes in the x cone (exact)
+      {"4x12:2s-abl64", true, false}, // 46  Philox keys rebuilt on the SALU (exact)
+      {"4x12:1s-abl64", true, false}, // 47  Philox keys rebuilt on the SALU (exact)
+      {"4x12:1s-abl256", true, false}, // 48  step-uniform Philox words on the SALU (exact)
+      {"4x12:1s-abl512", true, false}, // 49  Philox blocks of all levels before the barrier (exact)
+      {"4x12:1s-abl1024", true, false}, // 50  the top level's Philox block before the barrier (exact)
+      {"4x12:1s-abl1536", true, false}, // 51  the top two levels' Philox blocks before the barrier
+      {"4x12:1s-abl2048", true, false}, // 52  non-temporal output stores (exact)
+      {"4x12:1s-abl4096", true, false}, // 53  device-scope (write-through) output stores (exact)
+      {"4x12:1s-abl6144", true, false}, // 54  both (exact)
 #endif
   };
   *n = (int)(sizeof(t) / sizeof(t[0]));
   return t;
 }
 
-// whether a config is worth timing for a launch of k steps over g: the folded-strip tile
-// (FCfg::FOLD) equals 4x12:1s unless the last x strip fits half a wave
+// whether a config is worth timing for a launch of k steps over g: the folded-strip tiles
+// (FCfg::FOLD) equal their unfolded shapes unless the last x strip fits half a wave
 inline bool fused_cfg_applies(int i, const Geom& g, int k) {
   int n = 0;
   const FusedCfgEntry* t = fused_cfg_table(&n);
-  if (i < 0 || i >= n || strcmp(t[i].name, "4x12:1sf") != 0) return true;
+  if (i < 0 || i >= n || (strcmp(t[i].name, "4x12:1sf") != 0 && strcmp(t[i].name, "4x12:1sfn") != 0))
+    return true;
   const int xstep = 64 - 2 * k;
   const int ntx = (g.nx + xstep - 1) / xstep;
   return ntx >= 2 && g.nx - (ntx - 1) * xstep <= 32 - 2 * k;
@@ -1093,9 +1195,14 @@ void run_fused_cfg(const void* s, void* d, const FusedArgs& a, const gs::Params&
       case 15: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true>, T>::run(s, d, a, p, st); return;
       case 16: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
       case 17: FusedLaunch<FCfg<T, TL, 4, 4, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
+      case 28: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 0, false, 1>, T>::run(s, d, a, p, st); return;
+      case 29: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 0, false, 1>, T>::run(s, d, a, p, st); return;
+      case 30: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, false, true, 0, false, 1>, T>::run(s, d, a, p, st); return;
+      case 34: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 0, false, 3>, T>::run(s, d, a, p, st); return;
+      case 35: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 0, false, 2>, T>::run(s, d, a, p, st); return;
 #ifdef GS_ABLATION
-      case 35: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
-      case 36: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 43: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 44: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
 #endif
       default: break;
     }
@@ -1126,26 +1233,29 @@ void run_fused_cfg(const void* s, void* d, const FusedArgs& a, const gs::Params&
       case 25: if (block_supported(a) && run_block<BCfg<T, TL, 8, 2, 16, NZ, true, true>>(s, d, a, p, st)) return; break;
       case 26: if (block_supported(a) && run_block<BCfg<T, TL, 4, 4, 16, NZ, true, true>>(s, d, a, p, st)) return; break;
       case 27: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 0, true>, T>::run(s, d, a, p, st); return;
+      case 31: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 0, false, 2>, T>::run(s, d, a, p, st); return;
+      case 32: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 0, true, 2>, T>::run(s, d, a, p, st); return;
+      case 33: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 0, false, 2>, T>::run(s, d, a, p, st); return;
 #ifdef GS_ABLATION
-      case 28: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 1>, T>::run(s, d, a, p, st); return;
-      case 29: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 2>, T>::run(s, d, a, p, st); return;
-      case 30: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;
-      case 31: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;
-      case 32: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 8>, T>::run(s, d, a, p, st); return;
-      case 33: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 12>, T>::run(s, d, a, p, st); return;
-      case 34: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
-      case 35: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
-      case 36: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
-      case 37: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 32>, T>::run(s, d, a, p, st); return;
-      case 38: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 64>, T>::run(s, d, a, p, st); return;
-      case 39: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 64>, T>::run(s, d, a, p, st); return;
-      case 40: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 256>, T>::run(s, d, a, p, st); return;
-      case 41: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 512>, T>::run(s, d, a, p, st); return;
-      case 42: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 1024>, T>::run(s, d, a, p, st); return;
-      case 43: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 1536>, T>::run(s, d, a, p, st); return;
-      case 44: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 2048>, T>::run(s, d, a, p, st); return;
-      case 45: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 4096>, T>::run(s, d, a, p, st); return;
-      case 46: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 6144>, T>::run(s, d, a, p, st); return;
+      case 36: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 1>, T>::run(s, d, a, p, st); return;
+      case 37: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 2>, T>::run(s, d, a, p, st); return;
+      case 38: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;
+      case 39: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;
+      case 40: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 8>, T>::run(s, d, a, p, st); return;
+      case 41: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 12>, T>::run(s, d, a, p, st); return;
+      case 42: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 43: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 44: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 45: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 32>, T>::run(s, d, a, p, st); return;
+      case 46: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 64>, T>::run(s, d, a, p, st); return;
+      case 47: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 64>, T>::run(s, d, a, p, st); return;
+      case 48: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 256>, T>::run(s, d, a, p, st); return;
+      case 49: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 512>, T>::run(s, d, a, p, st); return;
+      case 50: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 1024>, T>::run(s, d, a, p, st); return;
+      case 51: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 1536>, T>::run(s, d, a, p, st); return;
+      case 52: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 2048>, T>::run(s, d, a, p, st); return;
+      case 53: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 4096>, T>::run(s, d, a, p, st); return;
+      case 54: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 6144>, T>::run(s, d, a, p, st); return;
 #endif
       default: break;  // 0 and 14: the default shape below
     }

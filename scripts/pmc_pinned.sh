@@ -17,6 +17,8 @@ c = fk[max(fk, key=int)]
 print(c["tile"] if c["tile"] != "default" else "-", c["sched"])
 PY
 ) || exit 1
+# PIN_TILE / PIN_SCHED override the bench's choice (A/B counter sets of two tiles)
+tile=${PIN_TILE:-$tile}; sched=${PIN_SCHED:-$sched}
 if [ "$tile" != "-" ]; then export GS_FUSED_CFG=$tile; fi
 export GS_FUSED_SCHED=$sched GS_AUTOTUNE=0
 echo "pinned tile=$tile sched=$sched" | tee "$out/pinned.txt"
