@@ -1089,6 +1089,10 @@ inline const FusedCfgEntry* fused_cfg_table(int* n) {
       {"blk8x2w16l", true, false}, // 25  last level in half-quad items
       {"blk4x4w16l", true, false}, // 26  last level in half-quad items
       {"4x12:1sf", true, false},   // 27  the last x strip folded into half-wave tiles (FCfg::FOLD)
+#ifdef GS_ABLATION
+      // measured and rejected in round 5 (exact; kept for reproduction in the ablation build):
+      // fp64 LDS x-sums 4-6 % slower, neighbour-only sync 5-6 % slower (profiles/r5_f64_counters.txt,
+      // r5_nsync_rejected.txt)
       {"4x8:1sx", false, true},    // 28  fp64: x-neighbour sums through LDS (FCfg::LX)
       {"4x6:2sx", false, true},    // 29  fp64: x-neighbour sums through LDS (FCfg::LX)
       {"4x8:1x", false, true},     // 30  fp64: x-neighbour sums through LDS, unskewed
@@ -1097,7 +1101,6 @@ inline const FusedCfgEntry* fused_cfg_table(int* n) {
       {"4x12:2sn", true, false},   // 33  2-plane prefetch + neighbour-only sync
       {"4x8:1sxn", false, true},   // 34  fp64: LDS x-sums + neighbour-only sync
       {"4x8:1sn", false, true},    // 35  fp64: neighbour-only sync
-#ifdef GS_ABLATION
       {"4x12:2s-abl1", true, false},  // 36  no barriers
       {"4x12:2s-abl2", true, false},  // 37  L2-resident loads
       {"4x12:1s-abl4", true, false},  // 38  Philox keys in VGPRs (exact)
@@ -1195,12 +1198,12 @@ void run_fused_cfg(const void* s, void* d, const FusedArgs& a, const gs::Params&
       case 15: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true>, T>::run(s, d, a, p, st); return;
       case 16: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
       case 17: FusedLaunch<FCfg<T, TL, 4, 4, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
+#ifdef GS_ABLATION
       case 28: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 0, false, 1>, T>::run(s, d, a, p, st); return;
       case 29: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 0, false, 1>, T>::run(s, d, a, p, st); return;
       case 30: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, false, true, 0, false, 1>, T>::run(s, d, a, p, st); return;
       case 34: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 0, false, 3>, T>::run(s, d, a, p, st); return;
       case 35: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 0, false, 2>, T>::run(s, d, a, p, st); return;
-#ifdef GS_ABLATION
       case 43: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
       case 44: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
 #endif
@@ -1233,10 +1236,10 @@ void run_fused_cfg(const void* s, void* d, const FusedArgs& a, const gs::Params&
       case 25: if (block_supported(a) && run_block<BCfg<T, TL, 8, 2, 16, NZ, true, true>>(s, d, a, p, st)) return; break;
       case 26: if (block_supported(a) && run_block<BCfg<T, TL, 4, 4, 16, NZ, true, true>>(s, d, a, p, st)) return; break;
       case 27: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 0, true>, T>::run(s, d, a, p, st); return;
+#ifdef GS_ABLATION
       case 31: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 0, false, 2>, T>::run(s, d, a, p, st); return;
       case 32: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 0, true, 2>, T>::run(s, d, a, p, st); return;
       case 33: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 0, false, 2>, T>::run(s, d, a, p, st); return;
-#ifdef GS_ABLATION
       case 36: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 1>, T>::run(s, d, a, p, st); return;
       case 37: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 2>, T>::run(s, d, a, p, st); return;
       case 38: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;

@@ -119,20 +119,3 @@ def test_production_library_rejects_ablation_variants():
     with pytest.raises(ValueError):
         native.fused_select("4x12:2s-abl1")
 
-
-@pytest.mark.parametrize("cfg,plain,L,fuse,sched", [
-    ("4x12:1sn", "4x12:1s", 512, 3, 1), ("4x12:1sn", "4x12:1s", 256, 3, 2),
-    ("4x12:1sfn", "4x12:1sf", 256, 3, 1), ("4x12:2sn", "4x12:2s", 512, 3, 2),
-    ("4x12:1sn", "4x12:1s", 128, 2, 0)])
-def test_neighbour_sync_bitwise_vs_barrier(cfg, plain, L, fuse, sched):
-    """FCfg::NSYNC (fused.hpp): each wave waits only for its up / down partner's LDS rows
-    instead of the workgroup barrier.  Against the golden model, and bit for bit against the
-    same tile with the barrier, random init, schedules 0-2, T=2 and 3."""
-    err, choice = _run(L, "Float32", fuse, 3 * fuse,
-                       env={"GS_FUSED_CFG": cfg, "GS_FUSED_SCHED": str(sched)})
-    assert err < 2e-5, (err, choice)
-    _, choice2 = _run(L, "Float32", fuse, 3 * fuse,
-                      env={"GS_FUSED_CFG": plain, "GS_FUSED_SCHED": str(sched)})
-    d1 = [w for w in choice.split() if len(w) == 40][0]
-    d2 = [w for w in choice2.split() if len(w) == 40][0]
-    assert d1 == d2, (choice, choice2)

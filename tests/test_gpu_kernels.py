@@ -200,28 +200,3 @@ def test_autotuner_choice_is_valid_and_state_unchanged(prec):
     assert np.abs(g.get_fields()[0] - c.get_fields()[0]).max() < tol
     assert np.abs(g.get_fields()[1] - c.get_fields()[1]).max() < tol
 
-
-@pytest.mark.parametrize("cfg", ["4x8:1sx", "4x6:2sx", "4x8:1x", "4x8:1sn", "4x8:1sxn"])
-@pytest.mark.parametrize("fuse", [2, 3])
-def test_fp64_lds_x_sums_bitwise(cfg, fuse):
-    """fp64 tiles with the x-neighbour pair sums through LDS (FCfg::LX) equal the DPP tiles bit
-    for bit (same association, zero pads like bound_ctrl), on an edge-heavy 70^3 grid with
-    noise, and the single-step path to fp64 rounding."""
-    from grayscott_amd.ops import native
-    native.load("hip")
-    outs = {}
-    try:
-        for name in ("4x8:1s", cfg):
-            native.fused_select(name)
-            native.fused_sched(2)
-            g = _sim("AMDGPU", 70, "Float64", 0.1, fuse=fuse)
-            g.iterate(4 * fuse + 1)
-            outs[name] = g.get_fields()
-            g.close()
-    finally:
-        native.fused_unpin()
-    np.testing.assert_array_equal(outs[cfg][0], outs["4x8:1s"][0])
-    np.testing.assert_array_equal(outs[cfg][1], outs["4x8:1s"][1])
-    c = _sim("CPU", 70, "Float64", 0.1, fuse=1)
-    c.iterate(4 * fuse + 1)
-    assert np.abs(outs[cfg][0] - c.get_fields()[0]).max() < 1e-12
