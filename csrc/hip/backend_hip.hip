@@ -854,6 +854,11 @@ class HipBackend final : public gs::Backend {
     gsk::launch_extract<T>(buf_[b], (T*)u, (T*)v, g_, stream_);
     HIP_CHECK(hipGetLastError());
   }
+  int extract_minmax(int b, void* u, void* v, void* part, int cap) override {
+    const int n = gsk::launch_extract_mm<T>(buf_[b], (T*)u, (T*)v, g_, (T*)part, cap, stream_);
+    HIP_CHECK(hipGetLastError());
+    return n;
+  }
   void randomize(int b, uint64_t seed, double lo, double hi) override {
     gsk::launch_randomize<T>(buf_[b], g_, seed, lo, hi, stream_);
     HIP_CHECK(hipGetLastError());

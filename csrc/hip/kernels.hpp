@@ -337,6 +337,64 @@ void launch_extract(const typename Vec2<T>::type* f, T* u, T* v, const Geom& g, 
   dim3 grid((g.nx + 255) / 256, g.ny, g.nz);
   k_interior<T, true><<<grid, 256, 0, st>>>(const_cast<typename Vec2<T>::type*>(f), u, v, g);
 }
+// Output snapshot with the BP4 block characteristics (SURVEY K14 + the writer's min / max): the
+// ghost-free copy of u and v AND each workgroup's min / max of both, so the host writer does not
+// scan the arrays again (a single-thread pass over 2 x 1 MB took ~75 us per field of the
+// reference example's output step, profiles/r5_output.txt).  Grid (ceil(nx / 256), G): workgroup
+// (bx, by) takes x columns bx*256 .. +255 of rows by, by + G, ... (row = y + ny * z); partials:
+// 4 values (u min, u max, v min, v max) per workgroup, reduced on the host (fmin / fmax: exact,
+// order-independent; a NaN is skipped).
+constexpr int kMinMaxRows = 1024;
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_extract_mm(const typename Vec2<T>::type* __restrict__ f,
+                                                    T* __restrict__ u, T* __restrict__ v, Geom g,
+                                                    T* __restrict__ part) {
+  const int x = blockIdx.x * 256 + threadIdx.x;
+  const int rows = g.ny * g.nz;
+  const T inf = (T)INFINITY;
+  T a = inf, b = -inf, c = inf, d = -inf;
+  if (x < g.nx) {
+    for (int r = blockIdx.y; r < rows; r += gridDim.y) {
+      const int z = r / g.ny, y = r - z * g.ny;
+      const typename Vec2<T>::type e = f[gs::lin(g, x, y, z)];
+      const int64_t o = (int64_t)r * g.nx + x;
+      u[o] = e.x;
+      v[o] = e.y;
+      a = fmin(a, e.x); b = fmax(b, e.x);
+      c = fmin(c, e.y); d = fmax(d, e.y);
+    }
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    a = fmin(a, __shfl_xor(a, m)); b = fmax(b, __shfl_xor(b, m));
+    c = fmin(c, __shfl_xor(c, m)); d = fmax(d, __shfl_xor(d, m));
+  }
+  __shared__ T w[4][4];
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { w[wave][0] = a; w[wave][1] = b; w[wave][2] = c; w[wave][3] = d; }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    const int k = threadIdx.x;
+    T r = w[0][k];
+    for (int i = 1; i < 4; ++i) r = (k & 1) ? fmax(r, w[i][k]) : fmin(r, w[i][k]);
+    part[4 * ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) + k] = r;
+  }
+}
+
+// returns the number of partial quadruples written (at most `cap`)
+template <typename T>
+int launch_extract_mm(const typename Vec2<T>::type* f, T* u, T* v, const Geom& g, T* part,
+                      int cap, hipStream_t st) {
+  const int gx = (g.nx + 255) / 256;
+  const int rows = g.ny * g.nz;
+  int gy = std::min(rows, kMinMaxRows);
+  gy = std::max(1, std::min(gy, cap / std::max(1, gx)));
+  if (gx * gy > cap || rows < 1) return -1;
+  k_extract_mm<T><<<dim3(gx, gy), 256, 0, st>>>(f, u, v, g, part);
+  return gx * gy;
+}
+
 template <typename T>
 void launch_insert(typename Vec2<T>::type* f, const T* u, const T* v, const Geom& g, hipStream_t st) {
   dim3 grid((g.nx + 255) / 256, g.ny, g.nz);

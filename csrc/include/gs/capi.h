@@ -39,6 +39,7 @@ int gs_set_step(gs_engine* e, int64_t t);
 int gs_current_buffer(gs_engine* e);
 int gs_sync(gs_engine* e);
 int gs_extract(gs_engine* e, void* u, void* v);
+int gs_extract_minmax(gs_engine* e, void* u, void* v, void* part, int32_t cap);
 int gs_insert(gs_engine* e, const void* u, const void* v);
 int gs_stats(gs_engine* e, double* out6);
 // random interior u, v ~ U[lo, hi) keyed on the global cell (any decomposition: same state)

@@ -103,6 +103,17 @@ int gs_sync(gs_engine* e) { GS_TRY(e->eng->backend()->wait_all(gs::comm_timeout_
 int gs_extract(gs_engine* e, void* u, void* v) {
   GS_TRY(e->eng->backend()->extract(e->eng->cur(), u, v))
 }
+// extract + per-chunk min / max (Backend::extract_minmax): the number of quadruples written at
+// `part` (<= cap), -2 when the backend has no such path, -1 on error
+int gs_extract_minmax(gs_engine* e, void* u, void* v, void* part, int32_t cap) {
+  try {
+    const int n = e->eng->backend()->extract_minmax(e->eng->cur(), u, v, part, cap);
+    return n < 0 ? -2 : n;
+  } catch (const std::exception& ex) {
+    g_gs_err = ex.what();
+    return -1;
+  }
+}
 int gs_insert(gs_engine* e, const void* u, const void* v) {
   GS_TRY(e->eng->backend()->insert(e->eng->cur(), u, v))
 }

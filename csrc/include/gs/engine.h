@@ -114,6 +114,12 @@ class Backend {
   // asynchronous transport error into an exception after `timeout_s` seconds (watchdog)
   virtual void wait_all(double timeout_s) { (void)timeout_s; host_sync(); }
   virtual void extract(int b, void* u, void* v) = 0;
+  // extract plus each chunk's min / max of u and v (cap quadruples {umin, umax, vmin, vmax} of the
+  // field's type at `part`); returns the number written, or -1 if the backend has no such path
+  virtual int extract_minmax(int b, void* u, void* v, void* part, int cap) {
+    (void)b; (void)u; (void)v; (void)part; (void)cap;
+    return -1;
+  }
   virtual void insert(int b, const void* u, const void* v) = 0;
   // random interior of buffer b, a function of the global cell only (gs::random_init_cell)
   virtual void randomize(int b, uint64_t seed, double lo, double hi) = 0;

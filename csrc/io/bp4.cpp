@@ -532,8 +532,19 @@ int bp4_begin_step(void* h) {
   }
 }
 
+static int put_block(void* h, int32_t var, const void* data, const double* given_mm);
+
 // Appends one block of variable `var` (host memory, row-major contiguous `count`).
-int bp4_put(void* h, int32_t var, const void* data) {
+int bp4_put(void* h, int32_t var, const void* data) { return put_block(h, var, data, nullptr); }
+
+// bp4_put with the block's min / max supplied by the caller (computed where the data was made,
+// e.g. by the GPU snapshot kernel), so the writer does not scan the block again
+int bp4_put_minmax(void* h, int32_t var, const void* data, double mn, double mx) {
+  const double mm[2] = {mn, mx};
+  return put_block(h, var, data, mm);
+}
+
+static int put_block(void* h, int32_t var, const void* data, const double* given_mm) {
   try {
     Writer* w = (Writer*)h;
     if (!w->step_open) throw std::runtime_error("put outside a step");
@@ -543,7 +554,10 @@ int bp4_put(void* h, int32_t var, const void* data) {
     for (auto c : v.count) n *= c;
     const bool single = v.count.empty();
     double mn = 0, mx = 0;
-    switch (v.type) {
+    if (given_mm && !single) {
+      mn = given_mm[0];
+      mx = given_mm[1];
+    } else switch (v.type) {
       case type_real: minmax_of<float>(data, n, mn, mx); break;
       case type_double: minmax_of<double>(data, n, mn, mx); break;
       case type_integer: minmax_of<int32_t>(data, n, mn, mx); break;

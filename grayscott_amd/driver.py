@@ -145,7 +145,7 @@ def run(settings: Settings, out=sys.stdout) -> dict:
                 print(f"Simulation at step {step} writing output step "
                       f"{step / settings.plotgap}", file=out, flush=True)
             t1 = time.perf_counter()
-            with timer.phase("output"):
+            with timer.phase("output", sync=not stream.async_io):
                 snap = stream.write_step(step, sim)
             io_s += time.perf_counter() - t1
             if settings.diagnostics:

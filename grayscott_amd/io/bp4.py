@@ -69,6 +69,8 @@ def _lib():
         lib.bp4_begin_step.restype = c_int32
         lib.bp4_put.argtypes = [c_void_p, c_int32, c_void_p]
         lib.bp4_put.restype = c_int32
+        lib.bp4_put_minmax.argtypes = [c_void_p, c_int32, c_void_p, ctypes.c_double, ctypes.c_double]
+        lib.bp4_put_minmax.restype = c_int32
         lib.bp4_end_step.argtypes = [c_void_p]
         lib.bp4_end_step.restype = c_int32
         lib.bp4_step_metadata.argtypes = [c_void_p, POINTER(ctypes.POINTER(ctypes.c_char))]
@@ -152,14 +154,21 @@ class BP4Writer:
     def begin_step(self) -> None:
         self._chk(self.lib.bp4_begin_step(self.h), "begin_step")
 
-    def put(self, name: str, data) -> None:
+    def put(self, name: str, data, minmax=None) -> None:
+        """Append this rank's block of ``name``.  ``minmax``: the block's (min, max), when the
+        caller already has them (the GPU snapshot computes them, GrayScott.snapshot_fields), so
+        the writer does not scan the block for its characteristics."""
         vid, dt, count = self._vars[name]
         a = np.ascontiguousarray(np.asarray(data, dtype=dt))
         if count and a.shape != count:
             raise BP4Error(f"{name}: block shape {a.shape} != count {count}")
         if not count and a.size != 1:
             raise BP4Error(f"{name}: single value expected")
-        self._chk(self.lib.bp4_put(self.h, vid, a.ctypes.data), f"put {name}")
+        if minmax is not None and count:
+            self._chk(self.lib.bp4_put_minmax(self.h, vid, a.ctypes.data, float(minmax[0]),
+                                              float(minmax[1])), f"put {name}")
+        else:
+            self._chk(self.lib.bp4_put(self.h, vid, a.ctypes.data), f"put {name}")
 
     def end_step(self) -> bytes:
         """Close the step's process group; returns this rank's metadata blob."""

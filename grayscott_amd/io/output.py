@@ -177,15 +177,16 @@ class SimulationOutput:
         depth = max(1, min(self.queue, PINNED_RING_BYTES // max(1, _snapshot_bytes(sim))))
         while len(self._pending) >= depth:
             self._commit_oldest()
-        snap = sim.snapshot_fields("output", depth=depth)
-        u, v, wait = snap
+        u, v, wait, mm = sim.snapshot_fields("output", depth=depth, minmax=True)
+        snap = (u, v, wait)
 
         def job():
             wait()
+            (umn, umx), (vmn, vmx) = mm()  # the snapshot kernel's min / max (no host scan)
             self.w.begin_step()
             self.w.put("step", np.int32(step))
-            self.w.put("U", u)
-            self.w.put("V", v)
+            self.w.put("U", u, minmax=(umn, umx))
+            self.w.put("V", v, minmax=(vmn, vmx))
             return self.w.end_step()
 
         self._pending.append((step, worker("gs-async-output").submit(job)))

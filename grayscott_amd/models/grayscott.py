@@ -354,7 +354,9 @@ class GrayScott:
         u, v = self.get_fields_device()
         return u.numpy(), v.numpy()
 
-    def snapshot_fields(self, slot: str = "output", depth: int = 1):
+    _MM_CAP = 2048  # partial min / max quadruples of the snapshot kernel (kernels.hpp kMinMaxRows)
+
+    def snapshot_fields(self, slot: str = "output", depth: int = 1, minmax: bool = False):
         """Asynchronous ghost-stripped copy of u, v for output: the compaction
         kernel runs in stream order on the compute stream, the D2H copy into pinned host
         buffers on a separate I/O stream, so stepping continues while the copy (and the file
@@ -366,9 +368,16 @@ class GrayScott:
         a snapshot (its write joined) before the ``depth``-th next call of the same slot reuses
         its host buffers (the output stream keeps up to ``depth`` steps in flight).  The device
         buffers are not overwritten before the previous D2H copy out of them has finished (the
-        compute stream waits for it), so consumers of different slots never race."""
+        compute stream waits for it), so consumers of different slots never race.
+
+        ``minmax``: also return, as a fourth element, a callable giving ((u min, u max), (v min,
+        v max)) of the snapshot once ``wait()`` has returned -- computed by the snapshot kernel
+        itself (per-chunk partials copied with the data), so the BP4 writer need not scan the
+        arrays for its block characteristics."""
         if self.backend != "hip":
             u, v = self.get_fields()
+            if minmax:
+                return u, v, lambda: None, lambda: ((u.min(), u.max()), (v.min(), v.max()))
             return u, v, lambda: None
         tdt = _TORCH_DTYPES[self.dtype]
         depth = max(1, int(depth))
@@ -379,18 +388,25 @@ class GrayScott:
         if st is None or len(st["host"]) != depth:
             if st is not None and st["done"] is not None:
                 st["done"].synchronize()  # the old ring's last copy has landed
+            cap = self._MM_CAP
             st = self._snaps[slot] = {
                 "dev": [torch.empty(self.local_shape, dtype=tdt, device=self.device)
-                        for _ in range(2)],
+                        for _ in range(2)] + [torch.empty(4 * cap, dtype=tdt, device=self.device)],
                 "host": [[torch.empty(self.local_shape, dtype=tdt, pin_memory=True)
-                          for _ in range(2)] for _ in range(depth)],
+                          for _ in range(2)] + [torch.empty(4 * cap, dtype=tdt, pin_memory=True)]
+                         for _ in range(depth)],
                 "next": 0, "done": None}
         dev, host = st["dev"], st["host"][st["next"]]
         st["next"] = (st["next"] + 1) % depth
         cur = torch.cuda.current_stream(self.device)
         if st["done"] is not None:
             cur.wait_event(st["done"])  # the previous D2H out of dev[] has finished
-        self.engine.extract(dev[0].data_ptr(), dev[1].data_ptr())
+        nmm = 0
+        if minmax:
+            nmm = self.engine.extract_minmax(dev[0].data_ptr(), dev[1].data_ptr(),
+                                             dev[2].data_ptr(), self._MM_CAP)
+        if not nmm:
+            self.engine.extract(dev[0].data_ptr(), dev[1].data_ptr())
         ready = torch.cuda.Event()
         ready.record(cur)
         done = torch.cuda.Event()
@@ -398,9 +414,22 @@ class GrayScott:
             self._io_stream.wait_event(ready)
             host[0].copy_(dev[0], non_blocking=True)
             host[1].copy_(dev[1], non_blocking=True)
+            if nmm:
+                host[2][:4 * nmm].copy_(dev[2][:4 * nmm], non_blocking=True)
             done.record(self._io_stream)
         st["done"] = done
-        return host[0].numpy(), host[1].numpy(), done.synchronize
+        u, v = host[0].numpy(), host[1].numpy()
+        if not minmax:
+            return u, v, done.synchronize
+        if nmm:
+            part = host[2].numpy()[:4 * nmm].reshape(nmm, 4)
+
+            def mm():
+                return ((part[:, 0].min(), part[:, 1].max()), (part[:, 2].min(), part[:, 3].max()))
+        else:
+            def mm():
+                return ((u.min(), u.max()), (v.min(), v.max()))
+        return u, v, done.synchronize, mm
 
     def set_fields(self, u, v) -> None:
         """Overwrite the interior of the current state (restart).  ``u``, ``v``: (nz, ny, nx)

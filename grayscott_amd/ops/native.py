@@ -87,6 +87,8 @@ def _declare(lib) -> None:
     lib.gs_set_step.restype = c_int
     lib.gs_extract.argtypes = [c_void_p, c_void_p, c_void_p]
     lib.gs_extract.restype = c_int
+    lib.gs_extract_minmax.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_int32]
+    lib.gs_extract_minmax.restype = c_int
     lib.gs_insert.argtypes = [c_void_p, c_void_p, c_void_p]
     lib.gs_insert.restype = c_int
     lib.gs_stats.argtypes = [c_void_p, POINTER(c_double)]
@@ -303,6 +305,17 @@ class Engine:
     def extract(self, u_ptr: int, v_ptr: int):
         self._chk(self.lib.gs_extract(self.h, c_void_p(u_ptr or None), c_void_p(v_ptr or None)),
                   "extract")
+
+    def extract_minmax(self, u_ptr: int, v_ptr: int, part_ptr: int, cap: int) -> int:
+        """extract() plus each chunk's (u min, u max, v min, v max) at ``part_ptr`` (``cap``
+        quadruples of the field type): the number written, or 0 if the backend has no such
+        path (the CPU backend)."""
+        n = self.lib.gs_extract_minmax(self.h, c_void_p(u_ptr), c_void_p(v_ptr),
+                                       c_void_p(part_ptr), int(cap))
+        if n == -2:
+            return 0
+        self._chk(0 if n >= 0 else -1, "extract_minmax")
+        return n
 
     def insert(self, u_ptr: int, v_ptr: int):
         self._chk(self.lib.gs_insert(self.h, c_void_p(u_ptr), c_void_p(v_ptr)), "insert")

@@ -29,13 +29,19 @@ class PhaseTimer:
         self.calls: Dict[str, int] = defaultdict(int)
 
     @contextmanager
-    def phase(self, name: str):
-        self.sync()
+    def phase(self, name: str, sync: bool = True):
+        """Time a host phase.  ``sync``: wait for the device on both sides, so queued device work
+        is not counted in the phase (and the phase's own device work is); an asynchronous phase
+        (the output step: stream-ordered snapshot, host-thread write) passes False and is timed on
+        the host only -- a device wait there would stall the host's run-ahead every output step."""
+        if sync:
+            self.sync()
         t0 = time.perf_counter()
         try:
             yield
         finally:
-            self.sync()
+            if sync:
+                self.sync()
             self.total[name] += time.perf_counter() - t0
             self.calls[name] += 1
 

@@ -200,3 +200,20 @@ def test_autotuner_choice_is_valid_and_state_unchanged(prec):
     assert np.abs(g.get_fields()[0] - c.get_fields()[0]).max() < tol
     assert np.abs(g.get_fields()[1] - c.get_fields()[1]).max() < tol
 
+
+
+@pytest.mark.parametrize("prec,L", [("Float32", 40), ("Float64", 40), ("Float32", 300)])
+def test_snapshot_minmax_equals_host_scan(prec, L):
+    """The output snapshot's min / max (k_extract_mm partials, reduced on the host) equal a scan
+    of the snapshot itself, and the snapshot equals get_fields (nx = 300: two x chunks)."""
+    g = _sim("AMDGPU", L, prec, 0.1, fuse=2)
+    g.randomize_fields(seed=3, lo=-0.5, hi=1.5)
+    g.iterate(5)
+    u, v, wait, mm = g.snapshot_fields("t", minmax=True)
+    wait()
+    (a, b), (c, d) = mm()
+    assert (a, b, c, d) == (u.min(), u.max(), v.min(), v.max())
+    gu, gv = g.get_fields()
+    np.testing.assert_array_equal(u, gu)
+    np.testing.assert_array_equal(v, gv)
+    g.close()

@@ -295,3 +295,23 @@ def test_async_checkpoint_matches_sync_gpu(tmp_path):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     _async_vs_sync(tmp_path, "AMDGPU", 96, 40, 3, (4, 6))
+
+
+def test_put_with_given_minmax(tmp_path):
+    """BP4Writer.put(minmax=...) stores the caller's block min / max (the GPU snapshot's) as the
+    block characteristics; the data round-trips unchanged."""
+    import numpy as np
+
+    from grayscott_amd.io.bp4 import BP4Reader, BP4Writer
+    w = BP4Writer(str(tmp_path / "mm.bp"), "T")
+    w.define_variable("U", np.float32, (2, 3, 4), (0, 0, 0), (2, 3, 4))
+    a = np.arange(24, dtype=np.float32).reshape(2, 3, 4) - 5
+    w.begin_step()
+    w.put("U", a, minmax=(a.min(), a.max()))
+    w.write_metadata([w.end_step()])
+    w.close()
+    r = BP4Reader(str(tmp_path / "mm.bp"))
+    np.testing.assert_array_equal(r.read("U", 0), a)
+    blk = r.variables(0)["U"].blocks[0]
+    assert (blk.vmin, blk.vmax) == (-5.0, 18.0)
+    r.close()
