@@ -191,7 +191,8 @@ def self_launch(args, argv, ngpus: int) -> int:
                     rec = None
                 if isinstance(rec, dict) and rec.get("value") is None:
                     # rank 0's own failure record: name the first rank this parent saw fail
-                    if info.get("failed_rank") not in (None, 0):
+                    # (a deadline stays a timeout: every rank exits 124 then, in any order)
+                    if info.get("failed_rank") not in (None, 0) and rec.get("status") != "timeout":
                         rec["status"] = "rank_failed"
                     rec["failed_rank"] = info.get("failed_rank")
                     rec["exit_codes"] = info.get("codes")

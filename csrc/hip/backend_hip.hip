@@ -25,10 +25,13 @@
 namespace gsk {
 extern template bool launch_fused<float>(const Vec2<float>::type*, Vec2<float>::type*, const Geom&,
                                          const gs::Params&, int, int64_t, hipStream_t, int, int,
-                                         int, int, int, int, int, int, bool);
+                                         int, int, int, int, int, int, bool, const GateLaunch*);
 extern template bool launch_fused<double>(const Vec2<double>::type*, Vec2<double>::type*,
                                           const Geom&, const gs::Params&, int, int64_t,
-                                          hipStream_t, int, int, int, int, int, int, int, int, bool);
+                                          hipStream_t, int, int, int, int, int, int, int, int, bool,
+                                          const GateLaunch*);
+extern template int fused_gated_occupancy<float>(int, int);
+extern template int fused_gated_occupancy<double>(int, int);
 extern template bool launch_shell<float>(const void*, void*, const Geom&, const gs::Params&, int,
                                          int64_t, int, int, hipStream_t);
 extern template bool launch_shell<double>(const void*, void*, const Geom&, const gs::Params&, int,
@@ -129,6 +132,7 @@ class HipBackend final : public gs::Backend {
   }
   ~HipBackend() override {
     ipc_release();
+    gate_release();
     if (comm_ && comm_ != shared_comm().comm) ncclCommDestroy(comm_);
     if (ws_) (void)hipFree(ws_);
     if (ev_) (void)hipEventDestroy(ev_);
@@ -672,6 +676,17 @@ class HipBackend final : public gs::Backend {
       throw std::runtime_error("ipc: the transport needs symmetric neighbours (send peers = "
                                "receive peers), as every Cartesian decomposition has");
     ipc_ = true;
+    // the gated pass (gate.hpp) packs every message straight into a landing slot: it needs a
+    // landing-buffer route for each (no local self copies: a periodic wrap onto this rank
+    // without loopback goes through the stream path)
+    gplan_ = p;
+    gate_plan_ok_ = p.nsend > 0 && p.nrecv > 0;
+    for (int i = 0; i < p.nsend; ++i) gate_plan_ok_ = gate_plan_ok_ && send_peer_[i] >= 0;
+    for (int i = 0; i < p.nrecv; ++i) gate_plan_ok_ = gate_plan_ok_ && recv_peer_[i] >= 0;
+    // peer processes on this same GPU (tests): their gated launches compete for its slots
+    gate_sharers_ = 0;
+    for (const PeerMap& pm : peers_) gate_sharers_ += (pm.rank != rank_ && pm.device == dev_) ? 1 : 0;
+    gate_release();
   }
 
   void ipc_pack(int b, const gs::HaloPlan& p) {
@@ -741,6 +756,8 @@ class HipBackend final : public gs::Backend {
   }
 
   void ipc_release() {
+    gate_release();
+    gate_plan_ok_ = false;
     if (landing_ || !peers_.empty()) {
       (void)hipDeviceSynchronize();
       for (PeerMap& pm : peers_)
@@ -759,6 +776,251 @@ class HipBackend final : public gs::Backend {
     ipc_dflag_ = nullptr;
     ipc_err_ = ipc_err_dev_ = nullptr;
     ipc_ = false;
+  }
+
+  // ---------------------------------------------------------------------------------------
+  // Gated pass (gate.hpp, engine.h advance_gated): one k_fused launch per pass carries the IPC
+  // halo exchange.  The host builds the unit table (one unit per workgroup, start-gated units
+  // sized shorter by the expected exchange time) for the tile shape the full pass was tuned to,
+  // and tunes that expected time on the device (gate_tune).
+  bool gated_supported(int n) const override {
+    // the gated entry exists for the production variants only (FCfg::GATE_OK): non-periodic,
+    // noisy, 32-bit Philox counter
+    return ipc_ && gate_plan_ok_ && gsk::fused_supported(g_, n) && n >= 2 && n <= 3 &&
+           g_.nz >= 2 * n + 1 && !g_.periodic && p_.noise != 0.0 && gsk::philox_q32(g_) &&
+           !gs::debug_knobs().philox_generic &&
+           // peers sharing this GPU: only when asked (debug knob gated = 2) -- every rank's
+           // waiting units must be resident at once, across processes (gate_table)
+           (gate_sharers_ == 0 || gs::debug_knobs().gated >= 2);
+  }
+
+  void gate_release() {
+    if (d_gate_) (void)hipFree(d_gate_);
+    if (d_counter_) (void)hipFree(d_counter_);
+    if (d_stamps_) (void)hipFree(d_stamps_);
+    d_stamps_ = nullptr;
+    for (auto*& u : d_units_)
+      if (u) { (void)hipFree(u); u = nullptr; }
+    d_gate_ = nullptr;
+    d_counter_ = nullptr;
+    cnt_host_ = 0;
+    for (int i = 0; i < 4; ++i) { gate_tuned_[i] = false; nunits_[i] = npk_[i] = 0; gate_xp_[i] = -1; }
+  }
+
+  // the transport half of the launch arguments (device copy, built once per IPC connection)
+  void gate_setup() {
+    if (d_gate_) return;
+    gsk::GateArgs G{};
+    const gs::HaloPlan& p = gplan_;
+    G.nsend = p.nsend;
+    for (int i = 0; i < p.nsend; ++i) {
+      const PeerMap& pm = peers_[send_peer_[i]];
+      G.sbox[i] = p.send[i].box;
+      for (int sl = 0; sl < 2; ++sl) G.sdst[sl][i] = pm.landing + sl * pm.slot_cells + send_off_[i];
+      if (pm.device != dev_ || gs::debug_knobs().ipc_system_stores) G.sysmask |= 1u << i;
+    }
+    G.nrecv = p.nrecv;
+    for (int i = 0; i < p.nrecv; ++i) {
+      G.rbox[i] = p.recv[i].box;
+      for (int sl = 0; sl < 2; ++sl) G.rsrc[sl][i] = landing_ + sl * landing_cells_ + p.recv[i].offset;
+    }
+    for (int idx : recv_peers_) G.wflag[G.nwait++] = flags_ + peers_[idx].rank;
+    for (int idx : send_peers_) G.sflag[G.nsig++] = peers_[idx].flags + rank_;
+    HIP_CHECK(hipMalloc((void**)&d_counter_, sizeof(uint32_t)));
+    HIP_CHECK(hipMemset(d_counter_, 0, sizeof(uint32_t)));
+    cnt_host_ = 0;
+    G.counter = d_counter_;
+    G.ticks = ipc_ticks_;
+    G.min_ticks = ipc_emulate_ticks_;
+    G.err = ipc_err_dev_;
+    G.dflag = ipc_dflag_;
+    if (gs::debug_knobs().gate_stamps) {
+      HIP_CHECK(hipMalloc((void**)&d_stamps_, 8 * sizeof(unsigned long long)));
+      G.stamps = d_stamps_;
+    }
+    HIP_CHECK(hipMalloc((void**)&d_gate_, sizeof(gsk::GateArgs)));
+    HIP_CHECK(hipMemcpy(d_gate_, &G, sizeof(G), hipMemcpyHostToDevice));
+  }
+
+  // Unit table of a depth-n gated pass for the tile shape the full pass runs, with start-gated
+  // chunks shorter by xp planes (the expected exchange time in plane-times): the smallest plane
+  // budget per workgroup whose chunks fit the resident slots.  Sorted by (z0, tile): each XCD
+  // group of workgroups gets a contiguous range (sched 3), i.e. neighbouring tiles at one depth.
+  std::vector<gsk::GateUnit> gate_table(int n, int xp, int* npk) const {
+    const int cfg = gsk::gated_shape_cfg(sizeof(T) == 8, g_, n);
+    const char* name = gsk::fused_shape_name(cfg, sizeof(T) == 8, true);
+    const gsk::TileGrid tg = gsk::fused_tile_grid(name, g_, n);
+    // every unit resident at once (the device's occupancy of the gated entry): a start-gated
+    // unit that waits for the peers holds its slot, so a packer left unscheduled behind waiting
+    // units would stall every rank until the wall-clock bound
+    const int per_cu = gsk::fused_gated_occupancy<T>(cfg, n);
+    if (per_cu < 1) throw std::runtime_error("gated pass: no gated entry for this shape");
+    // (peer processes on this GPU, debug knob gated = 2: this rank's share of the slots)
+    const int slots = std::max(8, num_cus() * per_cu / (gate_sharers_ + 1));
+    const int nz = g_.nz;
+    const gs::HaloPlan& p = gplan_;
+    auto dep = [&](int X0, int xw, int Y0, int ye, int z0, int z1) {
+      for (int i = 0; i < p.nrecv; ++i) {
+        const gs::Box& b = p.recv[i].box;
+        if (b.x0 < X0 + xw && X0 < b.x0 + b.nx && b.y0 < Y0 + ye && Y0 < b.y0 + b.ny &&
+            b.z0 < z1 + n && z0 - n < b.z0 + b.nz)
+          return true;
+      }
+      return false;
+    };
+    struct Col { bool strip, lo, hi; };
+    std::vector<Col> cols((size_t)tg.ntiles);
+    for (int t = 0; t < tg.ntiles; ++t) {
+      int X0, xw, Y0, ye;
+      gsk::tile_window(tg, t, n, &X0, &xw, &Y0, &ye);
+      cols[t].strip = dep(X0, xw, Y0, ye, n, nz - n);
+      cols[t].lo = dep(X0, xw, Y0, ye, 0, 1);
+      cols[t].hi = dep(X0, xw, Y0, ye, nz - 1, nz);
+    }
+    const int F = 5 * n;  // pipeline fill + ramp of a unit, in plane-times (launch model)
+    // chunk [a, b) into pieces of at most len; gated pieces get pk = 0 (numbered later)
+    auto build = [&](int tau, std::vector<gsk::GateUnit>* out) -> int {
+      const int lg = std::max(1, tau - F - xp), li = std::max(1, tau - F);
+      int cnt = 0;
+      auto sect = [&](int t, int a, int b, int len, bool gated) {
+        if (b <= a) return;
+        const int k = (b - a + len - 1) / len;
+        for (int i = 0; i < k; ++i) {
+          const int z0 = a + (int)((int64_t)(b - a) * i / k), z1 = a + (int)((int64_t)(b - a) * (i + 1) / k);
+          if (out) out->push_back(gsk::GateUnit{t, z0, z1, gated ? 0 : -1});
+          ++cnt;
+        }
+      };
+      for (int t = 0; t < tg.ntiles; ++t) {
+        const Col& c = cols[t];
+        const int P = c.lo ? std::max(n, std::min(lg, nz)) : 0;
+        const int S = c.hi ? std::max(n, std::min(lg, nz)) : 0;
+        if (c.strip || P + S >= nz) {
+          sect(t, 0, nz, lg, true);
+        } else {
+          sect(t, 0, P, lg, true);
+          sect(t, P, nz - S, li, false);
+          sect(t, nz - S, nz, lg, true);
+        }
+      }
+      return cnt;
+    };
+    int tau = F + 1;
+    const int tmax = F + xp + nz + 1;
+    while (tau < tmax && build(tau, nullptr) > slots) ++tau;
+    std::vector<gsk::GateUnit> u;
+    build(tau, &u);
+    std::stable_sort(u.begin(), u.end(), [](const gsk::GateUnit& a, const gsk::GateUnit& b) {
+      return a.z0 != b.z0 ? a.z0 < b.z0 : a.tile < b.tile;
+    });
+    int k = 0;
+    for (auto& x : u)
+      if (x.pk >= 0) x.pk = k++;
+    *npk = k;
+    return u;
+  }
+
+  void gate_upload(int n, const std::vector<gsk::GateUnit>& u, int npk) {
+    const size_t bytes = std::max<size_t>(u.size(), 1) * sizeof(gsk::GateUnit);
+    if (!d_units_[n] || cap_units_[n] < u.size()) {
+      if (d_units_[n]) (void)hipFree(d_units_[n]);
+      HIP_CHECK(hipMalloc((void**)&d_units_[n], std::max<size_t>(bytes, 4096 * sizeof(gsk::GateUnit))));
+      cap_units_[n] = std::max<size_t>(u.size(), 4096);
+    }
+    HIP_CHECK(hipStreamSynchronize(stream_));  // no launch still reads the previous table
+    HIP_CHECK(hipMemcpy(d_units_[n], u.data(), bytes, hipMemcpyHostToDevice));
+    nunits_[n] = (int)u.size();
+    npk_[n] = npk;
+  }
+
+  // one gated pass src -> dst on the compute stream (exchange number ++xn_)
+  void gate_launch(int src, int dst, int n, int64_t t) {
+    gsk::GateLaunch gl{};
+    gl.units = d_units_[n];
+    gl.nunits = nunits_[n];
+    gl.gate = d_gate_;
+    gl.n = ++xn_;
+    cnt_host_ += (uint32_t)npk_[n];
+    gl.cnt = cnt_host_;
+    gl.npk = npk_[n];
+    if (d_stamps_) {  // debug knob gate_stamps: this launch's stamps only
+      const unsigned long long init[5] = {~0ull, 0ull, ~0ull, 0ull, 0ull};
+      HIP_CHECK(hipMemcpyAsync(d_stamps_, init, sizeof(init), hipMemcpyHostToDevice, stream_));
+    }
+    if (!gsk::launch_fused<T>(buf_[src], buf_[dst], g_, p_, n, t, stream_,
+                              gsk::gated_shape_cfg(sizeof(T) == 8, g_, n), 3, 0, g_.nz, 0, 0, 0,
+                              0, false, &gl))
+      throw std::runtime_error("gated pass: launch rejected");
+    HIP_CHECK(hipGetLastError());
+  }
+
+  // Expected exchange time per pass (xp, plane-times) tuned on the device: each candidate
+  // table is timed over a few passes, the fastest kept.  Every rank times the same candidates
+  // in the same order (each pass is an exchange all ranks take part in); ranks may keep
+  // different tables -- the protocol only needs every rank to pack and signal once per pass.
+  void gate_tune(int src, int dst, int n, int64_t t) {
+    if (!tuned_[n]) autotune(src, dst, n, t);
+    gate_setup();
+    static const int kXp[] = {0, 4, 8, 16, 24, 32};
+    float best = 1e30f;
+    int bxp = 0;
+    hipEvent_t e0, e1;
+    HIP_CHECK(hipEventCreate(&e0));
+    HIP_CHECK(hipEventCreate(&e1));
+    for (int xp : kXp) {
+      int npk = 0;
+      const std::vector<gsk::GateUnit> u = gate_table(n, xp, &npk);
+      gate_upload(n, u, npk);
+      gate_launch(src, dst, n, t);  // warm-up
+      HIP_CHECK(hipEventRecord(e0, stream_));
+      for (int r = 0; r < 3; ++r) gate_launch(src, dst, n, t);
+      HIP_CHECK(hipEventRecord(e1, stream_));
+      wait_all(gs::comm_timeout_s());
+      float ms = 0.f;
+      HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+      if (ms < best) { best = ms; bxp = xp; }
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    int npk = 0;
+    const std::vector<gsk::GateUnit> u = gate_table(n, bxp, &npk);
+    gate_upload(n, u, npk);
+    gate_xp_[n] = bxp;
+    gate_ms_[n] = best / 3.f;
+    gate_tuned_[n] = true;
+  }
+
+  void prepare_gated(int src, int dst, int n, int64_t t) override {
+    if (gated_supported(n) && !gate_tuned_[n]) gate_tune(src, dst, n, t);
+  }
+
+  bool fused_gated(int src, int dst, int n, int64_t t) override {
+    if (!gated_supported(n)) return false;
+    if (!gate_tuned_[n]) gate_tune(src, dst, n, t);
+    gate_launch(src, dst, n, t);
+    return true;
+  }
+
+  // debug knob gate_stamps: the last gated launch's exchange, µs after its first packer
+  // started -- {last arrival (packing done), first wait done, last wait done, last unpack done}
+  void gate_stamps(double* out4) {
+    for (int i = 0; i < 4; ++i) out4[i] = -1.0;
+    if (!d_stamps_) return;
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    unsigned long long h[5];
+    HIP_CHECK(hipMemcpy(h, d_stamps_, sizeof(h), hipMemcpyDeviceToHost));
+    int khz = 0;
+    HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev_));
+    const double us = 1000.0 / (double)std::max(khz, 1);
+    for (int i = 0; i < 4; ++i) out4[i] = h[0] == ~0ull ? -1.0 : (double)(h[i + 1] - h[0]) * us;
+  }
+
+  // {tuned xp (plane-times), units, packers, ms per pass} of depth n (-1: not tuned)
+  void gate_info(int n, double* out4) const {
+    out4[0] = gate_xp_[n];
+    out4[1] = nunits_[n];
+    out4[2] = npk_[n];
+    out4[3] = gate_ms_[n];
   }
 
   // Forget the device transport after a failed trial (the "auto" fallback chain): abort the
@@ -1028,6 +1290,21 @@ class HipBackend final : public gs::Backend {
   float tuned_ms_[4] = {0.f, 0.f, 0.f, 0.f};
   std::vector<ShellChoice> shells_;
   std::vector<PartChoice> parts_;
+  // gated pass (gate_*)
+  gs::HaloPlan gplan_{};
+  bool gate_plan_ok_ = false;
+  int gate_sharers_ = 0;  // peer ranks (other processes) on this GPU
+  unsigned long long* d_stamps_ = nullptr;  // debug knob gate_stamps
+  gsk::GateArgs* d_gate_ = nullptr;
+  uint32_t* d_counter_ = nullptr;
+  uint32_t cnt_host_ = 0;  // packer arrivals issued so far (the device counter's value after them)
+  gsk::GateUnit* d_units_[4] = {nullptr, nullptr, nullptr, nullptr};
+  size_t cap_units_[4] = {0, 0, 0, 0};
+  int nunits_[4] = {0, 0, 0, 0};
+  int npk_[4] = {0, 0, 0, 0};
+  int gate_xp_[4] = {-1, -1, -1, -1};
+  float gate_ms_[4] = {0.f, 0.f, 0.f, 0.f};
+  bool gate_tuned_[4] = {false, false, false, false};
 };
 
 }  // namespace
@@ -1229,6 +1506,29 @@ int gs_fused_choice(gs_engine* e, int32_t n, int32_t dtype, int32_t* out2, float
 }
 
 }  // extern "C"
+
+// the gated pass of depth n: out4 = {tuned expected exchange (plane-times, -1: not tuned),
+// units, packers, ms per pass measured while tuning}
+extern "C" int gs_gate_info(gs_engine* e, int32_t n, int32_t dtype, double* out4) {
+  if (n < 0 || n > 3) return -1;
+  try {
+    with_hip_backend(e, dtype, [&](auto* b) { b->gate_info(n, out4); });
+    return 0;
+  } catch (const std::exception& ex) {
+    g_gs_err = ex.what();
+    return -1;
+  }
+}
+
+extern "C" int gs_gate_stamps(gs_engine* e, int32_t dtype, double* out4) {
+  try {
+    with_hip_backend(e, dtype, [&](auto* b) { b->gate_stamps(out4); });
+    return 0;
+  } catch (const std::exception& ex) {
+    g_gs_err = ex.what();
+    return -1;
+  }
+}
 
 extern "C" const char* gs_fused_cfg_name(int32_t index) {
   int n = 0;

@@ -33,6 +33,19 @@
 //    32 bits (Q32: Lx * ceil(Ly/4) * Lz < 2^32, every grid up to L = 2580).
 #pragma once
 
+// Gated pass (IPC transport, gate.hpp): ONE k_fused launch per pass that also carries the halo
+// exchange.  Every workgroup runs one unit from a host-built table; a start-gated unit (its
+// level-0 cone reads ghost cells a neighbour fills) first packs its share of the outgoing
+// messages straight into the peers' landing buffers, the last packer signals the peers, then it
+// waits for the peers' signals and copies the ghost cells of its own cone out of its landing
+// slot before marching.  Ungated units (cone clear of every face with a neighbour) march at once.
+struct GateUnit {
+  int32_t tile;    // tile index (this launch's enumeration)
+  int32_t z0, z1;  // output planes [z0, z1)
+  int32_t pk;      // >= 0: start-gated, its packer index; -1: ungated
+};
+struct GateArgs;  // gate.hpp
+
 struct FusedArgs {
   Geom g;
   int32_t ntx, nty;
@@ -65,7 +78,21 @@ struct FusedArgs {
   // strip's narrow tiles (<= 32 - 2T outputs wide) run two per wave as nfold = ceil(nty / 2)
   // units -- lanes 0-31 y-tile 2f, lanes 32-63 y-tile 2f + 1 (idle past the last one)
   int32_t ntxf, nfold;
+  // gated pass (sched 3, gate.hpp): the unit table (one unit per workgroup), the transport state,
+  // the source buffer as a writable pointer (the in-kernel unpack fills its ghosts), this pass's
+  // exchange number and the packer-arrival count its last packer reaches
+  const GateUnit* gunits;
+  const GateArgs* gate;
+  void* field;
+  uint64_t gate_n;
+  uint32_t gate_cnt;
+  int32_t gate_npk;  // packers of this launch (its start-gated units)
+  int32_t ngunits;
 };
+
+template <typename T>
+__device__ __forceinline__ void gate_start(const FusedArgs& a, int pk, int X0, int xw, int Y0, int yext, int za,
+                           int zb);
 
 template <typename T> struct PairT;
 template <> struct PairT<float> { typedef float type __attribute__((ext_vector_type(2))); };
@@ -398,6 +425,11 @@ struct FCfg {
   static constexpr int STORE_AUX = ((ABL_ & 2048) ? 2 : 0) | ((ABL_ & 4096) ? 16 : 0);
   static constexpr bool hoisted(int l) { return HOISTN > 0 && l >= TL_ - HOISTN; }
   static constexpr int YSTEP = (RT - 2 * TL) & ~3;        // output rows per tile
+  // the shapes with a gated-pass entry (k_fused_gated, gate.hpp): the production path's skewed
+  // 1-prefetch tiles -- fp32 4x12 (folded or not), fp64 4x8 -- non-periodic, noisy, 32-bit counter
+  static constexpr bool GATE_OK = !PERIODIC_ && NOISE_ && Q32_ && ABL_ == 0 && OPT_ == 0 &&
+                                  ROWS_ == 4 && SKEW_ && PF_ == 1 &&
+                                  ((sizeof(T_) == 4 && WAVES_ == 12) || (sizeof(T_) == 8 && WAVES_ == 8));
   // rows of output level L = l + 1 that some stored output depends on: [l + 1, hi(l)]
   static constexpr int need_hi(int l) { return 2 * TL + YSTEP - 2 - l; }
 };
@@ -725,11 +757,12 @@ __device__ __forceinline__ bool fused_period(FusedState<C>& S,
   }
 }
 
-template <class C, typename T>
-__global__ __launch_bounds__(64 * C::WAVES, C::WPEU) void k_fused(const typename C::V2* __restrict__ s,
-                                                            typename C::V2* __restrict__ d,
-                                                            FusedArgs a, FoldCoef<T> f,
-                                                            uint64_t seed) {
+// The kernel body; GATED: the gated pass's entry (k_fused_gated, sched 3), whose prologue
+// carries the halo exchange (gate.hpp).  The plain entry compiles without any of it.
+template <class C, typename T, bool GATED>
+__device__ __forceinline__ void fused_body(const typename C::V2* __restrict__ s,
+                                           typename C::V2* __restrict__ d, const FusedArgs& a,
+                                           const FoldCoef<T>& f, uint64_t seed) {
   constexpr int ROWS = C::ROWS, WAVES = C::WAVES, TL = C::TL;
   static_assert(ROWS % 4 == 0, "rows per wave must hold whole noise quads");
   __shared__ typename C::V2 xch[TL][C::NS][WAVES][2][64];  // [level][ring][wave][row][lane]
@@ -785,6 +818,30 @@ __global__ __launch_bounds__(64 * C::WAVES, C::WPEU) void k_fused(const typename
     lu1 = min((b % 8 + 1) * per, nunits);
     lstep = gridDim.x / 8;
     if (lu0 >= lu1) return;
+  } else if (GATED) {
+    // gated pass: one table unit per workgroup, each XCD group a contiguous range (the host
+    // orders the table by z, then tile)
+    lu0 = (b % 8) * a.grpM + b / 8;
+    lu1 = lu0 + 1;
+    if (lu0 >= a.ngunits) return;
+    // a start-gated unit packs, signals, waits and fills its cone's ghost cells first -- here,
+    // before the march state below is live, so the production loop's registers are untouched
+    const GateUnit un = a.gunits[lu0];
+    if (un.pk >= 0) {
+      int X0, xw = 64, Y0, yext = WAVES * ROWS;
+      if (C::FOLD && un.tile >= a.ntxf * a.nty) {
+        const int f2 = un.tile - a.ntxf * a.nty;
+        X0 = a.ntxf * a.xstep - TL;
+        Y0 = a.ybase + 2 * f2 * a.ystep - TL;
+        xw = 32;
+        yext += a.ystep;
+      } else {
+        const int ntxe = C::FOLD ? a.ntxf : a.ntx;
+        X0 = (un.tile % ntxe) * a.xstep - TL;
+        Y0 = a.ybase + (un.tile / ntxe) * a.ystep - TL;
+      }
+      gate_start<T>(a, un.pk, X0, xw, Y0, yext, un.z0 - TL, un.z1 + TL);
+    }
   }
   FusedState<C> S;
   // a wave that skips a level still publishes that level's (never used) rows: keep them defined
@@ -836,6 +893,10 @@ __global__ __launch_bounds__(64 * C::WAVES, C::WPEU) void k_fused(const typename
       const int64_t U = a.units;
       u = (int64_t)blockIdx.x * U / gridDim.x;
       uend = (int64_t)(blockIdx.x + 1) * U / gridDim.x;
+    } else if (GATED) {
+      const GateUnit un = a.gunits[lu];
+      u = (int64_t)un.tile * nzv + (un.z0 - a.zlo[0]);
+      uend = (int64_t)un.tile * nzv + (un.z1 - a.zlo[0]);
     } else {
       const int chunk = lu / a.ntiles, tile = lu % a.ntiles;
       u = (int64_t)tile * nzv + (int64_t)chunk * nzv / a.nchunk;
@@ -937,6 +998,22 @@ __global__ __launch_bounds__(64 * C::WAVES, C::WPEU) void k_fused(const typename
   }  // work list
 }
 
+template <class C, typename T>
+__global__ __launch_bounds__(64 * C::WAVES, C::WPEU) void k_fused(const typename C::V2* __restrict__ s,
+                                                            typename C::V2* __restrict__ d,
+                                                            FusedArgs a, FoldCoef<T> f,
+                                                            uint64_t seed) {
+  fused_body<C, T, false>(s, d, a, f, seed);
+}
+
+// the gated pass's entry (gate.hpp): instantiated for the shapes FCfg::GATE_OK names only
+template <class C, typename T>
+__global__ __launch_bounds__(64 * C::WAVES, C::WPEU) void k_fused_gated(
+    const typename C::V2* __restrict__ s, typename C::V2* __restrict__ d, FusedArgs a,
+    FoldCoef<T> f, uint64_t seed) {
+  fused_body<C, T, true>(s, d, a, f, seed);
+}
+
 // ------------------------------------------------------------------------------------------
 inline int& fused_sched_slot();
 
@@ -966,6 +1043,15 @@ struct FusedLaunch {
     }
     return occ;
   }
+  // resident workgroups per CU of the gated entry (the host sizes a gated table to these slots)
+  static int gated_occupancy() {
+    int o = 0;
+    if constexpr (C::GATE_OK)
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k_fused_gated<C, T>, 64 * C::WAVES, 0) !=
+          hipSuccess)
+        o = 0;
+    return o;
+  }
   static void run(const void* s, void* d, const FusedArgs& a0, const gs::Params& p,
                   hipStream_t st) {
     FusedArgs a = a0;
@@ -984,6 +1070,17 @@ struct FusedLaunch {
       int dev = 0;
       (void)hipGetDevice(&dev);
       if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+    }
+    if (a.sched == 3) {
+      // gated pass: the table holds one unit per workgroup (sized by the host to the slots)
+      if constexpr (C::GATE_OK) {
+        a.nchunk = 1;
+        a.grpM = (a.ngunits + 7) / 8;
+        const FoldCoef<T> f = make_fold<T>(p);
+        k_fused_gated<C, T><<<(unsigned)(8 * a.grpM), 64 * C::WAVES, 0, st>>>(
+            (const typename C::V2*)s, (typename C::V2*)d, a, f, p.seed);
+      }
+      return;  // (gated_shape_cfg never names a shape without the gated entry)
     }
     const int64_t slots = std::max<int64_t>(1, (int64_t)occupancy() * cus - a.reserve);
     // enough planes per workgroup to amortise the 2T-plane pipeline fill, but at least one
@@ -1286,6 +1383,24 @@ void run_fused_tl(const void* s, void* d, const FusedArgs& a, const gs::Params& 
   }
 }
 
+// resident workgroups per CU of the gated entry that gated_shape_cfg names for depth n (0: none)
+template <typename T>
+int fused_gated_occupancy(int cfg, int n) {
+  auto one = [&](auto tl) -> int {
+    constexpr int TL = decltype(tl)::value;
+    if constexpr (sizeof(T) == 8) {
+      return FusedLaunch<FCfg<T, TL, 4, 8, 1, false, true, true, true>, T>::gated_occupancy();
+    } else {
+      if (cfg == fused_cfg_lookup("4x12:1sf"))
+        return FusedLaunch<FCfg<T, TL, 4, 12, 1, false, true, true, true, 0, true>, T>::gated_occupancy();
+      return FusedLaunch<FCfg<T, TL, 4, 12, 1, false, true, true>, T>::gated_occupancy();
+    }
+  };
+  if (n == 2) return one(std::integral_constant<int, 2>{});
+  if (n == 3) return one(std::integral_constant<int, 3>{});
+  return 0;
+}
+
 inline bool fused_supported(const Geom& g, int n) {
   if (n < 2 || n > 3 || g.H < n) return false;
   return !(g.periodic && (g.Ly % 4 != 0));  // noise quads would straddle the wrap
@@ -1299,11 +1414,87 @@ inline bool philox_q32(const Geom& g) {
 
 // cfg / sched < 0: the process-wide selection (GS_FUSED_CFG / GS_FUSED_SCHED or the
 // gs_fused_select / gs_fused_sched APIs).
+// a gated pass's launch (sched 3): the unit table and transport state (gate.hpp)
+struct GateLaunch {
+  const GateUnit* units;
+  int32_t nunits;
+  const GateArgs* gate;
+  uint64_t n;
+  uint32_t cnt;
+  int32_t npk;
+};
+
+// The tile grid a configuration's launch enumerates (FusedLaunch::run + fold_strip), on the host:
+// the gated pass's unit table names tiles by this enumeration.
+struct TileGrid {
+  int xstep, ystep, ybase, ntx, nty, ntxf, nfold, ntiles, rt;
+};
+// the configuration run_fused_cfg actually launches for table entry cfg (variants exist for the
+// non-periodic, noisy, 32-bit-counter production path only; everything else runs the default)
+inline const char* fused_shape_name(int cfg, bool f64, bool variants) {
+  int nt = 0;
+  const FusedCfgEntry* tab = fused_cfg_table(&nt);
+  const char* dflt = f64 ? "4x8:1s" : "4x12:2s";
+  if (!variants || cfg <= 0 || cfg >= nt || fused_cfg_is_block(cfg)) return dflt;
+  if (!(f64 ? tab[cfg].f64 : tab[cfg].f32)) return dflt;
+  return tab[cfg].name;
+}
+// the configuration a gated pass launches (FCfg::GATE_OK shapes only): fp32 the folded 4x12:1sf
+// where the last x strip folds, else 4x12:1s; fp64 the default 4x8:1s
+inline int gated_shape_cfg(bool f64, const Geom& g, int n) {
+  if (f64) return 0;
+  const int k = fused_cfg_lookup("4x12:1sf");
+  return fused_cfg_applies(k, g, n) ? k : fused_cfg_lookup("4x12:1s");
+}
+inline TileGrid fused_tile_grid(const char* name, const Geom& g, int n) {
+  TileGrid t{};
+  const int rows = atoi(name);
+  const char* xp = strchr(name, 'x');
+  const int waves = xp ? atoi(xp + 1) : 12;
+  const size_t len = strlen(name);
+  const bool fold = len > 0 && name[len - 1] == 'f';
+  t.rt = rows * waves;
+  t.xstep = 64 - 2 * n;
+  t.ystep = (t.rt - 2 * n) & ~3;
+  t.ybase = -mod4(g.oy - n);
+  t.ntx = (g.nx + t.xstep - 1) / t.xstep;
+  t.nty = (g.ny - t.ybase + t.ystep - 1) / t.ystep;
+  t.ntxf = t.ntx;
+  t.nfold = 0;
+  t.ntiles = t.ntx * t.nty;
+  const int rem = g.nx - (t.ntx - 1) * t.xstep;
+  if (fold && t.ntx >= 2 && rem <= 32 - 2 * n) {
+    t.ntxf = t.ntx - 1;
+    t.nfold = (t.nty + 1) / 2;
+    t.ntiles = t.ntxf * t.nty + t.nfold;
+  }
+  return t;
+}
+// level-0 read window of tile `tile` in x / y: [X0, X0 + xw) x [Y0, Y0 + yext)
+inline void tile_window(const TileGrid& t, int tile, int n, int* X0, int* xw, int* Y0, int* yext) {
+  int tx, ty;
+  if (t.nfold && tile >= t.ntxf * t.nty) {
+    const int f = tile - t.ntxf * t.nty;
+    tx = t.ntxf;
+    ty = 2 * f;
+    *xw = 32;
+    *yext = t.rt + t.ystep;
+  } else {
+    tx = tile % t.ntxf;
+    ty = tile / t.ntxf;
+    *xw = 64;
+    *yext = t.rt;
+  }
+  *X0 = tx * t.xstep - n;
+  *Y0 = t.ybase + ty * t.ystep - n;
+}
+
 template <typename T>
 bool launch_fused(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, const Geom& g,
                   const gs::Params& p, int n, int64_t t, hipStream_t st, int cfg = -1,
                   int sched = -1, int zlo0 = 0, int zlen0 = -1, int zlo1 = 0, int zlen1 = 0,
-                  int reserve = 0, int mask = 0, bool allow_block = false) {
+                  int reserve = 0, int mask = 0, bool allow_block = false,
+                  const GateLaunch* gate = nullptr) {
   if (!fused_supported(g, n)) return false;
   FusedArgs a{};
   a.allow_block = allow_block ? 1 : 0;
@@ -1331,6 +1522,20 @@ bool launch_fused(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, co
   a.cfg = cfg >= 0 ? cfg : fused_cfg_env();
   a.sched = sched >= 0 ? sched : fused_sched_slot();
   if (zlen1) a.sched = 0;  // two short runs: one workgroup per (tile, run)
+  if (gate) {
+    if (zlo0 != 0 || zlen0 != g.nz || zlen1 || mask || !gate->units || gate->nunits < 1) return false;
+    a.sched = 3;
+    a.gunits = gate->units;
+    a.ngunits = gate->nunits;
+    a.gate = gate->gate;
+    a.field = const_cast<typename Vec2<T>::type*>(s);
+    a.gate_n = gate->n;
+    a.gate_cnt = gate->cnt;
+    a.gate_npk = gate->npk;
+    a.allow_block = 0;
+  } else if (a.sched == 3) {
+    a.sched = 2;  // the gated schedule needs its table
+  }
   a.bcfix = g.periodic ? 0 : 1;
   if (n == 2) run_fused_tl<T, 2>(s, d, a, p, st);
   else run_fused_tl<T, 3>(s, d, a, p, st);

@@ -1,0 +1,246 @@
+// SPDX-License-Identifier: MIT
+// Gated pass: the halo exchange carried inside the k_fused launch of the pass (IPC transport).
+// Included inside namespace gsk at the end of kernels.hpp (it uses store_system and the IPC
+// wall clock of the pack / wait kernels above).
+//
+// The reference exchanges every halo with blocking host Sendrecv! calls and only then computes
+// (src/simulation/public.jl:58-64, communication.jl:138-199).  The stream-overlapped pass
+// (engine.h: inner launch + k_slab shell) hides the exchange but recomputes the k-deep face
+// slabs in a second, latency-bound launch: ~1.4x the full pass on a 2x2x2 rank
+// (profiles/r4_shell.txt).  Here a pass is one launch and every output is computed once:
+//   * the host splits each tile column into z-chunks, one unit per workgroup (GateUnit);
+//     a unit whose level-0 cone reads a ghost cell that a neighbour fills is START-GATED, every
+//     other unit marches at once;
+//   * start-gated units are the packers: each copies its share of every outgoing message
+//     straight into the receiving peer's landing buffer (IPC-mapped; system-coherent stores
+//     across devices), waits for its stores to be acknowledged and bumps a device counter; the
+//     packer whose add completes the pass's count publishes this exchange's sequence number in
+//     every send peer's flag array;
+//   * then each start-gated unit polls its own flags until every receive peer has published
+//     (a wall-clock bound turns a dead peer into an error, not a hang), copies the ghost cells
+//     of its own cone out of its landing slot (cones of neighbouring tiles overlap: a few cells
+//     are copied twice, with equal values) and marches;
+//   * the host sizes the chunks so that every workgroup finishes together: gated chunks are
+//     shorter by the expected exchange time (tuned on the device, backend_hip.hip gate_tune).
+// The same monotonic flags and two landing slots as the stream transport (backend_hip.hip
+// ipc_*): exchange n uses slot n & 1; a rank starts packing n only after its previous launch,
+// whose gated units waited for every peer's n - 1, so the peers have consumed slot n & 1 (their
+// launch n - 2 read it).  Results are bit-identical to the full pass: the arithmetic is k_fused's,
+// and chunking never changes a value.
+#pragma once
+
+struct GateArgs {
+  // outgoing messages: boxes (local interior cells), destination in the receiving peer's landing
+  // slot 0 / 1 (mapped into this process), bit m of sysmask: system-coherent stores
+  Box sbox[gs::kMaxMsgs];
+  void* sdst[2][gs::kMaxMsgs];
+  int32_t nsend;
+  uint32_t sysmask;
+  // incoming messages: ghost boxes (local), their data in this rank's landing slot 0 / 1
+  Box rbox[gs::kMaxMsgs];
+  const void* rsrc[2][gs::kMaxMsgs];
+  int32_t nrecv;
+  // sequence flags: this rank's (one per receive peer) and the peers' (one per send peer)
+  uint64_t* wflag[gs::kMaxMsgs];
+  uint64_t* sflag[gs::kMaxMsgs];
+  int32_t nwait, nsig;
+  uint32_t* counter;   // packer arrivals, monotonic over the engine's gated passes
+  uint64_t ticks;      // wall-clock ticks a wait may take (GS_COMM_TIMEOUT)
+  uint64_t min_ticks;  // debug knob ipc_emulate_us: the exchange lasts at least this long
+  int* err;            // host-mapped: a wait timed out (the watchdog raises)
+  int* dflag;          // device copy: later copies write NaN instead of stale landing data
+  // debug knob gate_stamps: wall-clock stamps of the launch's exchange (null: none) --
+  // [0] min start, [1] max packer arrival, [2] min / [3] max wait done, [4] max unpack done
+  unsigned long long* stamps;
+};
+
+// One message (pack) or the part of one inside a unit's cone (unpack), flattened: the pieces
+// of all messages form one index space [0, total), so a thread's cells of EVERY message are in
+// flight before its first store.  (On gfx9 the vector memory counter covers loads and stores and
+// retires in order: a loop of load -> store per message waits one uncached store / load round
+// trip per message -- 26 messages cost 45 us of packing and 25 us of unpacking that way.)
+struct GatePiece {
+  void* ptr;          // pack: the message's destination; unpack: its data in the landing slot
+  int x0, y0, z0;     // first cell (local coordinates)
+  int nx, ny;         // extent in x / y (z: until the next piece's start)
+  uint32_t start;     // first flat index
+  int sx0, sy0, sz0;  // unpack: origin of the message box in the landing slot
+  int snx, sny;       //         and its x / y extent
+  int sys;            // pack: system-coherent stores (a peer on another GPU)
+};
+
+template <typename T>
+constexpr int gate_batch() { return sizeof(T) == 4 ? 16 : 8; }  // cells per thread per batch
+
+template <typename T>
+__device__ __forceinline__ void gate_start(const FusedArgs& a, int pk, int X0, int xw, int Y0,
+                                        int yext, int za, int zb) {
+  using V2 = typename Vec2<T>::type;
+  constexpr int B = gate_batch<T>();
+  const GateArgs& G = *a.gate;
+  const Geom& g = a.g;
+  const int slot = (int)(a.gate_n & 1);
+  const uint32_t nt = blockDim.x, tid = threadIdx.x;
+  const uint64_t t0 = wall_clock64();
+  V2* f = (V2*)a.field;
+  __shared__ GatePiece gp[gs::kMaxMsgs];
+  __shared__ uint32_t gcells[gs::kMaxMsgs];
+  __shared__ uint32_t gtotal;
+  __shared__ int gnp;
+  // the piece table: one thread per message (their loads of the arguments in parallel), then
+  // thread 0 numbers the cells (and drops empty pieces) in LDS
+  auto number = [&](int nmsg) {
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t acc = 0;
+      int np = 0;
+      for (int m = 0; m < nmsg; ++m) {
+        if (!gcells[m]) continue;
+        if (np != m) gp[np] = gp[m];
+        gp[np++].start = acc;
+        acc += gcells[m];
+      }
+      gtotal = acc;
+      gnp = np;
+    }
+    __syncthreads();
+  };
+  // 1. this packer's share of the outgoing messages: flat cells pk * nt + tid, strided by all
+  // packers' threads
+  if (tid < (uint32_t)G.nsend) {
+    const Box b = G.sbox[tid];
+    gp[tid] = GatePiece{G.sdst[slot][tid], b.x0, b.y0, b.z0, b.nx, b.ny, 0u, 0, 0, 0, 0, 0,
+                        (int)((G.sysmask >> tid) & 1u)};
+    gcells[tid] = (uint32_t)gs::box_cells(b);
+  }
+  number(G.nsend);
+  {
+    const uint32_t total = gtotal, stride = (uint32_t)a.gate_npk * nt;
+    const int np = gnp;
+    for (uint32_t i0 = (uint32_t)pk * nt + tid; i0 < total; i0 += B * stride) {
+      V2 c[B];
+      V2* dst[B];
+      int sys[B];
+      int m = 0;
+#pragma unroll
+      for (int j = 0; j < B; ++j) {
+        const uint32_t i = i0 + (uint32_t)j * stride;
+        dst[j] = nullptr;
+        if (i < total) {
+          while (m + 1 < np && gp[m + 1].start <= i) ++m;  // i grows with j
+          const GatePiece& q = gp[m];
+          const uint32_t k = i - q.start;
+          const uint32_t r = k / (uint32_t)q.nx;
+          const uint32_t z = r / (uint32_t)q.ny;
+          const int x = (int)(k - r * (uint32_t)q.nx), y = (int)(r - z * (uint32_t)q.ny);
+          c[j] = f[gs::lin(g, q.x0 + x, q.y0 + y, q.z0 + (int)z)];
+          dst[j] = (V2*)q.ptr + k;
+          sys[j] = q.sys;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < B; ++j) {
+        if (!dst[j]) continue;
+        if (sys[j]) store_system(dst[j], c[j]);
+        else *dst[j] = c[j];
+      }
+    }
+  }
+  // every wave's stores acknowledged (uncached or system-coherent: no cache holds them), then
+  // one arrival per packer; the last one publishes the exchange.  No release fence: on gfx950 a
+  // system-scope release writes back the XCD's whole L2 (buffer_wbl2), here full of the marching
+  // workgroups' output lines -- and nothing it would write back is part of a message: every
+  // packer's landing stores are already acknowledged when its arrival is counted, and the flag
+  // store issues after the count (the same ordering as the stream path's pack / signal kernels)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    if (G.stamps) {
+      atomicMin(G.stamps + 0, (unsigned long long)t0);
+      atomicMax(G.stamps + 1, (unsigned long long)wall_clock64());
+    }
+    const uint32_t old = __hip_atomic_fetch_add(G.counter, 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+    if (old + 1u == a.gate_cnt)
+      for (int i = 0; i < G.nsig; ++i)
+        __hip_atomic_store(G.sflag[i], a.gate_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  // 2. every receive peer's messages of this exchange have landed (bounded wait).  Relaxed
+  // system-scope polls (the flags are uncached: every load reads memory).  No acquire fence (on
+  // gfx950 an agent-scope acquire invalidates the XCD's L2, which the marching workgroups
+  // stream through): the landing slot is uncached too, so no cache can hold a stale copy of
+  // the messages, and the copies below issue only after the polls return.
+  if (tid < (uint32_t)G.nwait) {
+    uint64_t* w = G.wflag[tid];
+    while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < a.gate_n) {
+      if (wall_clock64() - t0 > G.ticks) {
+        __hip_atomic_store(G.dflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(G.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  if (G.min_ticks && tid == 0)
+    while (wall_clock64() - t0 < G.min_ticks) __builtin_amdgcn_s_sleep(1);
+  if (G.stamps && tid == 0) {
+    const unsigned long long w = (unsigned long long)wall_clock64();
+    atomicMin(G.stamps + 2, w);
+    atomicMax(G.stamps + 3, w);
+  }
+  __syncthreads();
+  // 3. the ghost cells of this unit's level-0 cone [X0, X0 + xw) x [Y0, Y0 + yext) x [za, zb):
+  // the cone's part of every received message, one flat index space again
+  const bool poison = __hip_atomic_load(G.dflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+  if (tid < (uint32_t)G.nrecv) {
+    const Box b = G.rbox[tid];
+    const int x0 = max(b.x0, X0), x1 = min(b.x0 + b.nx, X0 + xw);
+    const int y0 = max(b.y0, Y0), y1 = min(b.y0 + b.ny, Y0 + yext);
+    const int z0 = max(b.z0, za), z1 = min(b.z0 + b.nz, zb);
+    const bool any = x0 < x1 && y0 < y1 && z0 < z1;
+    gp[tid] = GatePiece{const_cast<void*>(G.rsrc[slot][tid]), x0, y0, z0, x1 - x0, y1 - y0, 0u,
+                        b.x0, b.y0, b.z0, b.nx, b.ny, 0};
+    gcells[tid] = any ? (uint32_t)((x1 - x0) * (y1 - y0) * (z1 - z0)) : 0u;
+  }
+  number(G.nrecv);
+  {
+    const uint32_t total = gtotal;
+    const int np = gnp;
+    for (uint32_t i0 = tid; i0 < total; i0 += B * nt) {
+      V2 c[B];
+      int64_t o[B];
+      int p = 0;
+#pragma unroll
+      for (int j = 0; j < B; ++j) {
+        const uint32_t i = i0 + (uint32_t)j * nt;
+        o[j] = -1;
+        if (i < total) {
+          while (p + 1 < np && gp[p + 1].start <= i) ++p;
+          const GatePiece& q = gp[p];
+          const uint32_t k = i - q.start;
+          const uint32_t r = k / (uint32_t)q.nx;
+          const uint32_t zz = r / (uint32_t)q.ny;
+          const int x = q.x0 + (int)(k - r * (uint32_t)q.nx);
+          const int y = q.y0 + (int)(r - zz * (uint32_t)q.ny);
+          const int z = q.z0 + (int)zz;
+          c[j] = ((const V2*)q.ptr)[((int64_t)(z - q.sz0) * q.sny + (y - q.sy0)) * q.snx +
+                                   (x - q.sx0)];
+          o[j] = gs::lin(g, x, y, z);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < B; ++j) {
+        if (o[j] < 0) continue;
+        V2 v = c[j];
+        if (poison) v.x = v.y = __builtin_nan("");
+        f[o[j]] = v;
+      }
+    }
+  }
+  // the march's loads (other waves' cells too) come after every wave's ghost stores; and this
+  // CU's L1 forgets the lines the packing loaded: an interior cache line next to a face also
+  // holds ghost cells, stale ones from before the copies above (buffer_inv sc0: L1 only)
+  asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
+  __syncthreads();
+  if (G.stamps && tid == 0) atomicMax(G.stamps + 4, (unsigned long long)wall_clock64());
+}

@@ -6,5 +6,7 @@
 namespace gsk {
 template bool launch_fused<float>(const typename Vec2<float>::type*, typename Vec2<float>::type*,
                                const Geom&, const gs::Params&, int, int64_t, hipStream_t, int,
-                               int, int, int, int, int, int, int, bool);
+                               int, int, int, int, int, int, int, bool,
+                               const GateLaunch*);
+template int fused_gated_occupancy<float>(int, int);
 }  // namespace gsk

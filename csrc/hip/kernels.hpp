@@ -441,4 +441,6 @@ void launch_stats(const typename Vec2<T>::type* f, const Geom& g, double* ws, in
   k_stats<T><<<blocks, 256, 0, st>>>(f, g, ws);
 }
 
+#include "gate.hpp"
+
 }  // namespace gsk

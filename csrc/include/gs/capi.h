@@ -25,6 +25,8 @@ int gs_set_overlap(gs_engine* e, int32_t mode);  // -1 auto, 0 off, 1 on
 int gs_set_loopback(gs_engine* e, int32_t on);  // self messages via the device transport
 int gs_overlapped(gs_engine* e, int32_t k);      // 1 if a k-step pass overlaps its exchange
 int gs_chained(gs_engine* e, int32_t k);         // 1 if runs of k-step passes are chained on two streams
+int gs_set_gated(gs_engine* e, int32_t on);      // allow (1) / forbid (0) gated passes
+int gs_gated(gs_engine* e, int32_t k);           // 1 if k-step passes carry the exchange in-kernel (gate.hpp)
 int gs_depth(gs_engine* e);                      // steps per pass (fuse, or the measured depth)
 int gs_set_auto_depth(gs_engine* e, int32_t on);  // let prepare() pick the depth (single rank)
 int gs_plan_zplanes(gs_engine* e);               // 1 if halos are whole contiguous z planes

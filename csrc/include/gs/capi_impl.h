@@ -69,6 +69,11 @@ int gs_set_overlap(gs_engine* e, int32_t mode) { GS_TRY(e->eng->set_overlap(mode
 int gs_set_loopback(gs_engine* e, int32_t on) { GS_TRY(e->eng->set_loopback(on != 0)) }
 int gs_overlapped(gs_engine* e, int32_t k) { return e->eng->overlapped(k) ? 1 : 0; }
 int gs_chained(gs_engine* e, int32_t k) { return e->eng->chained(k) ? 1 : 0; }
+int gs_gated(gs_engine* e, int32_t k) { return e->eng->gated(k) ? 1 : 0; }
+int gs_set_gated(gs_engine* e, int32_t on) {
+  e->eng->set_gated(on != 0);
+  return 0;
+}
 int gs_depth(gs_engine* e) { return e->eng->depth(); }
 int gs_set_auto_depth(gs_engine* e, int32_t on) { GS_TRY(e->eng->set_auto_depth(on != 0)) }
 int gs_plan_zplanes(gs_engine* e) { return e->eng->plan().zplanes; }

@@ -12,6 +12,16 @@
 //   ipc_system_stores 0 (default); 1: the IPC pack stores every peer-bound message with system
 //                   coherence, as it always does for a peer on another GPU (tests of that path
 //                   on one GPU).
+//   gated           1 (default): full-depth passes over the IPC transport run gated (the exchange
+//                   inside the pass's fused launch, csrc/hip/gate.hpp) when every peer runs on
+//                   another GPU (or is this rank: loopback); 0: the stream-overlapped /
+//                   sequential paths (tests, A/B); 2: also with peer processes on this GPU (tests:
+//                   each rank's table then takes its share of the device's workgroup slots, so
+//                   every rank's waiting units fit at once).  Read when an engine is created.
+//   gate_stamps     0 (default); 1: gated passes record wall-clock stamps of their exchange (first
+//                   packer start, last arrival, first / last wait done, last unpack done; read
+//                   back by gs_gate_stamps -- scripts/bench_gated.py).  Read when the IPC
+//                   transport connects.
 //   cpu_ftz         1 (default): the CPU solver flushes fp32 denormals in its step region
 //                   (MXCSR FTZ + DAZ; ~100x faster where the reference example's v field
 //                   passes through them); 0: IEEE denormals, the reference's and the GPU's
@@ -27,7 +37,9 @@ struct DebugKnobs {
   int philox_generic = 0;
   double ipc_emulate_us = 0.0;
   int ipc_system_stores = 0;
+  int gate_stamps = 0;
   int cpu_ftz = 1;
+  int gated = 1;
 };
 
 inline DebugKnobs& debug_knobs() {
@@ -43,7 +55,9 @@ inline int debug_set(const char* name, double value) {
   else if (!strcmp(name, "philox_generic")) k.philox_generic = value != 0.0 ? 1 : 0;
   else if (!strcmp(name, "ipc_emulate_us")) k.ipc_emulate_us = value > 0.0 ? value : 0.0;
   else if (!strcmp(name, "ipc_system_stores")) k.ipc_system_stores = value != 0.0 ? 1 : 0;
+  else if (!strcmp(name, "gate_stamps")) k.gate_stamps = value != 0.0 ? 1 : 0;
   else if (!strcmp(name, "cpu_ftz")) k.cpu_ftz = value != 0.0 ? 1 : 0;
+  else if (!strcmp(name, "gated")) k.gated = value >= 2.0 ? 2 : (value != 0.0 ? 1 : 0);
   else return -1;
   return 0;
 }

@@ -80,6 +80,17 @@ class Backend {
     (void)src; (void)dst; (void)n; (void)t; (void)sides; (void)variant;
     return false;
   }
+  // Gated pass (device transport with in-kernel exchange, csrc/hip/gate.hpp): one launch per
+  // pass that packs, signals, waits and unpacks inside the fused kernel.  gated_supported: this
+  // backend can run depth-n passes that way now (IPC transport set up, a landing route for
+  // every message); prepare_gated: tune it (every rank the same passes); fused_gated: one pass
+  // src -> dst including the halo exchange of src.
+  virtual bool gated_supported(int n) const { (void)n; return false; }
+  virtual void prepare_gated(int src, int dst, int n, int64_t t) { (void)src; (void)dst; (void)n; (void)t; }
+  virtual bool fused_gated(int src, int dst, int n, int64_t t) {
+    (void)src; (void)dst; (void)n; (void)t;
+    return false;
+  }
   // in-place transport of a zplanes plan straight from / into field buffer b (no pack)
   virtual bool native_exchange_inplace(int b, const HaloPlan& p) { (void)b; (void)p; return false; }
   // asynchronous communication stream.  comm_fork: the comm stream waits for the compute
@@ -250,6 +261,11 @@ class Engine {
     if (!cfg_.use_fused) return;
     for (int n = 2; n <= cfg_.fuse; ++n) {
       be_->prepare_fused(cur_, 1 - cur_, n, t_);
+      if (gated(n)) {
+        // the gated pass's table and expected exchange time (every rank the same passes)
+        be_->prepare_gated(cur_, 1 - cur_, n, t_);
+        continue;
+      }
       // tune the overlapped passes' post-exchange launches now too (their first call times
       // the candidates), so no tuning lands inside a timed region; all on the compute stream
       if (overlapped(n)) {
@@ -396,6 +412,18 @@ class Engine {
     bc_parity_[b] = par;
   }
 
+  // whether full-depth passes run gated: the exchange inside the pass's fused launch
+  // (gate.hpp; the IPC transport).  Taken before the stream-overlapped modes; the debug knob
+  // gated = 0 (tests, A/B) or overlap off disable it.
+  bool gated(int k) const {
+    return gate_ && overlap_ != 0 && cfg_.use_fused && k > 1 && has_remote_ && tfn_ == nullptr &&
+           be_->gated_supported(k);
+  }
+
+  // gated passes off for this engine (the ranks of a job agree: either every rank's passes
+  // carry the exchange in-kernel or none does -- models/grayscott.py)
+  void set_gated(bool on) { gate_ = on && debug_knobs().gated != 0; }
+
   // whether full-depth passes run as a chain on two streams (advance_chained): any device
   // transport (RCCL in place or packed, IPC peer writes) -- a host callback serialises anyway
   bool chained(int k) const {
@@ -416,6 +444,12 @@ class Engine {
     while (nsteps > 0) {
       const int k = (int)(nsteps < kmax ? nsteps : kmax);
       const int oth = 1 - cur_;
+      if (nsteps >= (int64_t)k && gated(k)) {  // (its passes are counted inside)
+        const int64_t npass = nsteps / k;
+        advance_gated(k, npass);
+        nsteps -= npass * k;
+        continue;
+      }
       if (nsteps >= 2 * (int64_t)k && chained(k)) {  // (its passes are counted inside)
         const int64_t npass = nsteps / k;
         advance_chained(k, npass);
@@ -483,6 +517,27 @@ class Engine {
   }
 
  private:
+  // Gated passes: one fused launch per pass carries the halo exchange (gate.hpp).  Both buffers'
+  // outer ghosts are set up front (their time parities stay fixed while k does), so a pass is
+  // exactly one launch on the compute stream: no pack / unpack kernels, no comm stream, no
+  // cross-stream event.
+  void advance_gated(int k, int64_t npass) {
+    ensure_bc(cur_, t_);
+    ensure_bc(1 - cur_, t_ + k);
+    for (int64_t p = 0; p < npass; ++p) {
+      const int oth = 1 - cur_;
+      plog_.begin_pass(k);
+      TraceRange tr("gs.fused_gated");
+      pm(kPhFused, true);
+      if (!be_->fused_gated(cur_, oth, k, t_))
+        throw std::runtime_error("gated pass: the backend refused the launch");
+      pm(kPhFused, false);
+      ++ncomm_;
+      cur_ = oth;
+      t_ += k;
+    }
+  }
+
   // Chained overlapped passes over a device transport (RCCL).  The critical chain -- halo
   // exchange of pass p, then its post-exchange launches (z end slabs, ring tiles), then the
   // exchange of pass p+1 -- stays on the comm stream with no cross-stream hop; the inner part
@@ -590,6 +645,8 @@ class Engine {
   bool loopback_ = false;
   // debug knob overlap_chain = 0 (tests): overlapped passes one by one (gs/debug.h)
   bool chain_ = debug_knobs().overlap_chain != 0;
+  // debug knob gated = 0 (tests, A/B): no gated passes (gs/debug.h)
+  bool gate_ = debug_knobs().gated != 0;
   enum { kNone, kUnpack, kCallback };
   int xpending_ = kNone;
   int cur_ = 0;

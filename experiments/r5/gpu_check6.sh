@@ -1,0 +1,11 @@
+# Round 5, lease 6: gated passes without the L2-wide fences -- correctness, then the cost.
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/${GS_OUT:-r5c6}
+mkdir -p $O
+cd $R
+export TMPDIR=/tmp
+export GS_COMM_TIMEOUT=60
+timeout -k 10 600 python -u -m pytest tests/test_gpu_gated.py -m gpu -x -v --timeout 240 --timeout-method thread > $O/tests.log 2>&1 &&
+timeout -k 10 400 python -u scripts/bench_gated.py --n 256 --k 3 2 --out $O/gated.json > $O/gated.log 2>&1
+echo "exit $?"

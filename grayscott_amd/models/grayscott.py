@@ -207,6 +207,13 @@ class GrayScott:
             # also: no rank stores into a peer's landing buffer before every rank has mapped
             if self.ctx.allreduce(0.0 if err else 1.0, "min") <= 0:
                 raise RuntimeError(f"ipc transport set-up failed on some rank: {err}")
+            # gated passes (gate.hpp) on every rank or on none: a rank whose sub-domain cannot
+            # run them (too few planes, a peer it cannot map) keeps the stream-overlapped passes,
+            # and so must every peer -- the tuning passes and exchange counts must match
+            if self.ctx.is_distributed:
+                g = self.engine.gated(self.engine.depth())
+                if self.ctx.allreduce(1.0 if g else 0.0, "min") <= 0:
+                    self.engine.set_gated(False)
         elif kind in ("torch", "host"):
             stage = kind == "host" and self.backend == "hip"
             group = self.ctx.nccl_group() if (self.backend == "hip" and not stage) else None
@@ -235,8 +242,15 @@ class GrayScott:
 
     @property
     def overlapped(self) -> bool:
-        """Whether full-depth passes overlap their halo exchange with the inner planes."""
-        return self.engine.overlapped(self.fuse)
+        """Whether full-depth passes overlap their halo exchange with the update: gated (the
+        exchange inside the pass's fused launch) or stream-overlapped (inner part + shell)."""
+        return self.engine.gated(self.fuse) or self.engine.overlapped(self.fuse)
+
+    @property
+    def gated(self) -> bool:
+        """Whether full-depth passes carry the halo exchange inside their fused launch (the IPC
+        transport, csrc/hip/gate.hpp): pack, signal, wait and unpack in the kernel."""
+        return self.engine.gated(self.fuse)
 
     @property
     def depth(self) -> int:

@@ -77,6 +77,10 @@ def _declare(lib) -> None:
     lib.gs_overlapped.restype = c_int
     lib.gs_chained.argtypes = [c_void_p, c_int32]
     lib.gs_chained.restype = c_int
+    lib.gs_gated.argtypes = [c_void_p, c_int32]
+    lib.gs_gated.restype = c_int
+    lib.gs_set_gated.argtypes = [c_void_p, c_int32]
+    lib.gs_set_gated.restype = c_int
     lib.gs_depth.argtypes = [c_void_p]
     lib.gs_depth.restype = c_int
     lib.gs_set_auto_depth.argtypes = [c_void_p, c_int32]
@@ -274,6 +278,39 @@ class Engine:
 
     def chained(self, k: int) -> bool:
         return bool(self.lib.gs_chained(self.h, int(k)))
+
+    def gated(self, k: int) -> bool:
+        """Whether k-step passes carry the halo exchange inside their fused launch (gate.hpp)."""
+        return bool(self.lib.gs_gated(self.h, int(k)))
+
+    def gate_stamps(self):
+        """Debug knob gate_stamps: the last gated launch's exchange in µs after its first packer
+        started -- {"packed", "first_wait_done", "last_wait_done", "unpacked"}, or None."""
+        if not hasattr(self.lib, "gs_gate_stamps"):
+            return None
+        out = (c_double * 4)()
+        self.lib.gs_gate_stamps.argtypes = [c_void_p, c_int32, POINTER(c_double)]
+        self.lib.gs_gate_stamps.restype = c_int
+        if self.lib.gs_gate_stamps(self.h, DTYPE_CODES[self.dtype], out) != 0 or out[0] < 0:
+            return None
+        return dict(zip(("packed", "first_wait_done", "last_wait_done", "unpacked"),
+                        (round(float(x), 2) for x in out)))
+
+    def set_gated(self, on: bool):
+        """Allow / forbid gated passes on this engine (the job's ranks agree on it)."""
+        self._chk(self.lib.gs_set_gated(self.h, 1 if on else 0), "set_gated")
+
+    def gate_info(self, k: int):
+        """{"xp", "units", "packers", "ms"} of the tuned gated pass of depth k (HIP only), or None."""
+        if not hasattr(self.lib, "gs_gate_info"):
+            return None
+        out = (c_double * 4)()
+        self.lib.gs_gate_info.argtypes = [c_void_p, c_int32, c_int32, POINTER(c_double)]
+        self.lib.gs_gate_info.restype = c_int
+        if self.lib.gs_gate_info(self.h, int(k), DTYPE_CODES[self.dtype], out) != 0 or out[0] < 0:
+            return None
+        return {"xp": int(out[0]), "units": int(out[1]), "packers": int(out[2]),
+                "ms": round(float(out[3]), 5)}
 
     def set_auto_depth(self, on: bool):
         self._chk(self.lib.gs_set_auto_depth(self.h, 1 if on else 0), "set_auto_depth")

@@ -46,7 +46,8 @@ def kernels(text: str, everything: bool = False):
     out = []
     for r, d in zip(rows, dem):
         m = re.search(r"FCfg<(.*?)>", d)
-        out.append(((m.group(1) if m else d)[:80],) + r[1:])
+        tag = "G " if "k_fused_gated" in d else ""  # the gated pass's entry (gate.hpp)
+        out.append((((tag + m.group(1)) if m else d)[:80],) + r[1:])
     return out
 
 

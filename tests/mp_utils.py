@@ -34,6 +34,9 @@ def _worker(rank, world, port, outdir, cfg):
         from grayscott_amd.parallel.decomp import choose_dims, init_domain
         from grayscott_amd.utils.config import Settings
 
+        from grayscott_amd.ops import native
+        for name, value in (cfg.get("knobs") or {}).items():  # native test switches (gs/debug.h)
+            native.debug_set(name, value, "hip")
         settings = Settings(**cfg["settings"])
         backend = "hip" if settings.backend.lower() in ("amdgpu", "hip", "gpu") else "cpu"
         ctx = gdist.init_from_env(backend)
@@ -55,6 +58,7 @@ def _worker(rank, world, port, outdir, cfg):
         np.savez(os.path.join(outdir, f"rank{rank}.npz"), u=u, v=v, info=info,
                  offsets=np.array(dom.proc_offsets), sizes=np.array(dom.proc_sizes),
                  step=sim.step, transport=sim.transport, overlapped=sim.overlapped,
+                 gated=sim.gated, gate=json.dumps(sim.engine.gate_info(sim.engine.depth())),
                  profile=json.dumps(prof),
                  zplanes=sim.engine.plan()["zplanes"])
         sim.close()
@@ -91,6 +95,7 @@ def run_ranks(world: int, cfg: dict, timeout: float = 240.0):
             v[sl] = d["v"]
             meta.append({"step": int(d["step"]), "transport": str(d["transport"]),
                          "overlapped": bool(d["overlapped"]), "zplanes": bool(d["zplanes"]),
+                         "gated": bool(d["gated"]), "gate": __import__("json").loads(str(d["gate"])),
                          "info": __import__("json").loads(str(d["info"])),
                          "profile": __import__("json").loads(str(d["profile"]))})
         return u, v, meta

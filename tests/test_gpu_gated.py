@@ -1,0 +1,169 @@
+"""Gated passes on ONE MI355X: the IPC halo exchange carried inside the pass's fused launch
+(csrc/hip/gate.hpp, engine.h advance_gated, backend_hip.hip gate_*).
+
+Start-gated workgroups pack their share of every outgoing message into the peers' landing
+buffers, the last packer publishes the exchange, and each start-gated workgroup waits for its
+peers' flags and copies the ghost cells of its own cone before marching; every other workgroup
+marches at once.  Every result must be bit-identical to the single-rank run (and to the
+stream-overlapped passes, debug knob gated = 0): chunking a tile column into units never
+changes a value.  The reference's blocking exchange-then-compute step is
+src/simulation/public.jl:58-64.
+"""
+import numpy as np
+import pytest
+import torch
+
+from .mp_utils import run_ranks
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _cfg(L, steps, fuse, prec="Float32", knobs=None, **extra):
+    s = dict(L=L, precision=prec, F=0.02, k=0.048, dt=1.0, Du=0.2, Dv=0.1, noise=0.1,
+             backend="AMDGPU", seed=1234)
+    s.update(extra)
+    # gated = 2: gated passes although the ranks share this one GPU (each rank's unit table
+    # then takes its share of the device's workgroup slots)
+    return {"settings": s, "steps": steps, "fuse": fuse, "transport": "ipc",
+            "knobs": dict({"gated": 2}, **(knobs or {}))}
+
+
+def _single(L, steps, fuse, prec="Float32", random_init=None):
+    cfg = _cfg(L, steps, fuse, prec)
+    cfg.pop("transport")
+    if random_init is not None:
+        cfg["random_init"] = random_init
+    return run_ranks(1, cfg)
+
+
+@pytest.mark.parametrize("which,L,fuse,prec", [("z", 48, 3, "Float32"), ("yz", 40, 3, "Float32"),
+                                                ("yz", 36, 2, "Float64")])
+def test_gated_loopback(which, L, fuse, prec):
+    """One process, its halos sent to ITSELF through the landing buffer on a non-periodic
+    geometry (wraps as messages): z neighbours only, or the 8 directions with dx = 0 (faces,
+    edges) -- the same values as the same rank with device self copies.  (x wraps on a
+    non-periodic geometry are not a real configuration: the self-copy reference's small-grid
+    block kernel treats cells beyond the global x faces as boundary, so x messages are covered
+    by the multi-process tests below.)"""
+    import dataclasses
+
+    from grayscott_amd.models.grayscott import GrayScott
+    from grayscott_amd.parallel.decomp import init_domain
+    from grayscott_amd.utils.config import Settings
+
+    dom = init_domain(L, 1, 0, periodic=True)
+    nbr = list(dom.nbr27)
+    # index (dx + 1) * 9 + (dy + 1) * 3 + (dz + 1): keep dx = 0 (and dy = 0 for "z")
+    nbr = [r if i // 9 == 1 and (which != "z" or (i // 3) % 3 == 1) else -1
+           for i, r in enumerate(nbr)]
+    loop = dataclasses.replace(dom, periodic=False, nbr27=nbr)
+    s = Settings(L=L, precision=prec, F=0.02, k=0.048, dt=1.0, Du=0.2, Dv=0.1, noise=0.1,
+                 backend="AMDGPU", seed=99, overlap="on")
+    out = []
+    # the reference: the same wraps as device self copies (no loopback)
+    for kw in ({}, dict(transport="ipc", loopback=True)):
+        sim = GrayScott(s, loop, fuse=fuse, **kw)
+        try:
+            sim.init_fields()
+            sim.randomize_fields(seed=7)
+            sim.iterate(5 * fuse + 1)
+            sim.synchronize()
+            out.append(sim.get_fields() + (sim.gated, sim.engine.gate_info(fuse)))
+        finally:
+            sim.close()
+    (u0, v0, g0, _), (u1, v1, g1, info) = out
+    assert not g0 and g1 and info["units"] > 0 and info["packers"] > 0, info
+    assert np.isfinite(u1).all()
+    np.testing.assert_array_equal(u1, u0)
+    np.testing.assert_array_equal(v1, v0)
+
+
+@pytest.mark.parametrize("world,dims,L,fuse,prec", [
+    (2, [1, 1, 2], 48, 3, "Float32"),   # z slabs: whole-plane messages
+    (2, [2, 1, 1], 64, 3, "Float32"),   # x split: strip tiles start-gated over the whole column
+    (4, [2, 2, 1], 64, 2, "Float64"),
+    (8, [2, 2, 2], 64, 3, "Float32"),   # every face, edge and corner message
+    (3, [1, 1, 3], 40, 2, "Float32"),   # a middle rank with two receive peers
+])
+def test_gated_matches_single_rank(world, dims, L, fuse, prec):
+    steps = 4 * fuse + 1  # full gated passes and a trailing partial pass (stream exchange)
+    u1, v1, _ = _single(L, steps, fuse, prec, random_init=11)
+    cfg = _cfg(L, steps, fuse, prec, overlap="on")
+    cfg["dims"] = dims
+    cfg["random_init"] = 11
+    un, vn, meta = run_ranks(world, cfg)
+    assert all(m["transport"] == "ipc" and m["gated"] for m in meta), meta
+    for m in meta:  # the tuned table: every unit a workgroup, some of them packers
+        g = m["gate"]
+        assert g is not None and g["units"] > 0 and 0 < g["packers"] <= g["units"], g
+    assert np.isfinite(un).all()
+    np.testing.assert_array_equal(un, u1)
+    np.testing.assert_array_equal(vn, v1)
+
+
+def test_gated_off_is_the_stream_overlap():
+    """Debug knob gated = 0: the same job runs the stream-overlapped passes (inner launch + shell,
+    pack / flag / unpack kernels on the comm stream), bit-identical to the gated run."""
+    L, steps, fuse = 48, 10, 3
+    base = dict(overlap="on")
+    cfg_g = _cfg(L, steps, fuse, **base)
+    cfg_s = _cfg(L, steps, fuse, knobs={"gated": 0}, **base)
+    for c in (cfg_g, cfg_s):
+        c["dims"] = [2, 2, 1]
+        c["random_init"] = 5
+    ug, vg, mg = run_ranks(4, cfg_g)
+    us, vs, ms = run_ranks(4, cfg_s)
+    assert all(m["gated"] for m in mg) and not any(m["gated"] for m in ms)
+    assert all(m["overlapped"] for m in ms)
+    np.testing.assert_array_equal(ug, us)
+    np.testing.assert_array_equal(vg, vs)
+
+
+def test_gated_emulated_slow_exchange():
+    """Debug knob ipc_emulate_us: every gated wait lasts at least 30 us (a slow xGMI hop
+    modelled on one GPU); the tuner sees it (its expected exchange time grows) and the result is
+    unchanged."""
+    L, steps, fuse = 64, 7, 3
+    u1, v1, _ = _single(L, steps, fuse, random_init=3)
+    cfg = _cfg(L, steps, fuse, knobs={"ipc_emulate_us": 30}, overlap="on")
+    cfg["dims"] = [2, 2, 2]
+    cfg["random_init"] = 3
+    un, vn, meta = run_ranks(8, cfg)
+    assert all(m["gated"] for m in meta)
+    np.testing.assert_array_equal(un, u1)
+    np.testing.assert_array_equal(vn, v1)
+
+
+def test_gated_halo_poisoning():
+    """NaN in every ghost / padding cell before the run: the in-kernel exchange must refill every
+    ghost cell some start-gated unit's cone reads, and no non-gated unit may read one."""
+    L, steps, fuse = 48, 9, 3
+    u1, v1, _ = _single(L, steps, fuse)
+    cfg = _cfg(L, steps, fuse, overlap="on")
+    cfg["dims"] = [2, 2, 1]
+    cfg["poison"] = True
+    un, vn, meta = run_ranks(4, cfg)
+    assert all(m["gated"] for m in meta)
+    assert np.isfinite(un).all() and np.isfinite(vn).all()
+    np.testing.assert_array_equal(un, u1)
+    np.testing.assert_array_equal(vn, v1)
+
+
+def test_gated_long_run():
+    """Soak of the in-kernel protocol: 4 ranks, 2x2x1, 300 steps of depth 3 (100 gated
+    exchanges, both landing slots reused 50 times each) -- bit-identical to one rank."""
+    L, steps, fuse = 40, 300, 3
+    u1, v1, _ = _single(L, steps, fuse, random_init=31)
+    cfg = _cfg(L, steps, fuse, overlap="on")
+    cfg["dims"] = [2, 2, 1]
+    cfg["random_init"] = 31
+    un, vn, meta = run_ranks(4, cfg)
+    assert all(m["gated"] and m["step"] == steps for m in meta)
+    np.testing.assert_array_equal(un, u1)
+    np.testing.assert_array_equal(vn, v1)
