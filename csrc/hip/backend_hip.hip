@@ -642,6 +642,18 @@ class HipBackend final : public gs::Backend {
       send_peer_[i] = idx;
       if (std::find(send_peers_.begin(), send_peers_.end(), idx) == send_peers_.end())
         send_peers_.push_back(idx);
+      if (m.peer == rank_ && gs::debug_knobs().ipc_pair_same_dir) {
+        // modelling only (debug knob): a loopback message lands in the ghost box of its OWN
+        // direction -- one-sided neighbour sets on one rank (timing; the values are no wrap)
+        int64_t off = -1;
+        for (int j = 0; j < p.nrecv; ++j)
+          if (p.recv[j].peer == rank_ && p.recv[j].dir == m.dir &&
+              gs::box_cells(p.recv[j].box) == gs::box_cells(m.box))
+            off = p.recv[j].offset;
+        if (off < 0) throw std::runtime_error("ipc: no same-direction receive (ipc_pair_same_dir)");
+        send_off_[i] = off;
+        continue;
+      }
       // the k-th send to P matches the k-th receive at P from this rank (make_halo_plan)
       int k = 0;
       for (int j = 0; j < i; ++j) k += p.send[j].peer == m.peer ? 1 : 0;
@@ -846,7 +858,7 @@ class HipBackend final : public gs::Backend {
   // chunks shorter by xp planes (the expected exchange time in plane-times): the smallest plane
   // budget per workgroup whose chunks fit the resident slots.  Sorted by (z0, tile): each XCD
   // group of workgroups gets a contiguous range (sched 3), i.e. neighbouring tiles at one depth.
-  std::vector<gsk::GateUnit> gate_table(int n, int xp, int* npk) const {
+  std::vector<gsk::GateUnit> gate_table(int n, int xp, bool allpk, int* npk) const {
     const int cfg = gsk::gated_shape_cfg(sizeof(T) == 8, g_, n);
     const char* name = gsk::fused_shape_name(cfg, sizeof(T) == 8, true);
     const gsk::TileGrid tg = gsk::fused_tile_grid(name, g_, n);
@@ -887,7 +899,7 @@ class HipBackend final : public gs::Backend {
         const int k = (b - a + len - 1) / len;
         for (int i = 0; i < k; ++i) {
           const int z0 = a + (int)((int64_t)(b - a) * i / k), z1 = a + (int)((int64_t)(b - a) * (i + 1) / k);
-          if (out) out->push_back(gsk::GateUnit{t, z0, z1, gated ? 0 : -1});
+          if (out) out->push_back(gsk::GateUnit{t, z0, z1, gated ? 0 : -1, gated ? 1 : 0});
           ++cnt;
         }
       };
@@ -913,9 +925,11 @@ class HipBackend final : public gs::Backend {
     std::stable_sort(u.begin(), u.end(), [](const gsk::GateUnit& a, const gsk::GateUnit& b) {
       return a.z0 != b.z0 ? a.z0 < b.z0 : a.tile < b.tile;
     });
+    // packers: the start-gated units, or (allpk) every unit -- more CUs share the message
+    // stores, each ungated one marching after its share
     int k = 0;
     for (auto& x : u)
-      if (x.pk >= 0) x.pk = k++;
+      if (x.wait || allpk) x.pk = k++;
     *npk = k;
     return u;
   }
@@ -964,28 +978,31 @@ class HipBackend final : public gs::Backend {
     static const int kXp[] = {0, 4, 8, 16, 24, 32};
     float best = 1e30f;
     int bxp = 0;
+    bool ball = false;
     hipEvent_t e0, e1;
     HIP_CHECK(hipEventCreate(&e0));
     HIP_CHECK(hipEventCreate(&e1));
-    for (int xp : kXp) {
-      int npk = 0;
-      const std::vector<gsk::GateUnit> u = gate_table(n, xp, &npk);
-      gate_upload(n, u, npk);
-      gate_launch(src, dst, n, t);  // warm-up
-      HIP_CHECK(hipEventRecord(e0, stream_));
-      for (int r = 0; r < 3; ++r) gate_launch(src, dst, n, t);
-      HIP_CHECK(hipEventRecord(e1, stream_));
-      wait_all(gs::comm_timeout_s());
-      float ms = 0.f;
-      HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
-      if (ms < best) { best = ms; bxp = xp; }
-    }
+    for (int all = 0; all < 2; ++all)
+      for (int xp : kXp) {
+        int npk = 0;
+        const std::vector<gsk::GateUnit> u = gate_table(n, xp, all != 0, &npk);
+        gate_upload(n, u, npk);
+        gate_launch(src, dst, n, t);  // warm-up
+        HIP_CHECK(hipEventRecord(e0, stream_));
+        for (int r = 0; r < 3; ++r) gate_launch(src, dst, n, t);
+        HIP_CHECK(hipEventRecord(e1, stream_));
+        wait_all(gs::comm_timeout_s());
+        float ms = 0.f;
+        HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+        if (ms < best) { best = ms; bxp = xp; ball = all != 0; }
+      }
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     int npk = 0;
-    const std::vector<gsk::GateUnit> u = gate_table(n, bxp, &npk);
+    const std::vector<gsk::GateUnit> u = gate_table(n, bxp, ball, &npk);
     gate_upload(n, u, npk);
     gate_xp_[n] = bxp;
+    gate_allpk_[n] = ball;
     gate_ms_[n] = best / 3.f;
     gate_tuned_[n] = true;
   }
@@ -1294,6 +1311,7 @@ class HipBackend final : public gs::Backend {
   gs::HaloPlan gplan_{};
   bool gate_plan_ok_ = false;
   int gate_sharers_ = 0;  // peer ranks (other processes) on this GPU
+  bool gate_allpk_[4] = {false, false, false, false};  // tuned: every unit packs
   unsigned long long* d_stamps_ = nullptr;  // debug knob gate_stamps
   gsk::GateArgs* d_gate_ = nullptr;
   uint32_t* d_counter_ = nullptr;

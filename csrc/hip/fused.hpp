@@ -42,7 +42,8 @@
 struct GateUnit {
   int32_t tile;    // tile index (this launch's enumeration)
   int32_t z0, z1;  // output planes [z0, z1)
-  int32_t pk;      // >= 0: start-gated, its packer index; -1: ungated
+  int32_t pk;      // >= 0: a packer, its index; -1: none (every start-gated unit packs)
+  int32_t wait;    // 1: start-gated (waits for the peers, copies its cone's ghosts)
 };
 struct GateArgs;  // gate.hpp
 
@@ -91,8 +92,8 @@ struct FusedArgs {
 };
 
 template <typename T>
-__device__ __forceinline__ void gate_start(const FusedArgs& a, int pk, int X0, int xw, int Y0, int yext, int za,
-                           int zb);
+__device__ __forceinline__ void gate_start(const FusedArgs& a, int pk, bool wait, int X0, int xw,
+                                        int Y0, int yext, int za, int zb);
 
 template <typename T> struct PairT;
 template <> struct PairT<float> { typedef float type __attribute__((ext_vector_type(2))); };
@@ -827,7 +828,7 @@ __device__ __forceinline__ void fused_body(const typename C::V2* __restrict__ s,
     // a start-gated unit packs, signals, waits and fills its cone's ghost cells first -- here,
     // before the march state below is live, so the production loop's registers are untouched
     const GateUnit un = a.gunits[lu0];
-    if (un.pk >= 0) {
+    if (un.pk >= 0) {  // (a start-gated unit is always a packer)
       int X0, xw = 64, Y0, yext = WAVES * ROWS;
       if (C::FOLD && un.tile >= a.ntxf * a.nty) {
         const int f2 = un.tile - a.ntxf * a.nty;
@@ -840,7 +841,7 @@ __device__ __forceinline__ void fused_body(const typename C::V2* __restrict__ s,
         X0 = (un.tile % ntxe) * a.xstep - TL;
         Y0 = a.ybase + (un.tile / ntxe) * a.ystep - TL;
       }
-      gate_start<T>(a, un.pk, X0, xw, Y0, yext, un.z0 - TL, un.z1 + TL);
+      gate_start<T>(a, un.pk, un.wait != 0, X0, xw, Y0, yext, un.z0 - TL, un.z1 + TL);
     }
   }
   FusedState<C> S;

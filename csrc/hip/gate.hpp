@@ -67,14 +67,25 @@ struct GatePiece {
   int sx0, sy0, sz0;  // unpack: origin of the message box in the landing slot
   int snx, sny;       //         and its x / y extent
   int sys;            // pack: system-coherent stores (a peer on another GPU)
+  float inx, iny;     // 1 / nx, 1 / ny (gate_div)
 };
 
 template <typename T>
 constexpr int gate_batch() { return sizeof(T) == 4 ? 16 : 8; }  // cells per thread per batch
 
+// q = k / d for k < 2^24 from a float reciprocal (exact after one correction step): the
+// flat-index decodes below run per cell, integer division is ~40 instructions
+__device__ __forceinline__ uint32_t gate_div(uint32_t k, uint32_t d, float inv) {
+  uint32_t q = (uint32_t)((float)k * inv);
+  const int32_t r = (int32_t)(k - q * d);
+  if (r < 0) --q;
+  else if (r >= (int32_t)d) ++q;
+  return q;
+}
+
 template <typename T>
-__device__ __forceinline__ void gate_start(const FusedArgs& a, int pk, int X0, int xw, int Y0,
-                                        int yext, int za, int zb) {
+__device__ __forceinline__ void gate_start(const FusedArgs& a, int pk, bool wait, int X0, int xw,
+                                        int Y0, int yext, int za, int zb) {
   using V2 = typename Vec2<T>::type;
   constexpr int B = gate_batch<T>();
   const GateArgs& G = *a.gate;
@@ -110,13 +121,14 @@ __device__ __forceinline__ void gate_start(const FusedArgs& a, int pk, int X0, i
   if (tid < (uint32_t)G.nsend) {
     const Box b = G.sbox[tid];
     gp[tid] = GatePiece{G.sdst[slot][tid], b.x0, b.y0, b.z0, b.nx, b.ny, 0u, 0, 0, 0, 0, 0,
-                        (int)((G.sysmask >> tid) & 1u)};
+                        (int)((G.sysmask >> tid) & 1u), 1.0f / (float)b.nx, 1.0f / (float)b.ny};
     gcells[tid] = (uint32_t)gs::box_cells(b);
   }
   number(G.nsend);
   {
     const uint32_t total = gtotal, stride = (uint32_t)a.gate_npk * nt;
     const int np = gnp;
+    const bool small = total < (1u << 24);  // every piece-local index exact in a float
     for (uint32_t i0 = (uint32_t)pk * nt + tid; i0 < total; i0 += B * stride) {
       V2 c[B];
       V2* dst[B];
@@ -130,8 +142,8 @@ __device__ __forceinline__ void gate_start(const FusedArgs& a, int pk, int X0, i
           while (m + 1 < np && gp[m + 1].start <= i) ++m;  // i grows with j
           const GatePiece& q = gp[m];
           const uint32_t k = i - q.start;
-          const uint32_t r = k / (uint32_t)q.nx;
-          const uint32_t z = r / (uint32_t)q.ny;
+          const uint32_t r = small ? gate_div(k, (uint32_t)q.nx, q.inx) : k / (uint32_t)q.nx;
+          const uint32_t z = small ? gate_div(r, (uint32_t)q.ny, q.iny) : r / (uint32_t)q.ny;
           const int x = (int)(k - r * (uint32_t)q.nx), y = (int)(r - z * (uint32_t)q.ny);
           c[j] = f[gs::lin(g, q.x0 + x, q.y0 + y, q.z0 + (int)z)];
           dst[j] = (V2*)q.ptr + k;
@@ -165,6 +177,7 @@ __device__ __forceinline__ void gate_start(const FusedArgs& a, int pk, int X0, i
       for (int i = 0; i < G.nsig; ++i)
         __hip_atomic_store(G.sflag[i], a.gate_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+  if (!wait) return;  // a packer that needs no ghost cells marches at once
   // 2. every receive peer's messages of this exchange have landed (bounded wait).  Relaxed
   // system-scope polls (the flags are uncached: every load reads memory).  No acquire fence (on
   // gfx950 an agent-scope acquire invalidates the XCD's L2, which the marching workgroups
@@ -199,13 +212,15 @@ __device__ __forceinline__ void gate_start(const FusedArgs& a, int pk, int X0, i
     const int z0 = max(b.z0, za), z1 = min(b.z0 + b.nz, zb);
     const bool any = x0 < x1 && y0 < y1 && z0 < z1;
     gp[tid] = GatePiece{const_cast<void*>(G.rsrc[slot][tid]), x0, y0, z0, x1 - x0, y1 - y0, 0u,
-                        b.x0, b.y0, b.z0, b.nx, b.ny, 0};
+                        b.x0, b.y0, b.z0, b.nx, b.ny, 0, any ? 1.0f / (float)(x1 - x0) : 0.f,
+                        any ? 1.0f / (float)(y1 - y0) : 0.f};
     gcells[tid] = any ? (uint32_t)((x1 - x0) * (y1 - y0) * (z1 - z0)) : 0u;
   }
   number(G.nrecv);
   {
     const uint32_t total = gtotal;
     const int np = gnp;
+    const bool small = total < (1u << 24);
     for (uint32_t i0 = tid; i0 < total; i0 += B * nt) {
       V2 c[B];
       int64_t o[B];
@@ -218,8 +233,8 @@ __device__ __forceinline__ void gate_start(const FusedArgs& a, int pk, int X0, i
           while (p + 1 < np && gp[p + 1].start <= i) ++p;
           const GatePiece& q = gp[p];
           const uint32_t k = i - q.start;
-          const uint32_t r = k / (uint32_t)q.nx;
-          const uint32_t zz = r / (uint32_t)q.ny;
+          const uint32_t r = small ? gate_div(k, (uint32_t)q.nx, q.inx) : k / (uint32_t)q.nx;
+          const uint32_t zz = small ? gate_div(r, (uint32_t)q.ny, q.iny) : r / (uint32_t)q.ny;
           const int x = q.x0 + (int)(k - r * (uint32_t)q.nx);
           const int y = q.y0 + (int)(r - zz * (uint32_t)q.ny);
           const int z = q.z0 + (int)zz;

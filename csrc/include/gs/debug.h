@@ -22,6 +22,9 @@
 //                   packer start, last arrival, first / last wait done, last unpack done; read
 //                   back by gs_gate_stamps -- scripts/bench_gated.py).  Read when the IPC
 //                   transport connects.
+//   ipc_pair_same_dir 0 (default); 1: modelling only -- a loopback IPC message lands in the ghost
+//                   box of its own direction, so one rank can time a one-sided neighbour set
+//                   (+x, +y, +z: a 2x2x2 rank); the values are no wrap.  Read at connect.
 //   cpu_ftz         1 (default): the CPU solver flushes fp32 denormals in its step region
 //                   (MXCSR FTZ + DAZ; ~100x faster where the reference example's v field
 //                   passes through them); 0: IEEE denormals, the reference's and the GPU's
@@ -38,6 +41,7 @@ struct DebugKnobs {
   double ipc_emulate_us = 0.0;
   int ipc_system_stores = 0;
   int gate_stamps = 0;
+  int ipc_pair_same_dir = 0;
   int cpu_ftz = 1;
   int gated = 1;
 };
@@ -56,6 +60,7 @@ inline int debug_set(const char* name, double value) {
   else if (!strcmp(name, "ipc_emulate_us")) k.ipc_emulate_us = value > 0.0 ? value : 0.0;
   else if (!strcmp(name, "ipc_system_stores")) k.ipc_system_stores = value != 0.0 ? 1 : 0;
   else if (!strcmp(name, "gate_stamps")) k.gate_stamps = value != 0.0 ? 1 : 0;
+  else if (!strcmp(name, "ipc_pair_same_dir")) k.ipc_pair_same_dir = value != 0.0 ? 1 : 0;
   else if (!strcmp(name, "cpu_ftz")) k.cpu_ftz = value != 0.0 ? 1 : 0;
   else if (!strcmp(name, "gated")) k.gated = value >= 2.0 ? 2 : (value != 0.0 ? 1 : 0);
   else return -1;

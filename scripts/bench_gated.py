@@ -7,6 +7,9 @@ packers, counter, flags, bounded waits, cone unpacks -- with the sub-domain one 
 N-GPU job owns.  Per k-step pass (ms), for the neighbour sets:
   z      -- neighbours at -z / +z only (z slabs: whole-plane messages),
   all    -- all 26 directions (every face, edge and corner; the interior rank of a large grid);
+  plus   -- +x, +y, +z faces, their edges and corner: a 2x2x2 rank of BASELINE config 3 (debug
+            knob ipc_pair_same_dir: each message lands in its own direction's ghost box --
+            timing only, the values are no wrap);
 and the pass kinds:
   full       -- the fused pass of a rank without neighbours (no exchange): the floor,
   gated      -- the gated pass (the default for IPC, overlap on),
@@ -34,7 +37,7 @@ def main():
     ap.add_argument("--k", type=int, nargs="+", default=[3])
     ap.add_argument("--passes", type=int, default=60)
     ap.add_argument("--emulate-us", type=float, nargs="+", default=[0.0, 30.0])
-    ap.add_argument("--nbrs", nargs="+", default=["z", "all"])
+    ap.add_argument("--nbrs", nargs="+", default=["z", "plus", "all"])
     ap.add_argument("--prec", default="Float32")
     ap.add_argument("--out", default="")
     ap.add_argument("--stamps", action="store_true",
@@ -68,6 +71,9 @@ def main():
         if which == "z":  # keep dx = dy = 0
             nbr = [r if (i // 9 == 1 and (i // 3) % 3 == 1) or i == 13 else -1
                    for i, r in enumerate(nbr)]
+        elif which == "plus":  # dx, dy, dz in {0, 1}: +x, +y, +z faces, their edges, the corner
+            nbr = [r if i != 13 and i // 9 != 0 and (i // 3) % 3 != 0 and i % 3 != 0 else -1
+                   for i, r in enumerate(nbr)]
         return dataclasses.replace(dom, periodic=False, nbr27=nbr)
 
     rows = []
@@ -87,6 +93,7 @@ def main():
                         native.debug_set("gated", gated)
                         native.debug_set("ipc_emulate_us", em)
                         native.debug_set("gate_stamps", 1 if a.stamps else 0)
+                        native.debug_set("ipc_pair_same_dir", 1 if which == "plus" else 0)
                         try:
                             sim = GrayScott(settings(n, ov), loop_dom(n, which), fuse=k,
                                             transport="ipc", loopback=True)
@@ -104,6 +111,7 @@ def main():
                             native.debug_set("gated", 1)
                             native.debug_set("ipc_emulate_us", 0)
                             native.debug_set("gate_stamps", 0)
+                            native.debug_set("ipc_pair_same_dir", 0)
                     rows.append(row)
                     print(json.dumps(row), flush=True)
     if a.out:
