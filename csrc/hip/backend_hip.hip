@@ -1138,6 +1138,28 @@ class HipBackend final : public gs::Backend {
     HIP_CHECK(hipGetLastError());
     return n;
   }
+  // One output / checkpoint snapshot in a single call (models/grayscott.py snapshot_fields):
+  // the compute stream waits for the previous D2H out of the device buffers (prev, may be
+  // null), compacts the interior (with per-chunk min / max when part != null), and the I/O
+  // stream copies it into the pinned host buffers, recording done.  Returns the min / max
+  // quadruples copied (0: none).
+  int snapshot(int b, void* du, void* dv, void* dpart, int cap, void* hu, void* hv, void* hpart,
+               hipStream_t io, hipEvent_t prev, hipEvent_t ready, hipEvent_t done) {
+    if (prev) HIP_CHECK(hipStreamWaitEvent(stream_, prev, 0));
+    int n = 0;
+    if (dpart) n = gsk::launch_extract_mm<T>(buf_[b], (T*)du, (T*)dv, g_, (T*)dpart, cap, stream_);
+    if (!n) gsk::launch_extract<T>(buf_[b], (T*)du, (T*)dv, g_, stream_);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipEventRecord(ready, stream_));
+    HIP_CHECK(hipStreamWaitEvent(io, ready, 0));
+    const size_t bytes = (size_t)g_.nx * g_.ny * g_.nz * sizeof(T);
+    HIP_CHECK(hipMemcpyAsync(hu, du, bytes, hipMemcpyDeviceToHost, io));
+    HIP_CHECK(hipMemcpyAsync(hv, dv, bytes, hipMemcpyDeviceToHost, io));
+    if (n) HIP_CHECK(hipMemcpyAsync(hpart, dpart, (size_t)4 * n * sizeof(T), hipMemcpyDeviceToHost, io));
+    HIP_CHECK(hipEventRecord(done, io));
+    return n;
+  }
+
   void randomize(int b, uint64_t seed, double lo, double hi) override {
     gsk::launch_randomize<T>(buf_[b], g_, seed, lo, hi, stream_);
     HIP_CHECK(hipGetLastError());
@@ -1532,6 +1554,49 @@ extern "C" int gs_gate_info(gs_engine* e, int32_t n, int32_t dtype, double* out4
   try {
     with_hip_backend(e, dtype, [&](auto* b) { b->gate_info(n, out4); });
     return 0;
+  } catch (const std::exception& ex) {
+    g_gs_err = ex.what();
+    return -1;
+  }
+}
+
+// Snapshot events (HipBackend::snapshot): plain timing-disabled HIP events owned by the caller.
+extern "C" void* gs_event_create() {
+  hipEvent_t ev = nullptr;
+  if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return nullptr;
+  return (void*)ev;
+}
+extern "C" void gs_event_destroy(void* ev) {
+  if (ev) (void)hipEventDestroy((hipEvent_t)ev);
+}
+// wait for an event (the caller's thread; ctypes releases the GIL): 0, or -1 on an error.
+// Polled (hipEventQuery + short sleeps), not hipEventSynchronize: the writer thread waits here
+// while the stepping thread enqueues its next launches, and a blocking event wait inside the
+// runtime stalled those (the output step's snapshot call took ~85 us in the loop vs ~25 us
+// alone, scripts/profile_output.py)
+extern "C" int gs_event_sync(void* ev) {
+  int sleep_us = 5;
+  for (;;) {
+    const hipError_t r = hipEventQuery((hipEvent_t)ev);
+    if (r == hipSuccess) return 0;
+    if (r != hipErrorNotReady) {
+      g_gs_err = std::string("event sync: ") + hipGetErrorString(r);
+      return -1;
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(sleep_us));
+    if (sleep_us < 50) sleep_us *= 2;
+  }
+}
+extern "C" int gs_snapshot(gs_engine* e, int32_t dtype, void* du, void* dv, void* dpart, int32_t cap,
+                           void* hu, void* hv, void* hpart, void* io, void* prev, void* ready,
+                           void* done) {
+  try {
+    int n = 0;
+    with_hip_backend(e, dtype, [&](auto* b) {
+      n = b->snapshot(e->eng->cur(), du, dv, dpart, cap, hu, hv, hpart, (hipStream_t)io,
+                      (hipEvent_t)prev, (hipEvent_t)ready, (hipEvent_t)done);
+    });
+    return n;
   } catch (const std::exception& ex) {
     g_gs_err = ex.what();
     return -1;

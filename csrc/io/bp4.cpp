@@ -26,6 +26,11 @@
 
 #include <algorithm>
 #include <cmath>
+#include <condition_variable>
+#include <deque>
+#include <map>
+#include <mutex>
+#include <thread>
 #include <limits>
 #include <stdexcept>
 #include <string>
@@ -133,6 +138,33 @@ struct Writer {
   uint64_t pg_start = 0;
   std::vector<Block> blocks;
   Buf step_meta;        // serialized local step metadata (returned to the caller)
+  struct Async* async = nullptr;  // bp4_async_*: the native writer thread (null: none)
+};
+
+// The asynchronous output writer (bp4_async_submit / bp4_async_result): one native thread per
+// writer runs queued whole steps (wait for the step's device copy, then bp4_write_step_uv), so
+// no Python code runs on the writer side and the stepping thread never contends with it for the
+// interpreter lock.
+struct AsyncJob {
+  int64_t ticket;
+  int (*wait_fn)(void*);  // e.g. libgs_hip's gs_event_sync on the snapshot's "done" event
+  void* wait_arg;
+  int32_t var_step, step, var_u, var_v, nmm;
+  const void *u, *v, *part;
+};
+struct AsyncResult {
+  int rc;
+  std::string blob_or_error;
+};
+struct Async {
+  std::thread th;
+  std::mutex mu;
+  std::condition_variable cv, done;
+  std::deque<AsyncJob> q;
+  std::map<int64_t, AsyncResult> results;
+  int64_t next = 0;
+  bool stop = false;
+  std::string last;  // the blob of the last bp4_async_result (valid until the next call)
 };
 
 // per thread: the output and checkpoint writers run their data writes on different host
@@ -722,6 +754,122 @@ int bp4_end_step(void* h) {
   }
 }
 
+// One output step of the simulation stream in a single call (io/output.py's asynchronous job;
+// IO.jl:82-96 begin_step, put step / U / V, end_step): the caller's thread spends the whole data
+// write in native code.  part: nmm per-chunk (u min, u max, v min, v max) quadruples of the
+// field type (the GPU snapshot kernel's), reduced here; nmm = 0: the blocks are scanned.
+int bp4_write_step_uv(void* h, int32_t var_step, int32_t step, int32_t var_u, const void* u,
+                      int32_t var_v, const void* v, const void* part, int32_t nmm) {
+  try {
+    Writer* w = (Writer*)h;
+    if (bp4_begin_step(h) != 0) return -1;
+    if (put_block(h, var_step, &step, nullptr) != 0) return -1;
+    if (nmm > 0 && part) {
+      double mm[4] = {HUGE_VAL, -HUGE_VAL, HUGE_VAL, -HUGE_VAL};
+      const bool f64 = w->vars.at(var_u).type == type_double;
+      for (int32_t i = 0; i < nmm; ++i)
+        for (int j = 0; j < 4; ++j) {
+          const double x = f64 ? ((const double*)part)[4 * i + j] : (double)((const float*)part)[4 * i + j];
+          mm[j] = (j & 1) ? std::max(mm[j], x) : std::min(mm[j], x);
+        }
+      if (put_block(h, var_u, u, mm) != 0 || put_block(h, var_v, v, mm + 2) != 0) return -1;
+    } else if (put_block(h, var_u, u, nullptr) != 0 || put_block(h, var_v, v, nullptr) != 0) {
+      return -1;
+    }
+    return bp4_end_step(h);
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return -1;
+  }
+}
+
+static void async_loop(Writer* w) {
+  Async* a = w->async;
+  for (;;) {
+    AsyncJob j;
+    {
+      std::unique_lock<std::mutex> lk(a->mu);
+      a->cv.wait(lk, [&] { return a->stop || !a->q.empty(); });
+      if (a->q.empty()) return;  // stop, nothing queued
+      j = a->q.front();
+      a->q.pop_front();
+    }
+    AsyncResult r{0, {}};
+    if (j.wait_fn && j.wait_fn(j.wait_arg) != 0) {
+      r = {-1, "waiting for the step's device copy failed"};
+    } else if (bp4_write_step_uv(w, j.var_step, j.step, j.var_u, j.u, j.var_v, j.v, j.part,
+                                 j.nmm) != 0) {
+      r = {-1, g_err};
+    } else {
+      r.blob_or_error.assign(w->step_meta.b.data(), w->step_meta.size());
+    }
+    {
+      std::lock_guard<std::mutex> lk(a->mu);
+      a->results[j.ticket] = std::move(r);
+    }
+    a->done.notify_all();
+  }
+}
+
+// Queue one whole output step on the writer's native thread (started on first use); the
+// arrays must stay valid until bp4_async_result returns for the ticket.  Returns the ticket.
+int64_t bp4_async_submit(void* h, int (*wait_fn)(void*), void* wait_arg, int32_t var_step,
+                         int32_t step, int32_t var_u, const void* u, int32_t var_v, const void* v,
+                         const void* part, int32_t nmm) {
+  try {
+    Writer* w = (Writer*)h;
+    if (!w->async) {
+      w->async = new Async();
+      w->async->th = std::thread(async_loop, w);
+    }
+    Async* a = w->async;
+    std::lock_guard<std::mutex> lk(a->mu);
+    const int64_t t = a->next++;
+    a->q.push_back(AsyncJob{t, wait_fn, wait_arg, var_step, step, var_u, var_v, nmm, u, v, part});
+    a->cv.notify_one();
+    return t;
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return -1;
+  }
+}
+
+// Wait for a queued step (the caller's thread blocks; ctypes releases the GIL): 0 and its
+// metadata blob at *out (valid until the next call), or -1 with the step's error.
+int bp4_async_result(void* h, int64_t ticket, const char** out, int64_t* n) {
+  Writer* w = (Writer*)h;
+  Async* a = w->async;
+  if (!a) {
+    g_err = "bp4_async_result: nothing was submitted";
+    return -1;
+  }
+  std::unique_lock<std::mutex> lk(a->mu);
+  a->done.wait(lk, [&] { return a->results.count(ticket) != 0; });
+  AsyncResult r = std::move(a->results[ticket]);
+  a->results.erase(ticket);
+  lk.unlock();
+  if (r.rc != 0) {
+    g_err = r.blob_or_error;
+    return -1;
+  }
+  a->last = std::move(r.blob_or_error);
+  *out = a->last.data();
+  *n = (int64_t)a->last.size();
+  return 0;
+}
+
+static void async_stop(Writer* w) {
+  if (!w->async) return;
+  {
+    std::lock_guard<std::mutex> lk(w->async->mu);
+    w->async->stop = true;
+  }
+  w->async->cv.notify_all();
+  if (w->async->th.joinable()) w->async->th.join();
+  delete w->async;
+  w->async = nullptr;
+}
+
 int64_t bp4_step_metadata(void* h, const char** out) {
   Writer* w = (Writer*)h;
   *out = w->step_meta.b.data();
@@ -834,6 +982,7 @@ int bp4_write_metadata(void* h, int32_t nblobs, const char* const* blobs, const 
 int bp4_close(void* h) {
   Writer* w = (Writer*)h;
   if (!w) return 0;
+  async_stop(w);  // (runs the queued steps first)
   int rc = 0;
   if (w->data) rc |= fclose(w->data);
   if (w->md) rc |= fclose(w->md);

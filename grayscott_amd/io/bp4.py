@@ -71,6 +71,15 @@ def _lib():
         lib.bp4_put.restype = c_int32
         lib.bp4_put_minmax.argtypes = [c_void_p, c_int32, c_void_p, ctypes.c_double, ctypes.c_double]
         lib.bp4_put_minmax.restype = c_int32
+        lib.bp4_write_step_uv.argtypes = [c_void_p, c_int32, c_int32, c_int32, c_void_p, c_int32,
+                                          c_void_p, c_void_p, c_int32]
+        lib.bp4_write_step_uv.restype = c_int32
+        lib.bp4_async_submit.argtypes = [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32,
+                                         c_void_p, c_int32, c_void_p, c_void_p, c_int32]
+        lib.bp4_async_submit.restype = c_int64
+        lib.bp4_async_result.argtypes = [c_void_p, c_int64, POINTER(ctypes.POINTER(ctypes.c_char)),
+                                         POINTER(c_int64)]
+        lib.bp4_async_result.restype = c_int32
         lib.bp4_end_step.argtypes = [c_void_p]
         lib.bp4_end_step.restype = c_int32
         lib.bp4_step_metadata.argtypes = [c_void_p, POINTER(ctypes.POINTER(ctypes.c_char))]
@@ -169,6 +178,49 @@ class BP4Writer:
                                               float(minmax[1])), f"put {name}")
         else:
             self._chk(self.lib.bp4_put(self.h, vid, a.ctypes.data), f"put {name}")
+
+    def write_step_uv(self, step: int, u, v, part=None) -> bytes:
+        """One whole step -- begin, ``step``, ``U``, ``V`` (min / max reduced from the snapshot
+        kernel's per-chunk quadruples ``part``, or scanned when None), end -- in one native call
+        (the GIL is released for the entire data write); returns the metadata blob."""
+        _, dt, count = self._vars["U"]
+        for a in (u, v):
+            if a.dtype != dt or a.shape != count or not a.flags.c_contiguous:
+                raise BP4Error(f"write_step_uv: blocks must be C-contiguous {np.dtype(dt).name} {count}")
+        st = np.int32(step)
+        pp = part.ctypes.data if part is not None and len(part) else None
+        self._chk(self.lib.bp4_write_step_uv(
+            self.h, self._vars["step"][0], int(st), self._vars["U"][0], u.ctypes.data,
+            self._vars["V"][0], v.ctypes.data, pp, len(part) if pp else 0), "write_step_uv")
+        ptr = ctypes.POINTER(ctypes.c_char)()
+        n = self.lib.bp4_step_metadata(self.h, ctypes.byref(ptr))
+        return ctypes.string_at(ptr, n)
+
+    def submit_step_uv(self, step: int, u, v, part=None, wait_fn=None, wait_arg=None) -> int:
+        """Queue ``write_step_uv`` on the writer's native thread (started on first use), after
+        ``wait_fn(wait_arg)`` -- a C function pointer, e.g. libgs_hip's ``gs_event_sync`` on the
+        snapshot's copy event -- returns.  No Python runs on that thread.  ``u``, ``v``,
+        ``part`` must stay alive until ``step_result`` returns for the ticket."""
+        _, dt, count = self._vars["U"]
+        for a in (u, v):
+            if a.dtype != dt or a.shape != count or not a.flags.c_contiguous:
+                raise BP4Error(f"submit_step_uv: blocks must be C-contiguous {np.dtype(dt).name} {count}")
+        pp = part.ctypes.data if part is not None and len(part) else None
+        t = self.lib.bp4_async_submit(self.h, wait_fn, wait_arg, self._vars["step"][0],
+                                      int(np.int32(step)), self._vars["U"][0], u.ctypes.data,
+                                      self._vars["V"][0], v.ctypes.data, pp,
+                                      len(part) if pp else 0)
+        if t < 0:
+            raise BP4Error("submit_step_uv: " + self.lib.bp4_last_error().decode())
+        return int(t)
+
+    def step_result(self, ticket: int) -> bytes:
+        """Wait for a queued step; its metadata blob (raises the step's error)."""
+        ptr = ctypes.POINTER(ctypes.c_char)()
+        n = c_int64(0)
+        self._chk(self.lib.bp4_async_result(self.h, int(ticket), ctypes.byref(ptr), ctypes.byref(n)),
+                  "async step")
+        return ctypes.string_at(ptr, n.value)
 
     def end_step(self) -> bytes:
         """Close the step's process group; returns this rank's metadata blob."""

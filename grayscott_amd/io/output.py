@@ -179,15 +179,22 @@ class SimulationOutput:
             self._commit_oldest()
         u, v, wait, mm = sim.snapshot_fields("output", depth=depth, minmax=True)
         snap = (u, v, wait)
+        part = getattr(mm, "part", None)
+        fn, arg = _native_wait(wait)
+        if fn is not None:
+            # the whole step on the writer's native thread (bp4_async_submit): it waits for the
+            # D2H copy itself (gs_event_sync) and writes; no Python runs beside the stepping
+            t = self.w.submit_step_uv(step, u, v, part, fn, arg)
+            self._pending.append((step, _Ticket(self.w, t, (u, v, part, wait))))
+            self.last_step = step
+            return snap
 
         def job():
+            # two native calls, the GIL released throughout (a Python put sequence here held it
+            # between calls and stalled the stepping thread's own native calls): the D2H wait,
+            # then the whole step -- the snapshot kernel's min / max partials reduced in C++
             wait()
-            (umn, umx), (vmn, vmx) = mm()  # the snapshot kernel's min / max (no host scan)
-            self.w.begin_step()
-            self.w.put("step", np.int32(step))
-            self.w.put("U", u, minmax=(umn, umx))
-            self.w.put("V", v, minmax=(vmn, vmx))
-            return self.w.end_step()
+            return self.w.write_step_uv(step, u, v, getattr(mm, "part", None))
 
         self._pending.append((step, worker("gs-async-output").submit(job)))
         self.last_step = step
@@ -220,6 +227,34 @@ class SimulationOutput:
         self.flush()
         self.w.close()
         self.ctx.barrier()
+
+
+def _native_wait(wait):
+    """(C function pointer, argument) that waits like ``wait`` -- a snapshot's native event
+    (libgs_hip gs_event_sync) or nothing to wait for (the CPU backend's ready arrays) -- or
+    (None, None) when only the Python callable can (the torch-event snapshot A/B path)."""
+    ev = getattr(wait, "__self__", None)
+    if ev is None:  # the CPU backend's lambda: the arrays are ready
+        return 0, None
+    from ..ops import native
+    if isinstance(ev, native.NativeEvent):
+        import ctypes
+        return ctypes.cast(ev.lib.gs_event_sync, ctypes.c_void_p).value, ev.ptr
+    return None, None
+
+
+class _Ticket:
+    """A step queued on the BP4 writer's native thread; ``keep`` holds the arrays (and the
+    event) it reads until its result is taken."""
+
+    def __init__(self, w: BP4Writer, ticket: int, keep):
+        self.w, self.ticket, self.keep = w, ticket, keep
+
+    def result(self) -> bytes:
+        try:
+            return self.w.step_result(self.ticket)
+        finally:
+            self.keep = None
 
 
 def _snapshot_bytes(sim) -> int:

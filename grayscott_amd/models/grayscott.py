@@ -412,6 +412,31 @@ class GrayScott:
                 "next": 0, "done": None}
         dev, host = st["dev"], st["host"][st["next"]]
         st["next"] = (st["next"] + 1) % depth
+        # one native call (HipBackend::snapshot): the compute stream waits for the previous D2H
+        # out of dev[] (event "done" of the last call), compacts (+ min / max partials), the I/O
+        # stream copies into the pinned ring slot -- ~10 us of host time instead of the ~60-190
+        # us of separate torch stream / event / copy calls
+        if not self.native_snapshot:
+            return self._snapshot_torch(st, dev, host, minmax)
+        evs = st.setdefault("events", [])
+        if len(evs) < 2 * depth + 2:
+            evs.extend(native.NativeEvent() for _ in range(2 * depth + 2 - len(evs)))
+        k = st.setdefault("ev_next", 0)
+        st["ev_next"] = (k + 2) % len(evs)
+        ready, done = evs[k], evs[k + 1]
+        nmm = self.engine.snapshot(dev[0].data_ptr(), dev[1].data_ptr(),
+                                   dev[2].data_ptr() if minmax else 0, self._MM_CAP,
+                                   host[0].data_ptr(), host[1].data_ptr(),
+                                   host[2].data_ptr() if minmax else 0,
+                                   self._io_stream.cuda_stream, st["done"], ready, done)
+        st["done"] = done
+        return self._snapshot_views(host, nmm, done, minmax)
+
+    # the snapshot through torch stream / event / copy calls (A/B of the native call:
+    # scripts/profile_output.py --torch-snapshot)
+    native_snapshot = True
+
+    def _snapshot_torch(self, st, dev, host, minmax):
         cur = torch.cuda.current_stream(self.device)
         if st["done"] is not None:
             cur.wait_event(st["done"])  # the previous D2H out of dev[] has finished
@@ -432,17 +457,20 @@ class GrayScott:
                 host[2][:4 * nmm].copy_(dev[2][:4 * nmm], non_blocking=True)
             done.record(self._io_stream)
         st["done"] = done
+        return self._snapshot_views(host, nmm, done, minmax)
+
+    def _snapshot_views(self, host, nmm, done, minmax):
         u, v = host[0].numpy(), host[1].numpy()
         if not minmax:
             return u, v, done.synchronize
+        part = host[2].numpy()[:4 * nmm].reshape(nmm, 4) if nmm else None
         if nmm:
-            part = host[2].numpy()[:4 * nmm].reshape(nmm, 4)
-
             def mm():
                 return ((part[:, 0].min(), part[:, 1].max()), (part[:, 2].min(), part[:, 3].max()))
         else:
             def mm():
                 return ((u.min(), u.max()), (v.min(), v.max()))
+        mm.part = part  # the raw quadruples (io/output.py hands them to the native writer)
         return u, v, done.synchronize, mm
 
     def set_fields(self, u, v) -> None:

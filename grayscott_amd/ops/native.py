@@ -79,6 +79,11 @@ def _declare(lib) -> None:
     lib.gs_chained.restype = c_int
     lib.gs_gated.argtypes = [c_void_p, c_int32]
     lib.gs_gated.restype = c_int
+    if hasattr(lib, "gs_snapshot"):
+        lib.gs_snapshot.argtypes = [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_int32,
+                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                    c_void_p]
+        lib.gs_snapshot.restype = c_int
     lib.gs_set_gated.argtypes = [c_void_p, c_int32]
     lib.gs_set_gated.restype = c_int
     lib.gs_depth.argtypes = [c_void_p]
@@ -354,6 +359,19 @@ class Engine:
         self._chk(0 if n >= 0 else -1, "extract_minmax")
         return n
 
+    def snapshot(self, du: int, dv: int, dpart: int, cap: int, hu: int, hv: int, hpart: int,
+                 io_stream: int, prev, ready, done) -> int:
+        """HIP only: compact the interior into (du, dv) [+ per-chunk min / max at dpart] on the
+        compute stream after event ``prev``, copy to the pinned (hu, hv[, hpart]) on the I/O
+        stream, record ``done`` (NativeEvent handles).  Returns the min / max quadruples."""
+        n = self.lib.gs_snapshot(self.h, DTYPE_CODES[self.dtype], c_void_p(du), c_void_p(dv),
+                                 c_void_p(dpart or None), int(cap), c_void_p(hu), c_void_p(hv),
+                                 c_void_p(hpart or None), c_void_p(io_stream or None),
+                                 c_void_p(prev.ptr if prev is not None else None),
+                                 c_void_p(ready.ptr), c_void_p(done.ptr))
+        self._chk(0 if n >= 0 else -1, "snapshot")
+        return n
+
     def insert(self, u_ptr: int, v_ptr: int):
         self._chk(self.lib.gs_insert(self.h, c_void_p(u_ptr), c_void_p(v_ptr)), "insert")
 
@@ -529,6 +547,33 @@ def cpu_threads(n: int = 0) -> int:
     lib.gs_cpu_threads.argtypes = [c_int32]
     lib.gs_cpu_threads.restype = c_int
     return int(lib.gs_cpu_threads(int(n)))
+
+
+class NativeEvent:
+    """A HIP event owned by Python (gs_event_create): ``synchronize()`` waits with the GIL
+    released; destroyed with the object."""
+
+    def __init__(self):
+        self.lib = load("hip")
+        self.lib.gs_event_create.restype = c_void_p
+        self.lib.gs_event_destroy.argtypes = [c_void_p]
+        self.lib.gs_event_sync.argtypes = [c_void_p]
+        self.lib.gs_event_sync.restype = c_int
+        self.ptr = self.lib.gs_event_create()
+        if not self.ptr:
+            raise RuntimeError("gs_event_create failed")
+
+    def synchronize(self) -> None:
+        if self.lib.gs_event_sync(self.ptr) != 0:
+            raise RuntimeError(self.lib.gs_last_error().decode())
+
+    def __del__(self):
+        ptr, self.ptr = getattr(self, "ptr", None), None
+        if ptr:
+            try:
+                self.lib.gs_event_destroy(ptr)
+            except Exception:  # pragma: no cover - interpreter teardown
+                pass
 
 
 def debug_set(name: str, value: float, which: str = "hip") -> None:

@@ -7,6 +7,7 @@ every host-side piece of the output path, and prints per-call means:
 
   sync            sim.synchronize() (the driver's phase timer waits for the device around phases)
   snapshot        GrayScott.snapshot_fields: compaction launch, D2H enqueue on the I/O stream
+    native_call   the one C call that does it (HipBackend::snapshot)
   commit          SimulationOutput._commit_oldest: join the data write, gather, metadata
     join          the writer thread's job result (waits for its data write)
     gather        ctx.gather_object of the metadata blob
@@ -57,6 +58,9 @@ def main(argv=None) -> int:
     ap.add_argument("--backend", default="AMDGPU")
     ap.add_argument("--out", default="")
     ap.add_argument("--repeat", type=int, default=2, help="runs (the first warms the page cache)")
+    ap.add_argument("--torch-snapshot", action="store_true",
+                    help="the snapshot through torch calls instead of the native one (A/B)")
+    ap.add_argument("--queue", type=int, default=0, help="output_queue (0: the setting's)")
     a = ap.parse_args(argv)
 
     from grayscott_amd import driver
@@ -65,8 +69,12 @@ def main(argv=None) -> int:
     from grayscott_amd.parallel.dist import DistContext
     from grayscott_amd.utils.config import get_settings
 
+    GrayScott.native_snapshot = not a.torch_snapshot
     wrap(GrayScott, "synchronize", "sync")
     wrap(GrayScott, "snapshot_fields", "snapshot")
+    from grayscott_amd.ops import native
+    wrap(native.Engine, "snapshot", "snapshot.native_call")
+    wrap(GrayScott, "_snapshot_views", "snapshot.views")
     wrap(output.SimulationOutput, "_commit_oldest", "commit")
     wrap(output.SimulationOutput, "write_step", "write_step")
     wrap(output._Job, "result", "commit.join")
@@ -79,10 +87,13 @@ def main(argv=None) -> int:
         STATS.clear()
         s = get_settings([a.config])
         s.backend = a.backend
+        if a.queue:
+            s.output_queue = a.queue
         s.output = a.out or os.path.join(tempfile.gettempdir(), f"gs_prof_{os.getpid()}_{r}.bp")
         res = driver.run(s, out=open(os.devnull, "w"))
         steps_out = STATS["write_step"][0]
-        rec = {"run": r, "loop_s": round(res["loop_s"], 5), "compute_s": round(res["compute_s"], 5),
+        rec = {"run": r, "snapshot": "torch" if a.torch_snapshot else "native",
+               "queue": s.output_queue, "loop_s": round(res["loop_s"], 5), "compute_s": round(res["compute_s"], 5),
                "output_s": round(res["timers"].get("output", {}).get("seconds", 0.0), 5),
                "output_steps": steps_out,
                "per_call_us": {k: round(1e6 * v[1] / max(1, v[0]), 1) for k, v in sorted(STATS.items())},

@@ -315,3 +315,49 @@ def test_put_with_given_minmax(tmp_path):
     blk = r.variables(0)["U"].blocks[0]
     assert (blk.vmin, blk.vmax) == (-5.0, 18.0)
     r.close()
+
+
+@pytest.mark.parametrize("dtype", ["float32", "float64"])
+def test_write_step_uv_matches_put_sequence(tmp_path, dtype):
+    """BP4Writer.write_step_uv (one native call per output step: begin, step, U, V with the
+    snapshot kernel's min / max partials reduced in C++, end) writes the same bytes as the
+    begin / put / put / put / end sequence -- data subfile, md.0 and md.idx."""
+    import numpy as np
+
+    from grayscott_amd.io.bp4 import BP4Writer
+    rng = np.random.default_rng(3)
+    shape = (5, 6, 7)
+    steps = [(rng.random(shape).astype(dtype), rng.random(shape).astype(dtype)) for _ in range(3)]
+    outs = []
+    for mode in ("puts", "one_call", "one_call_scan"):
+        p = str(tmp_path / f"{mode}.bp")
+        w = BP4Writer(p, "SimulationOutput", 0, 1)
+        w.define_variable("step", np.int32)
+        w.define_variable("U", np.dtype(dtype).type, shape, (0, 0, 0), shape)
+        w.define_variable("V", np.dtype(dtype).type, shape, (0, 0, 0), shape)
+        for i, (u, v) in enumerate(steps):
+            if mode == "puts":
+                w.begin_step()
+                w.put("step", np.int32(10 * i))
+                w.put("U", u)
+                w.put("V", v)
+                blob = w.end_step()
+            else:
+                part = None
+                if mode == "one_call":  # two chunks' (u min, u max, v min, v max)
+                    h = shape[0] // 2
+                    part = np.array([[u[:h].min(), u[:h].max(), v[:h].min(), v[:h].max()],
+                                     [u[h:].min(), u[h:].max(), v[h:].min(), v[h:].max()]],
+                                    dtype=dtype)
+                blob = w.write_step_uv(10 * i, u, v, part)
+            w.write_metadata([blob])
+        w.close()
+        outs.append({f: open(os.path.join(p, f), "rb").read() for f in ("data.0", "md.0", "md.idx")})
+        # md.idx records (64 B after a 64 B header) carry a wall-clock ms stamp at +48
+        idx = bytearray(outs[-1]["md.idx"])
+        for r in range(64, len(idx), 64):
+            idx[r + 48:r + 56] = bytes(8)
+        outs[-1]["md.idx"] = bytes(idx)
+    for f in ("data.0", "md.0", "md.idx"):
+        assert outs[1][f] == outs[0][f], f
+        assert outs[2][f] == outs[0][f], f
