@@ -40,6 +40,39 @@ def main():
         wait()
         t = tick("wait", t)
     print(json.dumps({k: round(1e6 * v / n, 1) for k, v in acc.items()}), flush=True)
+    # the same cadence with the output stream's native writer thread writing each snapshot
+    import tempfile
+    from grayscott_amd.io.output import SimulationOutput
+    out = SimulationOutput(s, sim.domain, path=os.path.join(tempfile.gettempdir(), f"snap2_{os.getpid()}.bp"))
+    for label in ("with writer", "with writer (again)"):
+        acc.clear()
+        for it in range(n):
+            t = time.perf_counter()
+            sim.iterate(10)
+            t = tick("iterate(10)", t)
+            out.write_step(it, sim)
+            t = tick("write_step", t)
+        out.flush()
+        print(json.dumps({"what": label, **{k: round(1e6 * v / n, 1) for k, v in acc.items()}}), flush=True)
+    import grayscott_amd.models.grayscott as gm
+    orig = gm.GrayScott.snapshot_fields
+    sn = {"t": 0.0}
+
+    def timed(self, *a, **k):
+        t0 = time.perf_counter()
+        try:
+            return orig(self, *a, **k)
+        finally:
+            sn["t"] += time.perf_counter() - t0
+    gm.GrayScott.snapshot_fields = timed
+    acc.clear()
+    for it in range(n):
+        sim.iterate(10)
+        out.write_step(it, sim)
+    out.flush()
+    print(json.dumps({"what": "snapshot_fields inside write_step, with writer", "us": round(1e6 * sn["t"] / n, 1)}), flush=True)
+    gm.GrayScott.snapshot_fields = orig
+    out.close()
     # the same with the profiler on the snapshot
     import cProfile
     import pstats

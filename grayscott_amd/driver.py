@@ -103,6 +103,8 @@ def run(settings: Settings, out=sys.stdout) -> dict:
         # a restarted run continues the existing output: its steps up to the restart step stay
         stream = SimulationOutput(settings, domain, ctx,
                                   append_after_step=step if settings.restart else None)
+        if settings.plotgap > 0:
+            stream.prepare(sim)
     if (settings.restart and settings.plotgap > 0 and step > 0 and step % settings.plotgap == 0
             and stream.last_step != step):
         # the failed run had not committed this output step: the restored state is that step's

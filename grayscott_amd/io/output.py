@@ -174,7 +174,7 @@ class SimulationOutput:
         # the ring of pinned host snapshots is bounded in bytes, not in steps: at most
         # PINNED_RING_BYTES per rank (queue x snapshot), so an 8-rank node pins <= 8 GiB for
         # output whatever the sub-domain size (one step in flight beyond that)
-        depth = max(1, min(self.queue, PINNED_RING_BYTES // max(1, _snapshot_bytes(sim))))
+        depth = self._depth(sim)
         while len(self._pending) >= depth:
             self._commit_oldest()
         u, v, wait, mm = sim.snapshot_fields("output", depth=depth, minmax=True)
@@ -199,6 +199,18 @@ class SimulationOutput:
         self._pending.append((step, worker("gs-async-output").submit(job)))
         self.last_step = step
         return snap
+
+    def _depth(self, sim) -> int:
+        # the ring of pinned host snapshots is bounded in bytes, not in steps
+        return max(1, min(self.queue, PINNED_RING_BYTES // max(1, _snapshot_bytes(sim))))
+
+    def prepare(self, sim) -> None:
+        """Before the time loop (the driver's io_init phase): allocate the asynchronous output's
+        pinned host ring and events and take one snapshot into every ring slot, so the first
+        output steps do not pay the pinned allocations, the copy engines' first use of each
+        buffer or the snapshot kernel's code-object load inside the loop."""
+        if self.async_io and hasattr(sim, "prepare_snapshots"):
+            sim.prepare_snapshots("output", depth=self._depth(sim), minmax=True)
 
     def _commit_oldest(self) -> None:
         """Finish the oldest in-flight step: wait for its data write, gather the per-rank

@@ -436,6 +436,16 @@ class GrayScott:
     # scripts/profile_output.py --torch-snapshot)
     native_snapshot = True
 
+    def prepare_snapshots(self, slot: str, depth: int = 1, minmax: bool = False) -> None:
+        """Allocate ``slot``'s snapshot ring and fill every ring slot once (then wait): the
+        state is unchanged; later snapshots of that slot start from warm buffers."""
+        if self.backend != "hip":
+            return
+        wait = None
+        for _ in range(max(1, int(depth))):
+            wait = self.snapshot_fields(slot, depth=depth, minmax=minmax)[2]
+        wait()
+
     def _snapshot_torch(self, st, dev, host, minmax):
         cur = torch.cuda.current_stream(self.device)
         if st["done"] is not None:

@@ -61,6 +61,8 @@ def main(argv=None) -> int:
     ap.add_argument("--torch-snapshot", action="store_true",
                     help="the snapshot through torch calls instead of the native one (A/B)")
     ap.add_argument("--queue", type=int, default=0, help="output_queue (0: the setting's)")
+    ap.add_argument("--cprofile", action="store_true",
+                    help="also print the main thread's cProfile of the last run (top 25 by own time)")
     a = ap.parse_args(argv)
 
     from grayscott_amd import driver
@@ -90,7 +92,16 @@ def main(argv=None) -> int:
         if a.queue:
             s.output_queue = a.queue
         s.output = a.out or os.path.join(tempfile.gettempdir(), f"gs_prof_{os.getpid()}_{r}.bp")
+        pr = None
+        if a.cprofile and r == a.repeat - 1:
+            import cProfile
+            pr = cProfile.Profile()
+            pr.enable()
         res = driver.run(s, out=open(os.devnull, "w"))
+        if pr is not None:
+            pr.disable()
+            import pstats
+            pstats.Stats(pr, stream=sys.stderr).sort_stats("tottime").print_stats(25)
         steps_out = STATS["write_step"][0]
         rec = {"run": r, "snapshot": "torch" if a.torch_snapshot else "native",
                "queue": s.output_queue, "loop_s": round(res["loop_s"], 5), "compute_s": round(res["compute_s"], 5),
