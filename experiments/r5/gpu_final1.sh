@@ -1,0 +1,12 @@
+# Round 5: full GPU suite, the driver's bench command, a kernel-trace profile of the bench.
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/${GS_OUT:-r5f1}
+mkdir -p $O
+cd $R
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/tests.log 2>&1 &&
+timeout -k 10 200 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_driver.json 2> $O/bench_driver.err &&
+timeout -k 10 300 python bench.py > $O/bench_default.json 2> $O/bench_default.err &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o bench -- python3 bench.py --steps 100 --warmup 10 > $O/prof.log 2>&1
+echo "exit $?"
