@@ -178,6 +178,21 @@ __device__ __forceinline__ void gate_start(const FusedArgs& a, int pk, bool wait
         __hip_atomic_store(G.sflag[i], a.gate_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   if (!wait) return;  // a packer that needs no ghost cells marches at once
+  // the unpack's piece table -- the cone [X0, X0 + xw) x [Y0, Y0 + yext) x [za, zb)'s part of
+  // every received message, one flat index space again -- built while the exchange is in
+  // flight, so after the flags only the copies remain
+  if (tid < (uint32_t)G.nrecv) {
+    const Box b = G.rbox[tid];
+    const int x0 = max(b.x0, X0), x1 = min(b.x0 + b.nx, X0 + xw);
+    const int y0 = max(b.y0, Y0), y1 = min(b.y0 + b.ny, Y0 + yext);
+    const int z0 = max(b.z0, za), z1 = min(b.z0 + b.nz, zb);
+    const bool any = x0 < x1 && y0 < y1 && z0 < z1;
+    gp[tid] = GatePiece{const_cast<void*>(G.rsrc[slot][tid]), x0, y0, z0, x1 - x0, y1 - y0, 0u,
+                        b.x0, b.y0, b.z0, b.nx, b.ny, 0, any ? 1.0f / (float)(x1 - x0) : 0.f,
+                        any ? 1.0f / (float)(y1 - y0) : 0.f};
+    gcells[tid] = any ? (uint32_t)((x1 - x0) * (y1 - y0) * (z1 - z0)) : 0u;
+  }
+  number(G.nrecv);
   // 2. every receive peer's messages of this exchange have landed (bounded wait).  Relaxed
   // system-scope polls (the flags are uncached: every load reads memory).  No acquire fence (on
   // gfx950 an agent-scope acquire invalidates the XCD's L2, which the marching workgroups
@@ -202,21 +217,8 @@ __device__ __forceinline__ void gate_start(const FusedArgs& a, int pk, bool wait
     atomicMax(G.stamps + 3, w);
   }
   __syncthreads();
-  // 3. the ghost cells of this unit's level-0 cone [X0, X0 + xw) x [Y0, Y0 + yext) x [za, zb):
-  // the cone's part of every received message, one flat index space again
+  // 3. the ghost cells of this unit's level-0 cone (piece table built before the wait, above)
   const bool poison = __hip_atomic_load(G.dflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-  if (tid < (uint32_t)G.nrecv) {
-    const Box b = G.rbox[tid];
-    const int x0 = max(b.x0, X0), x1 = min(b.x0 + b.nx, X0 + xw);
-    const int y0 = max(b.y0, Y0), y1 = min(b.y0 + b.ny, Y0 + yext);
-    const int z0 = max(b.z0, za), z1 = min(b.z0 + b.nz, zb);
-    const bool any = x0 < x1 && y0 < y1 && z0 < z1;
-    gp[tid] = GatePiece{const_cast<void*>(G.rsrc[slot][tid]), x0, y0, z0, x1 - x0, y1 - y0, 0u,
-                        b.x0, b.y0, b.z0, b.nx, b.ny, 0, any ? 1.0f / (float)(x1 - x0) : 0.f,
-                        any ? 1.0f / (float)(y1 - y0) : 0.f};
-    gcells[tid] = any ? (uint32_t)((x1 - x0) * (y1 - y0) * (z1 - z0)) : 0u;
-  }
-  number(G.nrecv);
   {
     const uint32_t total = gtotal;
     const int np = gnp;
