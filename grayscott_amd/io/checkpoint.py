@@ -112,7 +112,17 @@ class CheckpointWriter:
         w = _open_writer(self.tmp, self.settings, self.domain, self.ctx)
         # its own snapshot buffers when not sharing the output step's: an output step still
         # being written must not see them overwritten
-        u, v, wait = snap if snap is not None else sim.snapshot_fields("checkpoint")
+        snap = snap if snap is not None else sim.snapshot_fields("checkpoint", minmax=True)
+        u, v, wait = snap[:3]
+        part = getattr(snap[3], "part", None) if len(snap) > 3 else None
+        from .output import _native_wait, _Ticket
+        fn, arg = _native_wait(wait)
+        if fn is not None:
+            # the whole step on the checkpoint writer's native thread (no Python beside the
+            # stepping): it waits for the snapshot's copy itself, then writes step / U / V
+            t = w.submit_step_uv(step, u, v, part, fn, arg)
+            self._pending = (w, _Ticket(w, t, (u, v, part, wait)))
+            return
 
         def job():
             wait()

@@ -162,7 +162,7 @@ class SimulationOutput:
         simulation: device snapshot + D2H on an I/O stream, data write on a host thread; the
         collective metadata gather of step n happens on the main thread when step
         n + queue is written (or at close), in step order, so no collective ever runs off the
-        main thread.  Returns the snapshot ``(u, v, wait)`` it writes from (None when
+        main thread.  Returns the snapshot ``(u, v, wait, mm)`` it writes from (None when
         synchronous), so an asynchronous checkpoint of the same step can share it; the caller
         must have finished every other reader of that snapshot before the output step that
         reuses its buffers (``queue`` steps later)."""
@@ -178,7 +178,7 @@ class SimulationOutput:
         while len(self._pending) >= depth:
             self._commit_oldest()
         u, v, wait, mm = sim.snapshot_fields("output", depth=depth, minmax=True)
-        snap = (u, v, wait)
+        snap = (u, v, wait, mm)
         part = getattr(mm, "part", None)
         fn, arg = _native_wait(wait)
         if fn is not None:
