@@ -307,17 +307,18 @@ def golden_check(sim, settings, dom, nsteps: int, init_seed):
     return err if err == err else float("inf")
 
 
-def parallelism_label(dims, transport: str, overlapped: bool) -> str:
+def parallelism_label(dims, transport: str, overlapped: bool, gated: bool = False) -> str:
     """``spatial-z-slabs 1x1x8 (ipc plane halos, overlapped)``, ``spatial-3d 2x2x2 (rccl packed
-    halos)``, ``spatial-3d 1x1x1``: the process grid, and with neighbours the halo transport
-    (z slabs exchange contiguous ghost planes in place, other grids packed faces / edges /
-    corners) and whether the exchange overlaps the inner update."""
+    halos)``, ``spatial-3d 2x2x2 (ipc packed halos, gated)``, ``spatial-3d 1x1x1``: the process
+    grid, and with neighbours the halo transport (z slabs exchange contiguous ghost planes in
+    place, other grids packed faces / edges / corners) and whether the exchange overlaps the
+    inner update -- gated: inside the pass's own fused launch (csrc/hip/gate.hpp)."""
     dstr = "x".join(str(int(d)) for d in dims)
     if all(int(d) == 1 for d in dims):
         return f"spatial-3d {dstr}"
     zslab = int(dims[0]) == 1 and int(dims[1]) == 1
     kind = "plane" if zslab else "packed"
-    tail = ", overlapped" if overlapped else ""
+    tail = ", gated" if gated else (", overlapped" if overlapped else "")
     return f"spatial-{'z-slabs' if zslab else '3d'} {dstr} ({transport} {kind} halos{tail})"
 
 
@@ -342,6 +343,7 @@ def summarize_profiles(rows):
     summary = {
         "passes": rows[0]["passes"], "steps_per_pass": rows[0]["depth"],
         "transport": rows[0]["transport"], "overlapped": rows[0]["overlapped"],
+        "gated": rows[0].get("gated", False), "gate": rows[0].get("gate"),
         "chained": rows[0].get("chained", False),
         "pass_us": round(max(r["pass_us"] for r in rows), 2),
         "phase_us": {k: round(max(r["phase_us"].get(k, 0.0) for r in rows), 2) for k in names},
@@ -550,7 +552,8 @@ def run(args) -> int:
                 "L": args.L,
                 "global_batch": 1,
                 "seq_len": args.L,
-                "parallelism": parallelism_label(dom.dims, sim.transport, sim.overlapped),
+                "parallelism": parallelism_label(dom.dims, sim.transport, sim.overlapped,
+                                                 sim.gated),
                 "dims": dom.dims,
                 "local_extent": dom.proc_sizes,
                 "fuse_steps": sim.depth, "ghost_width": sim.H,
@@ -558,6 +561,7 @@ def run(args) -> int:
                                  for n, c in sim.fused_choice().items()},
                 "transport": sim.transport,
                 "overlap": sim.overlapped,
+                "gated": sim.gated,
                 "noise": args.noise,
                 "backend": backend,
             },

@@ -324,6 +324,10 @@ class GrayScott:
                           if nb and data_us > 0 else None)
         r["transport"] = self.transport
         r["overlapped"] = bool(self.overlapped)
+        # gated passes: the exchange runs inside the "fused" phase (one launch per pass)
+        r["gated"] = bool(self.gated)
+        if r["gated"]:
+            r["gate"] = self.engine.gate_info(depth)
         r["chained"] = bool(chained)
         r["depth"] = depth
         return r

@@ -152,7 +152,7 @@ def time_data_path(settings, ctx, L: int, dims, fuse: int, steps: int = 30, warm
         sim.iterate(steps)
         sync()
         el = time.perf_counter() - t0
-        ovd = bool(sim.overlapped)
+        ovd = "gated" if sim.gated else bool(sim.overlapped)  # gated: the exchange in-kernel
     finally:
         sim.close()
     return ctx.allreduce(el, "max"), ovd

@@ -160,3 +160,5 @@ def test_parallelism_label():
     assert bench.parallelism_label([2, 2, 2], "rccl", False) == "spatial-3d 2x2x2 (rccl packed halos)"
     assert bench.parallelism_label([2, 2, 1], "ipc", True) == \
         "spatial-3d 2x2x1 (ipc packed halos, overlapped)"
+    assert bench.parallelism_label([2, 2, 2], "ipc", True, True) == \
+        "spatial-3d 2x2x2 (ipc packed halos, gated)"
