@@ -79,6 +79,9 @@ def parse_args(argv):
                     help="seconds from start after which every rank gives up: rank 0 prints a "
                          "JSON line with status 'timeout' (the phase it was in, the tuning rows "
                          "finished) and the job exits 124 (0 = off)")
+    ap.add_argument("--debug-knob", action="append", default=[], metavar="NAME=VALUE",
+                    help="set a native test switch on every rank (csrc/include/gs/debug.h; "
+                         "rehearsals on one GPU, e.g. gated=2)")
     ap.add_argument("--timeout", type=float, default=0.0,
                     help="self-launched jobs: kill all ranks after this many seconds (default: "
                          "the deadline + 60 s)")
@@ -408,6 +411,12 @@ def profile_reference_grid(settings, ctx, args, dims, row, passes: int):
 
 def run(args) -> int:
     import torch
+
+    if args.debug_knob and args.backend.lower() in ("amdgpu", "hip", "gpu"):
+        from grayscott_amd.ops import native
+        for kv in args.debug_knob:
+            name, _, value = kv.partition("=")
+            native.debug_set(name.strip(), float(value))
 
     from grayscott_amd.models.grayscott import GrayScott
     from grayscott_amd.parallel.decomp import choose_dims, dims_create, init_domain

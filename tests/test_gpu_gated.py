@@ -167,3 +167,27 @@ def test_gated_long_run():
     assert all(m["gated"] and m["step"] == steps for m in meta)
     np.testing.assert_array_equal(un, u1)
     np.testing.assert_array_equal(vn, v1)
+
+
+def test_bench_two_ranks_gated_data_path():
+    """bench.py with 2 ranks on the one GPU through the IPC transport, gated passes allowed on a
+    shared device (--debug-knob gated=2): the tuned data path runs gated, its JSON says so, and
+    the golden check of the timed path passes."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    from .mp_utils import ROOT
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--L", "96", "--steps", "12", "--warmup", "6",
+           "--transport", "ipc", "--decomposition", "balanced", "--overlap", "on", "--fuse", "3",
+           "--debug-knob", "gated=2", "--timeout", "400"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=480, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    d = json.loads(lines[-1])
+    assert d["value"] > 0 and d["check"]["golden_ok"], d.get("check")
+    assert d["config"]["gated"] and "gated" in d["config"]["parallelism"], d["config"]
