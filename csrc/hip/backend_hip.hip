@@ -958,7 +958,7 @@ class HipBackend final : public gs::Backend {
     gl.cnt = cnt_host_;
     gl.npk = npk_[n];
     if (d_stamps_) {  // debug knob gate_stamps: this launch's stamps only
-      const unsigned long long init[5] = {~0ull, 0ull, ~0ull, 0ull, 0ull};
+      const unsigned long long init[8] = {~0ull, 0ull, ~0ull, 0ull, 0ull, 0ull, 0ull, 0ull};
       HIP_CHECK(hipMemcpyAsync(d_stamps_, init, sizeof(init), hipMemcpyHostToDevice, stream_));
     }
     if (!gsk::launch_fused<T>(buf_[src], buf_[dst], g_, p_, n, t, stream_,
@@ -1019,18 +1019,23 @@ class HipBackend final : public gs::Backend {
   }
 
   // debug knob gate_stamps: the last gated launch's exchange, µs after its first packer
-  // started -- {last arrival (packing done), first wait done, last wait done, last unpack done}
-  void gate_stamps(double* out4) {
-    for (int i = 0; i < 4; ++i) out4[i] = -1.0;
+  // started -- {last arrival (packing done), first wait done, last wait done, last unpack done,
+  // the longest and the mean unpack of one unit}
+  void gate_stamps(double* out6) {
+    for (int i = 0; i < 6; ++i) out6[i] = -1.0;
     if (!d_stamps_) return;
     HIP_CHECK(hipStreamSynchronize(stream_));
-    unsigned long long h[5];
+    unsigned long long h[8];
     HIP_CHECK(hipMemcpy(h, d_stamps_, sizeof(h), hipMemcpyDeviceToHost));
     int khz = 0;
     HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev_));
     const double us = 1000.0 / (double)std::max(khz, 1);
-    for (int i = 0; i < 4; ++i) out4[i] = h[0] == ~0ull ? -1.0 : (double)(h[i + 1] - h[0]) * us;
+    if (h[0] == ~0ull) return;
+    for (int i = 0; i < 4; ++i) out6[i] = (double)(h[i + 1] - h[0]) * us;
+    out6[4] = (double)h[5] * us;                                  // longest unit unpack
+    out6[5] = h[7] ? (double)h[6] * us / (double)h[7] : 0.0;      // mean unit unpack
   }
+
 
   // {tuned xp (plane-times), units, packers, ms per pass} of depth n (-1: not tuned)
   void gate_info(int n, double* out4) const {
@@ -1603,9 +1608,9 @@ extern "C" int gs_snapshot(gs_engine* e, int32_t dtype, void* du, void* dv, void
   }
 }
 
-extern "C" int gs_gate_stamps(gs_engine* e, int32_t dtype, double* out4) {
+extern "C" int gs_gate_stamps(gs_engine* e, int32_t dtype, double* out6) {
   try {
-    with_hip_backend(e, dtype, [&](auto* b) { b->gate_stamps(out4); });
+    with_hip_backend(e, dtype, [&](auto* b) { b->gate_stamps(out6); });
     return 0;
   } catch (const std::exception& ex) {
     g_gs_err = ex.what();

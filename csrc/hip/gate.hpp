@@ -50,7 +50,8 @@ struct GateArgs {
   int* err;            // host-mapped: a wait timed out (the watchdog raises)
   int* dflag;          // device copy: later copies write NaN instead of stale landing data
   // debug knob gate_stamps: wall-clock stamps of the launch's exchange (null: none) --
-  // [0] min start, [1] max packer arrival, [2] min / [3] max wait done, [4] max unpack done
+  // [0] min start, [1] max packer arrival, [2] min / [3] max wait done, [4] max unpack done,
+  // [5] max / [6] sum of a unit's unpack duration (wait done -> unpack done), [7] units
   unsigned long long* stamps;
 };
 
@@ -211,10 +212,11 @@ __device__ __forceinline__ void gate_start(const FusedArgs& a, int pk, bool wait
   }
   if (G.min_ticks && tid == 0)
     while (wall_clock64() - t0 < G.min_ticks) __builtin_amdgcn_s_sleep(1);
+  unsigned long long wdone = 0;
   if (G.stamps && tid == 0) {
-    const unsigned long long w = (unsigned long long)wall_clock64();
-    atomicMin(G.stamps + 2, w);
-    atomicMax(G.stamps + 3, w);
+    wdone = (unsigned long long)wall_clock64();
+    atomicMin(G.stamps + 2, wdone);
+    atomicMax(G.stamps + 3, wdone);
   }
   __syncthreads();
   // 3. the ghost cells of this unit's level-0 cone (piece table built before the wait, above)
@@ -259,5 +261,11 @@ __device__ __forceinline__ void gate_start(const FusedArgs& a, int pk, bool wait
   // holds ghost cells, stale ones from before the copies above (buffer_inv sc0: L1 only)
   asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
   __syncthreads();
-  if (G.stamps && tid == 0) atomicMax(G.stamps + 4, (unsigned long long)wall_clock64());
+  if (G.stamps && tid == 0) {
+    const unsigned long long u = (unsigned long long)wall_clock64();
+    atomicMax(G.stamps + 4, u);
+    atomicMax(G.stamps + 5, u - wdone);
+    atomicAdd(G.stamps + 6, u - wdone);
+    atomicAdd(G.stamps + 7, 1ull);
+  }
 }
