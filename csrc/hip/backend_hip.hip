@@ -698,6 +698,7 @@ class HipBackend final : public gs::Backend {
     // peer processes on this same GPU (tests): their gated launches compete for its slots
     gate_sharers_ = 0;
     for (const PeerMap& pm : peers_) gate_sharers_ += (pm.rank != rank_ && pm.device == dev_) ? 1 : 0;
+    for (int& f : gate_fit_) f = -1;
     gate_release();
   }
 
@@ -803,7 +804,24 @@ class HipBackend final : public gs::Backend {
            !gs::debug_knobs().philox_generic &&
            // peers sharing this GPU: only when asked (debug knob gated = 2) -- every rank's
            // waiting units must be resident at once, across processes (gate_table)
-           (gate_sharers_ == 0 || gs::debug_knobs().gated >= 2);
+           (gate_sharers_ == 0 || gs::debug_knobs().gated >= 2) && gate_fits(n);
+  }
+
+  // whether a depth-n table fits the device's resident slots at all (its longest chunks: one
+  // unit per tile column, or per column end): more units than slots could leave a packer
+  // queued behind workgroups that wait for it -- e.g. a very flat sub-domain with more tile
+  // columns than workgroup slots keeps the stream-overlapped passes (cached per depth)
+  bool gate_fits(int n) const {
+    if (gate_fit_[n] < 0) {
+      try {
+        int npk = 0, slots = 0;
+        const size_t units = gate_table(n, 0, false, &npk, &slots, true).size();
+        gate_fit_[n] = units <= (size_t)slots ? 1 : 0;
+      } catch (const std::exception&) {
+        gate_fit_[n] = 0;  // no gated entry / occupancy for this shape: the stream path
+      }
+    }
+    return gate_fit_[n] == 1;
   }
 
   void gate_release() {
@@ -858,7 +876,8 @@ class HipBackend final : public gs::Backend {
   // chunks shorter by xp planes (the expected exchange time in plane-times): the smallest plane
   // budget per workgroup whose chunks fit the resident slots.  Sorted by (z0, tile): each XCD
   // group of workgroups gets a contiguous range (sched 3), i.e. neighbouring tiles at one depth.
-  std::vector<gsk::GateUnit> gate_table(int n, int xp, bool allpk, int* npk) const {
+  std::vector<gsk::GateUnit> gate_table(int n, int xp, bool allpk, int* npk,
+                                        int* slots_out = nullptr, bool longest = false) const {
     const int cfg = gsk::gated_shape_cfg(sizeof(T) == 8, g_, n);
     const char* name = gsk::fused_shape_name(cfg, sizeof(T) == 8, true);
     const gsk::TileGrid tg = gsk::fused_tile_grid(name, g_, n);
@@ -917,9 +936,10 @@ class HipBackend final : public gs::Backend {
       }
       return cnt;
     };
-    int tau = F + 1;
     const int tmax = F + xp + nz + 1;
+    int tau = longest ? tmax : F + 1;
     while (tau < tmax && build(tau, nullptr) > slots) ++tau;
+    if (slots_out) *slots_out = slots;
     std::vector<gsk::GateUnit> u;
     build(tau, &u);
     std::stable_sort(u.begin(), u.end(), [](const gsk::GateUnit& a, const gsk::GateUnit& b) {
@@ -1338,6 +1358,7 @@ class HipBackend final : public gs::Backend {
   gs::HaloPlan gplan_{};
   bool gate_plan_ok_ = false;
   int gate_sharers_ = 0;  // peer ranks (other processes) on this GPU
+  mutable int gate_fit_[4] = {-1, -1, -1, -1};  // gate_fits per depth (-1: not yet checked)
   bool gate_allpk_[4] = {false, false, false, false};  // tuned: every unit packs
   unsigned long long* d_stamps_ = nullptr;  // debug knob gate_stamps
   gsk::GateArgs* d_gate_ = nullptr;
