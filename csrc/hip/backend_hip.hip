@@ -888,70 +888,8 @@ class HipBackend final : public gs::Backend {
     if (per_cu < 1) throw std::runtime_error("gated pass: no gated entry for this shape");
     // (peer processes on this GPU, debug knob gated = 2: this rank's share of the slots)
     const int slots = std::max(8, num_cus() * per_cu / (gate_sharers_ + 1));
-    const int nz = g_.nz;
-    const gs::HaloPlan& p = gplan_;
-    auto dep = [&](int X0, int xw, int Y0, int ye, int z0, int z1) {
-      for (int i = 0; i < p.nrecv; ++i) {
-        const gs::Box& b = p.recv[i].box;
-        if (b.x0 < X0 + xw && X0 < b.x0 + b.nx && b.y0 < Y0 + ye && Y0 < b.y0 + b.ny &&
-            b.z0 < z1 + n && z0 - n < b.z0 + b.nz)
-          return true;
-      }
-      return false;
-    };
-    struct Col { bool strip, lo, hi; };
-    std::vector<Col> cols((size_t)tg.ntiles);
-    for (int t = 0; t < tg.ntiles; ++t) {
-      int X0, xw, Y0, ye;
-      gsk::tile_window(tg, t, n, &X0, &xw, &Y0, &ye);
-      cols[t].strip = dep(X0, xw, Y0, ye, n, nz - n);
-      cols[t].lo = dep(X0, xw, Y0, ye, 0, 1);
-      cols[t].hi = dep(X0, xw, Y0, ye, nz - 1, nz);
-    }
-    const int F = 5 * n;  // pipeline fill + ramp of a unit, in plane-times (launch model)
-    // chunk [a, b) into pieces of at most len; gated pieces get pk = 0 (numbered later)
-    auto build = [&](int tau, std::vector<gsk::GateUnit>* out) -> int {
-      const int lg = std::max(1, tau - F - xp), li = std::max(1, tau - F);
-      int cnt = 0;
-      auto sect = [&](int t, int a, int b, int len, bool gated) {
-        if (b <= a) return;
-        const int k = (b - a + len - 1) / len;
-        for (int i = 0; i < k; ++i) {
-          const int z0 = a + (int)((int64_t)(b - a) * i / k), z1 = a + (int)((int64_t)(b - a) * (i + 1) / k);
-          if (out) out->push_back(gsk::GateUnit{t, z0, z1, gated ? 0 : -1, gated ? 1 : 0});
-          ++cnt;
-        }
-      };
-      for (int t = 0; t < tg.ntiles; ++t) {
-        const Col& c = cols[t];
-        const int P = c.lo ? std::max(n, std::min(lg, nz)) : 0;
-        const int S = c.hi ? std::max(n, std::min(lg, nz)) : 0;
-        if (c.strip || P + S >= nz) {
-          sect(t, 0, nz, lg, true);
-        } else {
-          sect(t, 0, P, lg, true);
-          sect(t, P, nz - S, li, false);
-          sect(t, nz - S, nz, lg, true);
-        }
-      }
-      return cnt;
-    };
-    const int tmax = F + xp + nz + 1;
-    int tau = longest ? tmax : F + 1;
-    while (tau < tmax && build(tau, nullptr) > slots) ++tau;
     if (slots_out) *slots_out = slots;
-    std::vector<gsk::GateUnit> u;
-    build(tau, &u);
-    std::stable_sort(u.begin(), u.end(), [](const gsk::GateUnit& a, const gsk::GateUnit& b) {
-      return a.z0 != b.z0 ? a.z0 < b.z0 : a.tile < b.tile;
-    });
-    // packers: the start-gated units, or (allpk) every unit -- more CUs share the message
-    // stores, each ungated one marching after its share
-    int k = 0;
-    for (auto& x : u)
-      if (x.wait || allpk) x.pk = k++;
-    *npk = k;
-    return u;
+    return gs::gate_plan(tg, g_, gplan_, n, xp, allpk, slots, longest, npk);
   }
 
   void gate_upload(int n, const std::vector<gsk::GateUnit>& u, int npk) {

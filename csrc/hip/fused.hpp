@@ -39,12 +39,7 @@
 // messages straight into the peers' landing buffers, the last packer signals the peers, then it
 // waits for the peers' signals and copies the ghost cells of its own cone out of its landing
 // slot before marching.  Ungated units (cone clear of every face with a neighbour) march at once.
-struct GateUnit {
-  int32_t tile;    // tile index (this launch's enumeration)
-  int32_t z0, z1;  // output planes [z0, z1)
-  int32_t pk;      // >= 0: a packer, its index; -1: none (every start-gated unit packs)
-  int32_t wait;    // 1: start-gated (waits for the peers, copies its cone's ghosts)
-};
+using GateUnit = gs::GateUnit;  // a gated pass's unit (gs/gate_plan.h)
 struct GateArgs;  // gate.hpp
 
 struct FusedArgs {
@@ -1426,10 +1421,9 @@ struct GateLaunch {
 };
 
 // The tile grid a configuration's launch enumerates (FusedLaunch::run + fold_strip), on the host:
-// the gated pass's unit table names tiles by this enumeration.
-struct TileGrid {
-  int xstep, ystep, ybase, ntx, nty, ntxf, nfold, ntiles, rt;
-};
+// the gated pass's unit table names tiles by this enumeration (gs/gate_plan.h)
+using TileGrid = gs::TileGrid;
+using gs::tile_window;
 // the configuration run_fused_cfg actually launches for table entry cfg (variants exist for the
 // non-periodic, noisy, 32-bit-counter production path only; everything else runs the default)
 inline const char* fused_shape_name(int cfg, bool f64, bool variants) {
@@ -1448,46 +1442,11 @@ inline int gated_shape_cfg(bool f64, const Geom& g, int n) {
   return fused_cfg_applies(k, g, n) ? k : fused_cfg_lookup("4x12:1s");
 }
 inline TileGrid fused_tile_grid(const char* name, const Geom& g, int n) {
-  TileGrid t{};
   const int rows = atoi(name);
   const char* xp = strchr(name, 'x');
   const int waves = xp ? atoi(xp + 1) : 12;
   const size_t len = strlen(name);
-  const bool fold = len > 0 && name[len - 1] == 'f';
-  t.rt = rows * waves;
-  t.xstep = 64 - 2 * n;
-  t.ystep = (t.rt - 2 * n) & ~3;
-  t.ybase = -mod4(g.oy - n);
-  t.ntx = (g.nx + t.xstep - 1) / t.xstep;
-  t.nty = (g.ny - t.ybase + t.ystep - 1) / t.ystep;
-  t.ntxf = t.ntx;
-  t.nfold = 0;
-  t.ntiles = t.ntx * t.nty;
-  const int rem = g.nx - (t.ntx - 1) * t.xstep;
-  if (fold && t.ntx >= 2 && rem <= 32 - 2 * n) {
-    t.ntxf = t.ntx - 1;
-    t.nfold = (t.nty + 1) / 2;
-    t.ntiles = t.ntxf * t.nty + t.nfold;
-  }
-  return t;
-}
-// level-0 read window of tile `tile` in x / y: [X0, X0 + xw) x [Y0, Y0 + yext)
-inline void tile_window(const TileGrid& t, int tile, int n, int* X0, int* xw, int* Y0, int* yext) {
-  int tx, ty;
-  if (t.nfold && tile >= t.ntxf * t.nty) {
-    const int f = tile - t.ntxf * t.nty;
-    tx = t.ntxf;
-    ty = 2 * f;
-    *xw = 32;
-    *yext = t.rt + t.ystep;
-  } else {
-    tx = tile % t.ntxf;
-    ty = tile / t.ntxf;
-    *xw = 64;
-    *yext = t.rt;
-  }
-  *X0 = tx * t.xstep - n;
-  *Y0 = t.ybase + ty * t.ystep - n;
+  return gs::tile_grid(rows, waves, len > 0 && name[len - 1] == 'f', g, n);
 }
 
 template <typename T>

@@ -12,6 +12,7 @@
 
 #include "gs/common.h"
 #include "gs/debug.h"
+#include "gs/gate_plan.h"
 
 namespace gsk {
 

@@ -13,6 +13,7 @@
 
 #include "gs/capi.h"
 #include "gs/engine.h"
+#include "gs/gate_plan.h"
 
 gs::Backend* gs_make_backend(int32_t dtype, const gs::Geom& g, const gs::Params& p, void* b0,
                              void* b1, void* send, void* recv, void* stream);
@@ -70,6 +71,33 @@ int gs_set_loopback(gs_engine* e, int32_t on) { GS_TRY(e->eng->set_loopback(on !
 int gs_overlapped(gs_engine* e, int32_t k) { return e->eng->overlapped(k) ? 1 : 0; }
 int gs_chained(gs_engine* e, int32_t k) { return e->eng->chained(k) ? 1 : 0; }
 int gs_gated(gs_engine* e, int32_t k) { return e->eng->gated(k) ? 1 : 0; }
+
+// The gated pass's unit table (gs/gate_plan.h) for a sub-domain and neighbour set, host only:
+// tests check it on the CPU.  out: up to cap units of 5 int32 (tile, z0, z1, pk, wait); returns
+// the unit count (may exceed cap), -1 on bad arguments.  grid_out (9 int32): the TileGrid.
+int gs_gate_plan(const gs::Geom* g, const int32_t* nbr27, int32_t n, int32_t xp, int32_t allpk,
+                 int32_t slots, int32_t longest, int32_t rows, int32_t waves, int32_t fold,
+                 int32_t* out, int32_t cap, int32_t* npk, int32_t* grid_out) {
+  if (!g || !nbr27 || n < 1 || n > g->H || rows < 4 || waves < 1) return -1;
+  const gs::HaloPlan p = gs::make_halo_plan(*g, nbr27, true);
+  const gs::TileGrid tg = gs::tile_grid(rows, waves, fold != 0, *g, n);
+  int k = 0;
+  const std::vector<gs::GateUnit> u = gs::gate_plan(tg, *g, p, n, xp, allpk != 0, slots,
+                                                    longest != 0, &k);
+  for (size_t i = 0; i < u.size() && (int64_t)i < cap; ++i) {
+    out[5 * i] = u[i].tile;
+    out[5 * i + 1] = u[i].z0;
+    out[5 * i + 2] = u[i].z1;
+    out[5 * i + 3] = u[i].pk;
+    out[5 * i + 4] = u[i].wait;
+  }
+  if (npk) *npk = k;
+  if (grid_out) {
+    const int v[9] = {tg.xstep, tg.ystep, tg.ybase, tg.ntx, tg.nty, tg.ntxf, tg.nfold, tg.ntiles, tg.rt};
+    for (int i = 0; i < 9; ++i) grid_out[i] = v[i];
+  }
+  return (int)u.size();
+}
 int gs_set_gated(gs_engine* e, int32_t on) {
   e->eng->set_gated(on != 0);
   return 0;

@@ -210,6 +210,28 @@ def plan_sizes(g: Geom, nbr27, diagonals: bool):
     return int(s.value), int(r.value)
 
 
+def gate_plan(g: Geom, nbr27, n: int, xp: int = 0, allpk: bool = False, slots: int = 256,
+              longest: bool = False, rows: int = 4, waves: int = 12, fold: bool = False):
+    """The gated pass's unit table for a sub-domain (csrc/include/gs/gate_plan.h, host only):
+    ``(units, npk, grid)`` -- units as (tile, z0, z1, pk, wait) tuples, the packer count and the
+    tile grid {xstep, ystep, ybase, ntx, nty, ntxf, nfold, ntiles, rt}."""
+    lib = load("core")
+    lib.gs_gate_plan.restype = c_int
+    arr = (c_int32 * 27)(*nbr27)
+    grid = (c_int32 * 9)()
+    npk = c_int32()
+    cap = 1 << 16
+    out = (c_int32 * (5 * cap))()
+    k = lib.gs_gate_plan(ctypes.byref(g), arr, int(n), int(xp), 1 if allpk else 0, int(slots),
+                         1 if longest else 0, int(rows), int(waves), 1 if fold else 0, out, cap,
+                         ctypes.byref(npk), grid)
+    if k < 0 or k > cap:
+        raise ValueError(f"gs_gate_plan failed ({k})")
+    units = [tuple(out[5 * i:5 * i + 5]) for i in range(k)]
+    keys = ("xstep", "ystep", "ybase", "ntx", "nty", "ntxf", "nfold", "ntiles", "rt")
+    return units, int(npk.value), dict(zip(keys, list(grid)))
+
+
 def noise_block(gx, gy, gz4, Lx, Ly, step, seed):
     out = (c_uint32 * 4)()
     load("core").gs_noise_block(gx, gy, gz4, Lx, Ly, step, seed, out)

@@ -1,0 +1,112 @@
+"""The gated pass's unit table (csrc/include/gs/gate_plan.h), checked on the CPU against an
+independent computation of each unit's level-0 read box (the planner is shared by the HIP
+backend, backend_hip.hip gate_table; the GPU side is tests/test_gpu_gated.py).
+
+For every sub-domain / neighbour set: the units of each tile column partition its planes
+[0, nz); a unit is start-gated exactly when its read box -- the tile's x / y window x
+[z0 - n, z1 + n) -- meets a ghost region a neighbour fills (H cells deep on that side); the
+units fit the slots when some plane budget allows it; the table is sorted by (z0, tile) and the
+packers are numbered 0..npk-1 (the start-gated units, or every unit)."""
+import itertools
+
+import pytest
+
+from grayscott_amd.ops import native
+
+H = 3
+
+
+def _nbr(dirs):
+    """nbr27 with rank 0 at the given (dx, dy, dz) directions, -1 elsewhere (index
+    (dx + 1) * 9 + (dy + 1) * 3 + (dz + 1))."""
+    out = [-1] * 27
+    for dx, dy, dz in dirs:
+        out[(dx + 1) * 9 + (dy + 1) * 3 + (dz + 1)] = 0
+    return out
+
+
+def _ghost_regions(nx, ny, nz, dirs):
+    def rng(d, n):
+        return (-H, 0) if d < 0 else ((n, n + H) if d > 0 else (0, n))
+    return [(rng(dx, nx), rng(dy, ny), rng(dz, nz)) for dx, dy, dz in dirs]
+
+
+def _window(grid, tile, n):
+    """Independent copy of the kernel's tile window (fused.hpp fused_body / gate prologue)."""
+    if grid["nfold"] and tile >= grid["ntxf"] * grid["nty"]:
+        f = tile - grid["ntxf"] * grid["nty"]
+        tx, ty, xw, ye = grid["ntxf"], 2 * f, 32, grid["rt"] + grid["ystep"]
+    else:
+        tx, ty, xw, ye = tile % grid["ntxf"], tile // grid["ntxf"], 64, grid["rt"]
+    x0 = tx * grid["xstep"] - n
+    y0 = grid["ybase"] + ty * grid["ystep"] - n
+    return (x0, x0 + xw), (y0, y0 + ye)
+
+
+def _meets(a, b):
+    return a[0] < b[1] and b[0] < a[1]
+
+
+ONE_SIDED = [d for d in itertools.product((0, 1), repeat=3) if d != (0, 0, 0)]
+ALL26 = [d for d in itertools.product((-1, 0, 1), repeat=3) if d != (0, 0, 0)]
+Z_ONLY = [(0, 0, -1), (0, 0, 1)]
+X_SPLIT = [(1, 0, 0)]
+
+
+@pytest.mark.parametrize("shape,dirs,n,fold,xp,allpk,slots", [
+    ((64, 64, 64), Z_ONLY, 3, False, 0, False, 256),
+    ((256, 256, 64), Z_ONLY, 3, False, 16, False, 256),
+    ((128, 128, 128), ONE_SIDED, 3, True, 8, False, 256),
+    ((256, 256, 256), ONE_SIDED, 3, True, 16, True, 256),
+    ((96, 80, 72), ALL26, 2, False, 4, False, 128),
+    ((40, 40, 40), ALL26, 3, False, 0, False, 256),
+    ((32, 64, 64), X_SPLIT, 3, False, 24, True, 64),
+    ((512, 512, 8), Z_ONLY, 3, False, 0, False, 64),  # more columns than slots
+])
+def test_gate_plan_matches_independent_cones(shape, dirs, n, fold, xp, allpk, slots):
+    nx, ny, nz = shape
+    g = native.make_geom(nx, ny, nz, H, 0, 0, 0, nx * 2, ny * 2, nz * 2, False)
+    units, npk, grid = native.gate_plan(g, _nbr(dirs), n, xp=xp, allpk=allpk, slots=slots,
+                                        fold=fold)
+    ghosts = _ghost_regions(nx, ny, nz, dirs)
+    # each column's units partition [0, nz)
+    by_tile = {}
+    for t, z0, z1, pk, wait in units:
+        assert 0 <= t < grid["ntiles"] and 0 <= z0 < z1 <= nz
+        by_tile.setdefault(t, []).append((z0, z1))
+    assert sorted(by_tile) == list(range(grid["ntiles"]))
+    for t, iv in by_tile.items():
+        iv.sort()
+        assert iv[0][0] == 0 and iv[-1][1] == nz
+        assert all(a[1] == b[0] for a, b in zip(iv, iv[1:])), (t, iv)
+    # start-gated exactly when the read box meets a neighbour's ghost region
+    for t, z0, z1, pk, wait in units:
+        xr, yr = _window(grid, t, n)
+        zr = (z0 - n, z1 + n)
+        need = any(_meets(xr, gx) and _meets(yr, gy) and _meets(zr, gz) for gx, gy, gz in ghosts)
+        assert bool(wait) == need, (t, z0, z1, wait, need)
+    # fits the slots whenever the longest chunks do
+    longest, _, _ = native.gate_plan(g, _nbr(dirs), n, xp=xp, allpk=allpk, slots=slots,
+                                     fold=fold, longest=True)
+    if len(longest) <= slots:
+        assert len(units) <= slots
+    # order and packer numbering
+    assert units == sorted(units, key=lambda u: (u[1], u[0]))
+    pks = [u[3] for u in units if u[3] >= 0]
+    assert sorted(pks) == list(range(npk))
+    if allpk:
+        assert npk == len(units)
+    else:
+        assert all((u[3] >= 0) == bool(u[4]) for u in units)
+
+
+def test_gate_plan_tile_grid_matches_the_kernel():
+    """The planner's tile grid is the launch's (FusedLaunch::run + fold_strip): L=256, n=3,
+    4x12 tiles (58 x 40 outputs), the folded last x strip -- 4 x 7 full tiles + 4 folded units
+    = 32 tiles."""
+    g = native.make_geom(256, 256, 256, H, 0, 0, 0, 256, 256, 256, False)
+    _, _, grid = native.gate_plan(g, _nbr(Z_ONLY), 3, fold=True)
+    assert (grid["xstep"], grid["ystep"], grid["ntx"], grid["nty"]) == (58, 40, 5, 7)
+    assert (grid["ntxf"], grid["nfold"], grid["ntiles"]) == (4, 4, 32)
+    _, _, grid = native.gate_plan(g, _nbr(Z_ONLY), 3, fold=False)
+    assert grid["ntiles"] == 35
