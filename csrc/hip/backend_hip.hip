@@ -834,7 +834,11 @@ class HipBackend final : public gs::Backend {
     d_gate_ = nullptr;
     d_counter_ = nullptr;
     cnt_host_ = 0;
-    for (int i = 0; i < 4; ++i) { gate_tuned_[i] = false; nunits_[i] = npk_[i] = 0; gate_xp_[i] = -1; }
+    for (int i = 0; i < 4; ++i) {
+      gate_tuned_[i] = pairs_[i] = false;
+      nunits_[i] = npk_[i] = 0;
+      gate_xp_[i] = gate_u_[i] = -1;
+    }
   }
 
   // the transport half of the launch arguments (device copy, built once per IPC connection)
@@ -876,8 +880,11 @@ class HipBackend final : public gs::Backend {
   // chunks shorter by xp planes (the expected exchange time in plane-times): the smallest plane
   // budget per workgroup whose chunks fit the resident slots.  Sorted by (z0, tile): each XCD
   // group of workgroups gets a contiguous range (sched 3), i.e. neighbouring tiles at one depth.
+  // pairs (U >= 0): the two-entries-per-workgroup table, xp the expected exchange and U the
+  // cone unpack in plane-times (gs::gate_plan_pairs; empty when none fits the slots)
   std::vector<gsk::GateUnit> gate_table(int n, int xp, bool allpk, int* npk,
-                                        int* slots_out = nullptr, bool longest = false) const {
+                                        int* slots_out = nullptr, bool longest = false,
+                                        int U = -1) const {
     const int cfg = gsk::gated_shape_cfg(sizeof(T) == 8, g_, n);
     const char* name = gsk::fused_shape_name(cfg, sizeof(T) == 8, true);
     const gsk::TileGrid tg = gsk::fused_tile_grid(name, g_, n);
@@ -889,10 +896,12 @@ class HipBackend final : public gs::Backend {
     // (peer processes on this GPU, debug knob gated = 2: this rank's share of the slots)
     const int slots = std::max(8, num_cus() * per_cu / (gate_sharers_ + 1));
     if (slots_out) *slots_out = slots;
+    if (U >= 0) return gs::gate_plan_pairs(tg, g_, gplan_, n, xp, U, allpk, slots, npk);
     return gs::gate_plan(tg, g_, gplan_, n, xp, allpk, slots, longest, npk);
   }
 
-  void gate_upload(int n, const std::vector<gsk::GateUnit>& u, int npk) {
+  void gate_upload(int n, const std::vector<gsk::GateUnit>& u, int npk, bool pairs) {
+    pairs_[n] = pairs;
     const size_t bytes = std::max<size_t>(u.size(), 1) * sizeof(gsk::GateUnit);
     if (!d_units_[n] || cap_units_[n] < u.size()) {
       if (d_units_[n]) (void)hipFree(d_units_[n]);
@@ -915,6 +924,7 @@ class HipBackend final : public gs::Backend {
     cnt_host_ += (uint32_t)npk_[n];
     gl.cnt = cnt_host_;
     gl.npk = npk_[n];
+    gl.pairs = pairs_[n] ? 1 : 0;
     if (d_stamps_) {  // debug knob gate_stamps: this launch's stamps only
       const unsigned long long init[8] = {~0ull, 0ull, ~0ull, 0ull, 0ull, 0ull, 0ull, 0ull};
       HIP_CHECK(hipMemcpyAsync(d_stamps_, init, sizeof(init), hipMemcpyHostToDevice, stream_));
@@ -933,34 +943,48 @@ class HipBackend final : public gs::Backend {
   void gate_tune(int src, int dst, int n, int64_t t) {
     if (!tuned_[n]) autotune(src, dst, n, t);
     gate_setup();
-    static const int kXp[] = {0, 4, 8, 16, 24, 32};
+    // candidates: one-unit tables (expected exchange xp, packers) and pairs tables (an ungated
+    // chunk before each start-gated one: exchange X, unpack U); every rank times the same list
+    struct Cand { int xp, U; bool all; };
+    std::vector<Cand> cands;
+    const int mode = gs::debug_knobs().gate_mode;  // 1: one-unit only, 2: pairs only (tests)
+    for (int all = 0; all < 2; ++all) {
+      if (mode != 2)
+        for (int xp : {0, 4, 8, 16, 24, 32}) cands.push_back({xp, -1, all != 0});
+      if (mode != 1)
+        for (int X : {8, 16, 24, 32})
+          for (int U : {4, 8}) cands.push_back({X, U, all != 0});
+    }
     float best = 1e30f;
-    int bxp = 0;
-    bool ball = false;
+    Cand bc = cands[0];
     hipEvent_t e0, e1;
     HIP_CHECK(hipEventCreate(&e0));
     HIP_CHECK(hipEventCreate(&e1));
-    for (int all = 0; all < 2; ++all)
-      for (int xp : kXp) {
-        int npk = 0;
-        const std::vector<gsk::GateUnit> u = gate_table(n, xp, all != 0, &npk);
-        gate_upload(n, u, npk);
-        gate_launch(src, dst, n, t);  // warm-up
-        HIP_CHECK(hipEventRecord(e0, stream_));
-        for (int r = 0; r < 3; ++r) gate_launch(src, dst, n, t);
-        HIP_CHECK(hipEventRecord(e1, stream_));
-        wait_all(gs::comm_timeout_s());
-        float ms = 0.f;
-        HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
-        if (ms < best) { best = ms; bxp = xp; ball = all != 0; }
-      }
+    for (const Cand& c : cands) {
+      int npk = 0;
+      std::vector<gsk::GateUnit> u = gate_table(n, c.xp, c.all, &npk, nullptr, false, c.U);
+      const bool pairs = c.U >= 0 && !u.empty();
+      // no pairs table fits this rank: it still makes the candidate's launches (with a one-unit
+      // table), so every rank takes part in the same number of exchanges
+      if (u.empty()) u = gate_table(n, 0, c.all, &npk);
+      gate_upload(n, u, npk, pairs);
+      gate_launch(src, dst, n, t);  // warm-up
+      HIP_CHECK(hipEventRecord(e0, stream_));
+      for (int r = 0; r < 3; ++r) gate_launch(src, dst, n, t);
+      HIP_CHECK(hipEventRecord(e1, stream_));
+      wait_all(gs::comm_timeout_s());
+      float ms = 0.f;
+      HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+      if (ms < best && (c.U < 0 || pairs)) { best = ms; bc = c; }
+    }
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     int npk = 0;
-    const std::vector<gsk::GateUnit> u = gate_table(n, bxp, ball, &npk);
-    gate_upload(n, u, npk);
-    gate_xp_[n] = bxp;
-    gate_allpk_[n] = ball;
+    const std::vector<gsk::GateUnit> u = gate_table(n, bc.xp, bc.all, &npk, nullptr, false, bc.U);
+    gate_upload(n, u, npk, bc.U >= 0);
+    gate_xp_[n] = bc.xp;
+    gate_u_[n] = bc.U;
+    gate_allpk_[n] = bc.all;
     gate_ms_[n] = best / 3.f;
     gate_tuned_[n] = true;
   }
@@ -995,12 +1019,14 @@ class HipBackend final : public gs::Backend {
   }
 
 
-  // {tuned xp (plane-times), units, packers, ms per pass} of depth n (-1: not tuned)
-  void gate_info(int n, double* out4) const {
-    out4[0] = gate_xp_[n];
-    out4[1] = nunits_[n];
-    out4[2] = npk_[n];
-    out4[3] = gate_ms_[n];
+  // {tuned xp (plane-times), table entries, packers, ms per pass, pairs U (-1: one-unit
+  // table)} of depth n (xp -1: not tuned)
+  void gate_info(int n, double* out5) const {
+    out5[0] = gate_xp_[n];
+    out5[1] = nunits_[n];
+    out5[2] = npk_[n];
+    out5[3] = gate_ms_[n];
+    out5[4] = gate_u_[n];
   }
 
   // Forget the device transport after a failed trial (the "auto" fallback chain): abort the
@@ -1298,6 +1324,8 @@ class HipBackend final : public gs::Backend {
   int gate_sharers_ = 0;  // peer ranks (other processes) on this GPU
   mutable int gate_fit_[4] = {-1, -1, -1, -1};  // gate_fits per depth (-1: not yet checked)
   bool gate_allpk_[4] = {false, false, false, false};  // tuned: every unit packs
+  bool pairs_[4] = {false, false, false, false};       // the uploaded table is a pairs table
+  int gate_u_[4] = {-1, -1, -1, -1};                   // tuned pairs U (-1: one-unit table)
   unsigned long long* d_stamps_ = nullptr;  // debug knob gate_stamps
   gsk::GateArgs* d_gate_ = nullptr;
   uint32_t* d_counter_ = nullptr;
@@ -1513,10 +1541,10 @@ int gs_fused_choice(gs_engine* e, int32_t n, int32_t dtype, int32_t* out2, float
 
 // the gated pass of depth n: out4 = {tuned expected exchange (plane-times, -1: not tuned),
 // units, packers, ms per pass measured while tuning}
-extern "C" int gs_gate_info(gs_engine* e, int32_t n, int32_t dtype, double* out4) {
+extern "C" int gs_gate_info(gs_engine* e, int32_t n, int32_t dtype, double* out5) {
   if (n < 0 || n > 3) return -1;
   try {
-    with_hip_backend(e, dtype, [&](auto* b) { b->gate_info(n, out4); });
+    with_hip_backend(e, dtype, [&](auto* b) { b->gate_info(n, out5); });
     return 0;
   } catch (const std::exception& ex) {
     g_gs_err = ex.what();

@@ -84,11 +84,17 @@ struct FusedArgs {
   uint32_t gate_cnt;
   int32_t gate_npk;  // packers of this launch (its start-gated units)
   int32_t ngunits;
+  int32_t gate_pairs;  // 1: two table entries per workgroup (gs::gate_plan_pairs)
 };
 
 template <typename T>
 __device__ __forceinline__ void gate_start(const FusedArgs& a, int pk, bool wait, int X0, int xw,
                                         int Y0, int yext, int za, int zb);
+template <typename T>
+__device__ __forceinline__ void gate_pack(const FusedArgs& a, int pk);
+template <typename T, int BATCH>
+__device__ __forceinline__ void gate_unpack(const FusedArgs& a, int X0, int xw, int Y0, int yext,
+                                         int za, int zb);
 
 template <typename T> struct PairT;
 template <> struct PairT<float> { typedef float type __attribute__((ext_vector_type(2))); };
@@ -753,6 +759,26 @@ __device__ __forceinline__ bool fused_period(FusedState<C>& S,
   }
 }
 
+// level-0 read window of tile `tile` in x / y (gs::tile_window on the device)
+template <class C>
+__device__ __forceinline__ void gate_cone(const FusedArgs& a, int tile, int* X0, int* xw, int* Y0,
+                                          int* yext) {
+  constexpr int TL = C::TL;
+  *xw = 64;
+  *yext = C::WAVES * C::ROWS;
+  if (C::FOLD && tile >= a.ntxf * a.nty) {
+    const int f2 = tile - a.ntxf * a.nty;
+    *X0 = a.ntxf * a.xstep - TL;
+    *Y0 = a.ybase + 2 * f2 * a.ystep - TL;
+    *xw = 32;
+    *yext += a.ystep;
+  } else {
+    const int ntxe = C::FOLD ? a.ntxf : a.ntx;
+    *X0 = (tile % ntxe) * a.xstep - TL;
+    *Y0 = a.ybase + (tile / ntxe) * a.ystep - TL;
+  }
+}
+
 // The kernel body; GATED: the gated pass's entry (k_fused_gated, sched 3), whose prologue
 // carries the halo exchange (gate.hpp).  The plain entry compiles without any of it.
 template <class C, typename T, bool GATED>
@@ -815,28 +841,28 @@ __device__ __forceinline__ void fused_body(const typename C::V2* __restrict__ s,
     lstep = gridDim.x / 8;
     if (lu0 >= lu1) return;
   } else if (GATED) {
-    // gated pass: one table unit per workgroup, each XCD group a contiguous range (the host
-    // orders the table by z, then tile)
-    lu0 = (b % 8) * a.grpM + b / 8;
-    lu1 = lu0 + 1;
-    if (lu0 >= a.ngunits) return;
-    // a start-gated unit packs, signals, waits and fills its cone's ghost cells first -- here,
-    // before the march state below is live, so the production loop's registers are untouched
-    const GateUnit un = a.gunits[lu0];
-    if (un.pk >= 0) {  // (a start-gated unit is always a packer)
-      int X0, xw = 64, Y0, yext = WAVES * ROWS;
-      if (C::FOLD && un.tile >= a.ntxf * a.nty) {
-        const int f2 = un.tile - a.ntxf * a.nty;
-        X0 = a.ntxf * a.xstep - TL;
-        Y0 = a.ybase + 2 * f2 * a.ystep - TL;
-        xw = 32;
-        yext += a.ystep;
-      } else {
-        const int ntxe = C::FOLD ? a.ntxf : a.ntx;
-        X0 = (un.tile % ntxe) * a.xstep - TL;
-        Y0 = a.ybase + (un.tile / ntxe) * a.ystep - TL;
+    // gated pass: one table unit per workgroup (pairs: two entries, an ungated chunk then a
+    // start-gated one), each XCD group a contiguous range (the host orders the table by z, then
+    // tile)
+    const int w = (b % 8) * a.grpM + b / 8;
+    if (a.gate_pairs) {
+      if (2 * w >= a.ngunits) return;
+      lu0 = 2 * w;
+      lu1 = lu0 + 2;
+      const GateUnit e0 = a.gunits[lu0];
+      if (e0.pk >= 0) gate_pack<T>(a, e0.pk);  // the wait comes before the second entry
+    } else {
+      lu0 = w;
+      lu1 = lu0 + 1;
+      if (lu0 >= a.ngunits) return;
+      // a start-gated unit packs, signals, waits and fills its cone's ghost cells first -- here,
+      // before the march state below is live, so the production loop's registers are untouched
+      const GateUnit un = a.gunits[lu0];
+      if (un.pk >= 0) {  // (a start-gated unit is always a packer)
+        int X0, xw, Y0, yext;
+        gate_cone<C>(a, un.tile, &X0, &xw, &Y0, &yext);
+        gate_start<T>(a, un.pk, un.wait != 0, X0, xw, Y0, yext, un.z0 - TL, un.z1 + TL);
       }
-      gate_start<T>(a, un.pk, un.wait != 0, X0, xw, Y0, yext, un.z0 - TL, un.z1 + TL);
     }
   }
   FusedState<C> S;
@@ -891,6 +917,14 @@ __device__ __forceinline__ void fused_body(const typename C::V2* __restrict__ s,
       uend = (int64_t)(blockIdx.x + 1) * U / gridDim.x;
     } else if (GATED) {
       const GateUnit un = a.gunits[lu];
+      if (un.tile < 0) continue;  // an empty entry of a pairs table (uniform per workgroup)
+      if (a.gate_pairs && un.wait) {
+        // the second entry of a pair: the peers' flags and the cone's ghosts, after the first
+        // entry's march (which covered the exchange)
+        int X0, xw, Y0, yext;
+        gate_cone<C>(a, un.tile, &X0, &xw, &Y0, &yext);
+        gate_unpack<T, 4>(a, X0, xw, Y0, yext, un.z0 - TL, un.z1 + TL);
+      }
       u = (int64_t)un.tile * nzv + (un.z0 - a.zlo[0]);
       uend = (int64_t)un.tile * nzv + (un.z1 - a.zlo[0]);
     } else {
@@ -1071,7 +1105,7 @@ struct FusedLaunch {
       // gated pass: the table holds one unit per workgroup (sized by the host to the slots)
       if constexpr (C::GATE_OK) {
         a.nchunk = 1;
-        a.grpM = (a.ngunits + 7) / 8;
+        a.grpM = ((a.gate_pairs ? a.ngunits / 2 : a.ngunits) + 7) / 8;
         const FoldCoef<T> f = make_fold<T>(p);
         k_fused_gated<C, T><<<(unsigned)(8 * a.grpM), 64 * C::WAVES, 0, st>>>(
             (const typename C::V2*)s, (typename C::V2*)d, a, f, p.seed);
@@ -1418,6 +1452,7 @@ struct GateLaunch {
   uint64_t n;
   uint32_t cnt;
   int32_t npk;
+  int32_t pairs;  // the table holds two entries per workgroup
 };
 
 // The tile grid a configuration's launch enumerates (FusedLaunch::run + fold_strip), on the host:
@@ -1492,6 +1527,8 @@ bool launch_fused(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, co
     a.gate_n = gate->n;
     a.gate_cnt = gate->cnt;
     a.gate_npk = gate->npk;
+    a.gate_pairs = gate->pairs ? 1 : 0;
+    if (a.gate_pairs && (gate->nunits & 1)) return false;
     a.allow_block = 0;
   } else if (a.sched == 3) {
     a.sched = 2;  // the gated schedule needs its table

@@ -84,9 +84,10 @@ __device__ __forceinline__ uint32_t gate_div(uint32_t k, uint32_t d, float inv) 
   return q;
 }
 
+// 1. pack + arrive: this packer's share of every outgoing message, then its arrival at the
+// pass's counter (the last arrival publishes the exchange)
 template <typename T>
-__device__ __forceinline__ void gate_start(const FusedArgs& a, int pk, bool wait, int X0, int xw,
-                                        int Y0, int yext, int za, int zb) {
+__device__ __forceinline__ void gate_pack(const FusedArgs& a, int pk) {
   using V2 = typename Vec2<T>::type;
   constexpr int B = gate_batch<T>();
   const GateArgs& G = *a.gate;
@@ -178,7 +179,43 @@ __device__ __forceinline__ void gate_start(const FusedArgs& a, int pk, bool wait
       for (int i = 0; i < G.nsig; ++i)
         __hip_atomic_store(G.sflag[i], a.gate_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  if (!wait) return;  // a packer that needs no ghost cells marches at once
+}
+
+// 2. + 3. wait for the peers' flags and copy the ghost cells of the level-0 cone
+// [X0, X0 + xw) x [Y0, Y0 + yext) x [za, zb) out of the landing slot
+template <typename T, int BATCH = gate_batch<T>()>
+__device__ __forceinline__ void gate_unpack(const FusedArgs& a, int X0, int xw, int Y0, int yext,
+                                         int za, int zb) {
+  using V2 = typename Vec2<T>::type;
+  constexpr int B = BATCH;  // (a pairs table's second entry unpacks with the march state live)
+  const GateArgs& G = *a.gate;
+  const Geom& g = a.g;
+  const int slot = (int)(a.gate_n & 1);
+  const uint32_t nt = blockDim.x, tid = threadIdx.x;
+  const uint64_t t0 = wall_clock64();
+  V2* f = (V2*)a.field;
+  __shared__ GatePiece gp[gs::kMaxMsgs];
+  __shared__ uint32_t gcells[gs::kMaxMsgs];
+  __shared__ uint32_t gtotal;
+  __shared__ int gnp;
+  // the piece table: one thread per message (their loads of the arguments in parallel), then
+  // thread 0 numbers the cells (and drops empty pieces) in LDS
+  auto number = [&](int nmsg) {
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t acc = 0;
+      int np = 0;
+      for (int m = 0; m < nmsg; ++m) {
+        if (!gcells[m]) continue;
+        if (np != m) gp[np] = gp[m];
+        gp[np++].start = acc;
+        acc += gcells[m];
+      }
+      gtotal = acc;
+      gnp = np;
+    }
+    __syncthreads();
+  };
   // the unpack's piece table -- the cone [X0, X0 + xw) x [Y0, Y0 + yext) x [za, zb)'s part of
   // every received message, one flat index space again -- built while the exchange is in
   // flight, so after the flags only the copies remain
@@ -268,4 +305,12 @@ __device__ __forceinline__ void gate_start(const FusedArgs& a, int pk, bool wait
     atomicAdd(G.stamps + 6, u - wdone);
     atomicAdd(G.stamps + 7, 1ull);
   }
+}
+
+// a start-gated unit in the one-unit table: pack (a packer), then wait and unpack (gated)
+template <typename T>
+__device__ __forceinline__ void gate_start(const FusedArgs& a, int pk, bool wait, int X0, int xw,
+                                        int Y0, int yext, int za, int zb) {
+  if (pk >= 0) gate_pack<T>(a, pk);
+  if (wait) gate_unpack<T, gate_batch<T>()>(a, X0, xw, Y0, yext, za, zb);
 }

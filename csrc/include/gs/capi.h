@@ -28,7 +28,8 @@ int gs_chained(gs_engine* e, int32_t k);         // 1 if runs of k-step passes a
 int gs_set_gated(gs_engine* e, int32_t on);      // allow (1) / forbid (0) gated passes
 int gs_gate_plan(const gs::Geom* g, const int32_t* nbr27, int32_t n, int32_t xp, int32_t allpk,
                  int32_t slots, int32_t longest, int32_t rows, int32_t waves, int32_t fold,
-                 int32_t* out, int32_t cap, int32_t* npk, int32_t* grid_out);  // gs/gate_plan.h
+                 int32_t pairs, int32_t unpack, int32_t* out, int32_t cap, int32_t* npk,
+                 int32_t* grid_out);  // gs/gate_plan.h
 int gs_gated(gs_engine* e, int32_t k);           // 1 if k-step passes carry the exchange in-kernel (gate.hpp)
 int gs_depth(gs_engine* e);                      // steps per pass (fuse, or the measured depth)
 int gs_set_auto_depth(gs_engine* e, int32_t on);  // let prepare() pick the depth (single rank)

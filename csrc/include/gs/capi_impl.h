@@ -75,15 +75,18 @@ int gs_gated(gs_engine* e, int32_t k) { return e->eng->gated(k) ? 1 : 0; }
 // The gated pass's unit table (gs/gate_plan.h) for a sub-domain and neighbour set, host only:
 // tests check it on the CPU.  out: up to cap units of 5 int32 (tile, z0, z1, pk, wait); returns
 // the unit count (may exceed cap), -1 on bad arguments.  grid_out (9 int32): the TileGrid.
+// pairs: the two-units-per-workgroup table (xp = the expected exchange X, unpack = U).
 int gs_gate_plan(const gs::Geom* g, const int32_t* nbr27, int32_t n, int32_t xp, int32_t allpk,
                  int32_t slots, int32_t longest, int32_t rows, int32_t waves, int32_t fold,
-                 int32_t* out, int32_t cap, int32_t* npk, int32_t* grid_out) {
+                 int32_t pairs, int32_t unpack, int32_t* out, int32_t cap, int32_t* npk,
+                 int32_t* grid_out) {
   if (!g || !nbr27 || n < 1 || n > g->H || rows < 4 || waves < 1) return -1;
   const gs::HaloPlan p = gs::make_halo_plan(*g, nbr27, true);
   const gs::TileGrid tg = gs::tile_grid(rows, waves, fold != 0, *g, n);
   int k = 0;
-  const std::vector<gs::GateUnit> u = gs::gate_plan(tg, *g, p, n, xp, allpk != 0, slots,
-                                                    longest != 0, &k);
+  const std::vector<gs::GateUnit> u =
+      pairs ? gs::gate_plan_pairs(tg, *g, p, n, xp, unpack, allpk != 0, slots, &k)
+            : gs::gate_plan(tg, *g, p, n, xp, allpk != 0, slots, longest != 0, &k);
   for (size_t i = 0; i < u.size() && (int64_t)i < cap; ++i) {
     out[5 * i] = u[i].tile;
     out[5 * i + 1] = u[i].z0;

@@ -25,6 +25,8 @@
 //   ipc_pair_same_dir 0 (default); 1: modelling only -- a loopback IPC message lands in the ghost
 //                   box of its own direction, so one rank can time a one-sided neighbour set
 //                   (+x, +y, +z: a 2x2x2 rank); the values are no wrap.  Read at connect.
+//   gate_mode       0 (default): the gated pass's tuner times one-unit and pairs tables; 1: one-unit
+//                   tables only; 2: pairs tables only (tests of each kernel path).  Read at tuning.
 //   cpu_ftz         1 (default): the CPU solver flushes fp32 denormals in its step region
 //                   (MXCSR FTZ + DAZ; ~100x faster where the reference example's v field
 //                   passes through them); 0: IEEE denormals, the reference's and the GPU's
@@ -42,6 +44,7 @@ struct DebugKnobs {
   int ipc_system_stores = 0;
   int gate_stamps = 0;
   int ipc_pair_same_dir = 0;
+  int gate_mode = 0;
   int cpu_ftz = 1;
   int gated = 1;
 };
@@ -61,6 +64,7 @@ inline int debug_set(const char* name, double value) {
   else if (!strcmp(name, "ipc_system_stores")) k.ipc_system_stores = value != 0.0 ? 1 : 0;
   else if (!strcmp(name, "gate_stamps")) k.gate_stamps = value != 0.0 ? 1 : 0;
   else if (!strcmp(name, "ipc_pair_same_dir")) k.ipc_pair_same_dir = value != 0.0 ? 1 : 0;
+  else if (!strcmp(name, "gate_mode")) k.gate_mode = (int)value;
   else if (!strcmp(name, "cpu_ftz")) k.cpu_ftz = value != 0.0 ? 1 : 0;
   else if (!strcmp(name, "gated")) k.gated = value >= 2.0 ? 2 : (value != 0.0 ? 1 : 0);
   else return -1;

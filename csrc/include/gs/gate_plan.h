@@ -78,12 +78,11 @@ struct GateUnit {
   int32_t wait;    // 1: start-gated (waits for the peers, copies its cone's ghosts)
 };
 
-// The unit table (see above).  fill: a unit's pipeline fill + ramp in plane-times (the launch
-// model: 5n).  Sorted by (z0, tile), so each XCD group of workgroups (sched 3) gets a contiguous
-// range: neighbouring tiles at one depth.  allpk: every unit packs (else the start-gated ones).
-inline std::vector<GateUnit> gate_plan(const TileGrid& tg, const Geom& g, const HaloPlan& p,
-                                       int n, int xp, bool allpk, int slots, bool longest,
-                                       int* npk) {
+// Which ghost reads each tile column has: strip (an x / y ghost box at interior planes: gated
+// over its whole length), lo / hi (the z ghosts below / above, read by its end chunks)
+struct GateCol { bool strip, lo, hi; };
+inline std::vector<GateCol> gate_columns(const TileGrid& tg, const Geom& g, const HaloPlan& p,
+                                         int n) {
   const int nz = g.nz;
   auto dep = [&](int X0, int xw, int Y0, int ye, int z0, int z1) {
     for (int i = 0; i < p.nrecv; ++i) {
@@ -94,8 +93,7 @@ inline std::vector<GateUnit> gate_plan(const TileGrid& tg, const Geom& g, const 
     }
     return false;
   };
-  struct Col { bool strip, lo, hi; };
-  std::vector<Col> cols((size_t)tg.ntiles);
+  std::vector<GateCol> cols((size_t)tg.ntiles);
   for (int t = 0; t < tg.ntiles; ++t) {
     int X0, xw, Y0, ye;
     tile_window(tg, t, n, &X0, &xw, &Y0, &ye);
@@ -103,6 +101,17 @@ inline std::vector<GateUnit> gate_plan(const TileGrid& tg, const Geom& g, const 
     cols[t].lo = dep(X0, xw, Y0, ye, 0, 1);
     cols[t].hi = dep(X0, xw, Y0, ye, nz - 1, nz);
   }
+  return cols;
+}
+
+// The unit table (see above).  fill: a unit's pipeline fill + ramp in plane-times (the launch
+// model: 5n).  Sorted by (z0, tile), so each XCD group of workgroups (sched 3) gets a contiguous
+// range: neighbouring tiles at one depth.  allpk: every unit packs (else the start-gated ones).
+inline std::vector<GateUnit> gate_plan(const TileGrid& tg, const Geom& g, const HaloPlan& p,
+                                       int n, int xp, bool allpk, int slots, bool longest,
+                                       int* npk) {
+  const int nz = g.nz;
+  const std::vector<GateCol> cols = gate_columns(tg, g, p, n);
   const int F = 5 * n;
   auto build = [&](int tau, std::vector<GateUnit>* out) -> int {
     const int lg = std::max(1, tau - F - xp), li = std::max(1, tau - F);
@@ -118,7 +127,7 @@ inline std::vector<GateUnit> gate_plan(const TileGrid& tg, const Geom& g, const 
       }
     };
     for (int t = 0; t < tg.ntiles; ++t) {
-      const Col& c = cols[t];
+      const GateCol& c = cols[t];
       const int P = c.lo ? std::max(n, std::min(lg, nz)) : 0;
       const int S = c.hi ? std::max(n, std::min(lg, nz)) : 0;
       if (c.strip || P + S >= nz) {
@@ -142,6 +151,122 @@ inline std::vector<GateUnit> gate_plan(const TileGrid& tg, const Geom& g, const 
   int k = 0;
   for (auto& x : u)
     if (x.wait || allpk) x.pk = k++;
+  *npk = k;
+  return u;
+}
+
+// PAIRS variant: every workgroup runs up to two units in turn -- first an ungated chunk (entry
+// 2w), then a start-gated one (entry 2w + 1), whose wait for the peers' flags and cone unpack
+// happen between the two marches, so the first chunk covers the exchange instead of an idle
+// wait.  Entries with tile = -1 are empty.  Model, in plane-times: a unit costs its planes plus
+// fill = 3n - 1 (the skewed pipeline's fill and drain); a pair costs max(fill + a, X) + U + fill
+// + g for an ungated chunk of a planes and a gated chunk of g planes (X: the exchange, U: the
+// cone unpack, both expected values the device tunes); the table takes the smallest makespan M
+// that fits `slots` workgroups.  pk of entry 2w: the workgroup's packer index (-1: none): the
+// workgroups with a gated unit pack, or every one (allpk).
+inline std::vector<GateUnit> gate_plan_pairs(const TileGrid& tg, const Geom& g, const HaloPlan& p,
+                                             int n, int X, int U, bool allpk, int slots,
+                                             int* npk) {
+  const int nz = g.nz;
+  const std::vector<GateCol> cols = gate_columns(tg, g, p, n);
+  const int Fu = 3 * n - 1;
+  struct Piece { int t, z0, z1; };
+  // the gated chunks (at most lg planes) and the ungated ranges for a gated chunk length lg
+  auto split = [&](int lg, std::vector<Piece>* gated, std::vector<Piece>* free_) {
+    for (int t = 0; t < tg.ntiles; ++t) {
+      const GateCol& c = cols[t];
+      const int P = c.lo ? std::max(n, std::min(lg, nz)) : 0;
+      const int S = c.hi ? std::max(n, std::min(lg, nz)) : 0;
+      auto cut = [&](int a, int b) {
+        if (b <= a) return;
+        const int k = (b - a + lg - 1) / lg;
+        for (int i = 0; i < k; ++i)
+          gated->push_back(Piece{t, a + (int)((int64_t)(b - a) * i / k),
+                                 a + (int)((int64_t)(b - a) * (i + 1) / k)});
+      };
+      if (c.strip || P + S >= nz) {
+        cut(0, nz);
+      } else {
+        cut(0, P);
+        if (nz - S > P) free_->push_back(Piece{t, P, nz - S});
+        cut(nz - S, nz);
+      }
+    }
+  };
+  // the smallest makespan M (and its gated chunk length) whose pieces fit the slots
+  int bestM = -1, bestLg = nz;
+  for (int lg = std::max(1, n); lg <= nz; lg = lg < 8 ? lg + 1 : lg + lg / 8) {
+    std::vector<Piece> gated, free_;
+    split(lg, &gated, &free_);
+    if ((int)gated.size() > slots) continue;
+    int64_t wu = 0;
+    for (const Piece& f : free_) wu += f.z1 - f.z0;
+    // M: every gated chunk's pair ends by M; the ungated planes fit the pairs' first slots and
+    // the single workgroups
+    int lo = 1, hi = 4 * (nz + X + U + 2 * Fu) + 8;
+    auto fits = [&](int M) {
+      int64_t cap = 0;
+      for (const Piece& q : gated) {
+        const int tail = U + Fu + (q.z1 - q.z0);
+        if (std::max(X, 0) + tail > M) return false;  // not even without a first chunk
+        cap += std::max(0, M - tail - Fu);             // planes of a first chunk before it
+      }
+      cap += (int64_t)(slots - (int)gated.size()) * std::max(0, M - Fu);
+      return cap >= wu;
+    };
+    if (!fits(hi)) continue;
+    while (lo < hi) {
+      const int mid = (lo + hi) / 2;
+      if (fits(mid)) hi = mid; else lo = mid + 1;
+    }
+    if (bestM < 0 || lo < bestM) { bestM = lo; bestLg = lg; }
+  }
+  std::vector<GateUnit> u;
+  *npk = 0;
+  if (bestM < 0) return u;  // no pairs table fits
+  std::vector<Piece> gated, free_;
+  split(bestLg, &gated, &free_);
+  std::stable_sort(gated.begin(), gated.end(), [](const Piece& a, const Piece& b) {
+    return a.z0 != b.z0 ? a.z0 < b.z0 : a.t < b.t;
+  });
+  const GateUnit none{-1, 0, 0, -1, 0};
+  // cut the ungated ranges into the pairs' first chunks, then into single units; a chunk never
+  // crosses a column, so a range's short remainder can waste a pair's room: raise M until the
+  // workgroups fit
+  for (int M = bestM; M <= bestM + nz + 1; ++M) {
+    u.clear();
+    size_t fi = 0;
+    int fz = free_.empty() ? 0 : free_[0].z0;
+    auto take = [&](int len, Piece* out) -> bool {
+      while (fi < free_.size() && fz >= free_[fi].z1)
+        if (++fi < free_.size()) fz = free_[fi].z0;
+      if (fi >= free_.size() || len <= 0) return false;
+      const int z1 = std::min(free_[fi].z1, fz + len);
+      *out = Piece{free_[fi].t, fz, z1};
+      fz = z1;
+      return true;
+    };
+    for (const Piece& q : gated) {
+      Piece a{};
+      const bool first = take(M - (U + Fu + (q.z1 - q.z0)) - Fu, &a);
+      u.push_back(first ? GateUnit{a.t, a.z0, a.z1, -1, 0} : none);
+      u.push_back(GateUnit{q.t, q.z0, q.z1, -1, 1});
+    }
+    for (;;) {
+      Piece a{};
+      if (!take(M - Fu, &a)) break;
+      u.push_back(GateUnit{a.t, a.z0, a.z1, -1, 0});
+      u.push_back(none);
+    }
+    if ((int)(u.size() / 2) <= slots) break;
+  }
+  if ((int)(u.size() / 2) > slots) {
+    u.clear();
+    return u;
+  }
+  int k = 0;
+  for (size_t w = 0; w < u.size(); w += 2)
+    if (allpk || u[w + 1].wait) u[w].pk = k++;
   *npk = k;
   return u;
 }

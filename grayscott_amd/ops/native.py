@@ -211,10 +211,13 @@ def plan_sizes(g: Geom, nbr27, diagonals: bool):
 
 
 def gate_plan(g: Geom, nbr27, n: int, xp: int = 0, allpk: bool = False, slots: int = 256,
-              longest: bool = False, rows: int = 4, waves: int = 12, fold: bool = False):
+              longest: bool = False, rows: int = 4, waves: int = 12, fold: bool = False,
+              pairs: bool = False, unpack: int = 0):
     """The gated pass's unit table for a sub-domain (csrc/include/gs/gate_plan.h, host only):
     ``(units, npk, grid)`` -- units as (tile, z0, z1, pk, wait) tuples, the packer count and the
-    tile grid {xstep, ystep, ybase, ntx, nty, ntxf, nfold, ntiles, rt}."""
+    tile grid {xstep, ystep, ybase, ntx, nty, ntxf, nfold, ntiles, rt}.  pairs: the
+    two-units-per-workgroup table (entries 2w, 2w + 1; tile -1 = empty), xp the expected
+    exchange and ``unpack`` the cone unpack, in plane-times."""
     lib = load("core")
     lib.gs_gate_plan.restype = c_int
     arr = (c_int32 * 27)(*nbr27)
@@ -223,8 +226,8 @@ def gate_plan(g: Geom, nbr27, n: int, xp: int = 0, allpk: bool = False, slots: i
     cap = 1 << 16
     out = (c_int32 * (5 * cap))()
     k = lib.gs_gate_plan(ctypes.byref(g), arr, int(n), int(xp), 1 if allpk else 0, int(slots),
-                         1 if longest else 0, int(rows), int(waves), 1 if fold else 0, out, cap,
-                         ctypes.byref(npk), grid)
+                         1 if longest else 0, int(rows), int(waves), 1 if fold else 0,
+                         1 if pairs else 0, int(unpack), out, cap, ctypes.byref(npk), grid)
     if k < 0 or k > cap:
         raise ValueError(f"gs_gate_plan failed ({k})")
     units = [tuple(out[5 * i:5 * i + 5]) for i in range(k)]
@@ -330,16 +333,20 @@ class Engine:
         self._chk(self.lib.gs_set_gated(self.h, 1 if on else 0), "set_gated")
 
     def gate_info(self, k: int):
-        """{"xp", "units", "packers", "ms"} of the tuned gated pass of depth k (HIP only), or None."""
+        """{"xp", "units" (workgroups), "packers", "ms", "pairs_unpack"} of the tuned gated pass
+        of depth k (HIP only; pairs_unpack: the pairs table's U, None for a one-unit table), or
+        None."""
         if not hasattr(self.lib, "gs_gate_info"):
             return None
-        out = (c_double * 4)()
+        out = (c_double * 5)()
         self.lib.gs_gate_info.argtypes = [c_void_p, c_int32, c_int32, POINTER(c_double)]
         self.lib.gs_gate_info.restype = c_int
         if self.lib.gs_gate_info(self.h, int(k), DTYPE_CODES[self.dtype], out) != 0 or out[0] < 0:
             return None
-        return {"xp": int(out[0]), "units": int(out[1]), "packers": int(out[2]),
-                "ms": round(float(out[3]), 5)}
+        pairs = out[4] >= 0
+        return {"xp": int(out[0]), "units": int(out[1]) // (2 if pairs else 1),
+                "packers": int(out[2]), "ms": round(float(out[3]), 5),
+                "pairs_unpack": int(out[4]) if pairs else None}
 
     def set_auto_depth(self, on: bool):
         self._chk(self.lib.gs_set_auto_depth(self.h, 1 if on else 0), "set_auto_depth")

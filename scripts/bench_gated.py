@@ -12,7 +12,8 @@ N-GPU job owns.  Per k-step pass (ms), for the neighbour sets:
             timing only, the values are no wrap);
 and the pass kinds:
   full       -- the fused pass of a rank without neighbours (no exchange): the floor,
-  gated      -- the gated pass (the default for IPC, overlap on),
+  gated      -- the gated pass (the default for IPC, overlap on; --gate-modes: its one-unit /
+                pairs tables separately),
   stream     -- debug knob gated = 0: inner launch + shell with pack / flag / unpack kernels on
                 the comm stream (the round-4 overlapped pass),
   serial     -- overlap off: exchange, then the full pass.
@@ -40,6 +41,10 @@ def main():
     ap.add_argument("--nbrs", nargs="+", default=["z", "plus", "all"])
     ap.add_argument("--prec", default="Float32")
     ap.add_argument("--out", default="")
+    ap.add_argument("--gate-modes", type=int, nargs="+", default=[0],
+                    help="debug knob gate_mode per gated row: 0 tuned (one-unit and pairs tables), "
+                         "1 one-unit tables only, 2 pairs tables only")
+    ap.add_argument("--gated-only", action="store_true", help="skip the stream / serial rows")
     ap.add_argument("--stamps", action="store_true",
                     help="debug knob gate_stamps: the exchange's wall-clock stamps (after the "
                          "timed passes; the stamp resets add a copy per pass, so time without)")
@@ -88,9 +93,13 @@ def main():
                 for em in a.emulate_us:
                     row = {"n": n, "k": k, "nbrs": which, "emulate_us": em,
                            "full_ms": round(full, 4)}
-                    for kind, ov, gated in (("gated", "on", 1), ("stream", "on", 0),
-                                            ("serial", "off", 1)):
+                    kinds = [(f"gated{m}" if len(a.gate_modes) > 1 else "gated", "on", 1, m)
+                             for m in a.gate_modes]
+                    if not a.gated_only:
+                        kinds += [("stream", "on", 0, 0), ("serial", "off", 1, 0)]
+                    for kind, ov, gated, mode in kinds:
                         native.debug_set("gated", gated)
+                        native.debug_set("gate_mode", mode)
                         native.debug_set("ipc_emulate_us", em)
                         native.debug_set("gate_stamps", 1 if a.stamps else 0)
                         native.debug_set("ipc_pair_same_dir", 1 if which == "plus" else 0)
@@ -101,16 +110,17 @@ def main():
                                 ms = timed(sim, k)
                                 row[kind + "_ms"] = round(ms, 4)
                                 row[kind + "_x"] = round(ms / full, 4)
-                                if kind == "gated":
-                                    row["gated_ran"] = sim.gated
-                                    row["gate"] = sim.engine.gate_info(k)
-                                    row["stamps_us"] = sim.engine.gate_stamps()
+                                if kind.startswith("gated"):
+                                    row[kind + "_ran"] = sim.gated
+                                    row[kind + "_table"] = sim.engine.gate_info(k)
+                                    row[kind + "_stamps_us"] = sim.engine.gate_stamps()
                             finally:
                                 sim.close()
                         finally:
                             native.debug_set("gated", 1)
                             native.debug_set("ipc_emulate_us", 0)
                             native.debug_set("gate_stamps", 0)
+                            native.debug_set("gate_mode", 0)
                             native.debug_set("ipc_pair_same_dir", 0)
                     rows.append(row)
                     print(json.dumps(row), flush=True)

@@ -110,3 +110,46 @@ def test_gate_plan_tile_grid_matches_the_kernel():
     assert (grid["ntxf"], grid["nfold"], grid["ntiles"]) == (4, 4, 32)
     _, _, grid = native.gate_plan(g, _nbr(Z_ONLY), 3, fold=False)
     assert grid["ntiles"] == 35
+
+
+@pytest.mark.parametrize("shape,dirs,n,fold,X,U,allpk,slots", [
+    ((256, 256, 256), ONE_SIDED, 3, True, 16, 6, False, 256),
+    ((256, 256, 256), ONE_SIDED, 3, True, 32, 6, True, 256),
+    ((256, 256, 256), ALL26, 3, True, 24, 8, False, 256),
+    ((96, 80, 72), ALL26, 2, False, 8, 4, False, 128),
+    ((512, 512, 64), Z_ONLY, 3, False, 40, 6, False, 256),
+    ((64, 64, 64), Z_ONLY, 3, False, 0, 0, True, 256),
+])
+def test_gate_plan_pairs(shape, dirs, n, fold, X, U, allpk, slots):
+    """The two-units-per-workgroup table: entry 2w is an ungated chunk (or empty), 2w + 1 a
+    start-gated chunk (or empty); together the chunks partition every column; only the second
+    entries read ghosts (checked against the independent cones); at most `slots` workgroups."""
+    nx, ny, nz = shape
+    g = native.make_geom(nx, ny, nz, H, 0, 0, 0, nx * 2, ny * 2, nz * 2, False)
+    units, npk, grid = native.gate_plan(g, _nbr(dirs), n, xp=X, allpk=allpk, slots=slots,
+                                        fold=fold, pairs=True, unpack=U)
+    assert units and len(units) % 2 == 0 and len(units) // 2 <= slots
+    ghosts = _ghost_regions(nx, ny, nz, dirs)
+    by_tile = {}
+    for i, (t, z0, z1, pk, wait) in enumerate(units):
+        if t < 0:
+            continue
+        assert 0 <= z0 < z1 <= nz
+        by_tile.setdefault(t, []).append((z0, z1))
+        xr, yr = _window(grid, t, n)
+        need = any(_meets(xr, gx) and _meets(yr, gy) and _meets((z0 - n, z1 + n), gz)
+                   for gx, gy, gz in ghosts)
+        assert bool(wait) == need, (i, t, z0, z1, wait, need)
+        assert bool(wait) == (i % 2 == 1)  # gated units are second, ungated first
+    assert sorted(by_tile) == list(range(grid["ntiles"]))
+    for t, iv in by_tile.items():
+        iv.sort()
+        assert iv[0][0] == 0 and iv[-1][1] == nz
+        assert all(a[1] == b[0] for a, b in zip(iv, iv[1:])), (t, iv)
+    pks = [units[w][3] for w in range(0, len(units), 2) if units[w][3] >= 0]
+    assert sorted(pks) == list(range(npk))
+    for w in range(0, len(units), 2):
+        if units[w + 1][4]:
+            assert units[w][3] >= 0  # a workgroup with a gated unit packs
+        if allpk:
+            assert units[w][3] >= 0

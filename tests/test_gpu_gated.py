@@ -42,9 +42,12 @@ def _single(L, steps, fuse, prec="Float32", random_init=None):
     return run_ranks(1, cfg)
 
 
-@pytest.mark.parametrize("which,L,fuse,prec", [("z", 48, 3, "Float32"), ("yz", 40, 3, "Float32"),
-                                                ("yz", 36, 2, "Float64")])
-def test_gated_loopback(which, L, fuse, prec):
+@pytest.mark.parametrize("which,L,fuse,prec,mode", [("z", 48, 3, "Float32", 0),
+                                                     ("yz", 40, 3, "Float32", 0),
+                                                     ("yz", 36, 2, "Float64", 0),
+                                                     ("z", 48, 3, "Float32", 2),
+                                                     ("yz", 40, 3, "Float32", 2)])
+def test_gated_loopback(which, L, fuse, prec, mode, debug_knob):
     """One process, its halos sent to ITSELF through the landing buffer on a non-periodic
     geometry (wraps as messages): z neighbours only, or the 8 directions with dx = 0 (faces,
     edges) -- the same values as the same rank with device self copies.  (x wraps on a
@@ -66,6 +69,7 @@ def test_gated_loopback(which, L, fuse, prec):
     s = Settings(L=L, precision=prec, F=0.02, k=0.048, dt=1.0, Du=0.2, Dv=0.1, noise=0.1,
                  backend="AMDGPU", seed=99, overlap="on")
     out = []
+    debug_knob("gate_mode", mode)  # 2: pairs tables only
     # the reference: the same wraps as device self copies (no loopback)
     for kw in ({}, dict(transport="ipc", loopback=True)):
         sim = GrayScott(s, loop, fuse=fuse, **kw)
@@ -84,24 +88,29 @@ def test_gated_loopback(which, L, fuse, prec):
     np.testing.assert_array_equal(v1, v0)
 
 
-@pytest.mark.parametrize("world,dims,L,fuse,prec", [
-    (2, [1, 1, 2], 48, 3, "Float32"),   # z slabs: whole-plane messages
-    (2, [2, 1, 1], 64, 3, "Float32"),   # x split: strip tiles start-gated over the whole column
-    (4, [2, 2, 1], 64, 2, "Float64"),
-    (8, [2, 2, 2], 64, 3, "Float32"),   # every face, edge and corner message
-    (3, [1, 1, 3], 40, 2, "Float32"),   # a middle rank with two receive peers
+@pytest.mark.parametrize("world,dims,L,fuse,prec,mode", [
+    (2, [1, 1, 2], 48, 3, "Float32", 1),   # z slabs: whole-plane messages
+    (2, [2, 1, 1], 64, 3, "Float32", 1),   # x split: strip tiles start-gated over the whole column
+    (4, [2, 2, 1], 64, 2, "Float64", 1),
+    (8, [2, 2, 2], 64, 3, "Float32", 1),   # every face, edge and corner message
+    (3, [1, 1, 3], 40, 2, "Float32", 1),   # a middle rank with two receive peers
+    # pairs tables (an ungated chunk, then the start-gated one, per workgroup)
+    (2, [1, 1, 2], 48, 3, "Float32", 2),
+    (4, [2, 2, 1], 64, 2, "Float64", 2),
+    (8, [2, 2, 2], 64, 3, "Float32", 2),
 ])
-def test_gated_matches_single_rank(world, dims, L, fuse, prec):
+def test_gated_matches_single_rank(world, dims, L, fuse, prec, mode):
     steps = 4 * fuse + 1  # full gated passes and a trailing partial pass (stream exchange)
     u1, v1, _ = _single(L, steps, fuse, prec, random_init=11)
-    cfg = _cfg(L, steps, fuse, prec, overlap="on")
+    cfg = _cfg(L, steps, fuse, prec, knobs={"gate_mode": mode}, overlap="on")
     cfg["dims"] = dims
     cfg["random_init"] = 11
     un, vn, meta = run_ranks(world, cfg)
     assert all(m["transport"] == "ipc" and m["gated"] for m in meta), meta
-    for m in meta:  # the tuned table: every unit a workgroup, some of them packers
+    for m in meta:  # the tuned table: its workgroups, some of them packers
         g = m["gate"]
         assert g is not None and g["units"] > 0 and 0 < g["packers"] <= g["units"], g
+        assert (g["pairs_unpack"] is not None) == (mode == 2), g
     assert np.isfinite(un).all()
     np.testing.assert_array_equal(un, u1)
     np.testing.assert_array_equal(vn, v1)
