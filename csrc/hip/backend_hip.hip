@@ -30,8 +30,8 @@ extern template bool launch_fused<double>(const Vec2<double>::type*, Vec2<double
                                           const Geom&, const gs::Params&, int, int64_t,
                                           hipStream_t, int, int, int, int, int, int, int, int, bool,
                                           const GateLaunch*);
-extern template int fused_gated_occupancy<float>(int, int);
-extern template int fused_gated_occupancy<double>(int, int);
+extern template int fused_gated_occupancy<float>(int, int, bool);
+extern template int fused_gated_occupancy<double>(int, int, bool);
 extern template bool launch_shell<float>(const void*, void*, const Geom&, const gs::Params&, int,
                                          int64_t, int, int, hipStream_t);
 extern template bool launch_shell<double>(const void*, void*, const Geom&, const gs::Params&, int,
@@ -891,7 +891,7 @@ class HipBackend final : public gs::Backend {
     // every unit resident at once (the device's occupancy of the gated entry): a start-gated
     // unit that waits for the peers holds its slot, so a packer left unscheduled behind waiting
     // units would stall every rank until the wall-clock bound
-    const int per_cu = gsk::fused_gated_occupancy<T>(cfg, n);
+    const int per_cu = gsk::fused_gated_occupancy<T>(cfg, n, U >= 0);
     if (per_cu < 1) throw std::runtime_error("gated pass: no gated entry for this shape");
     // (peer processes on this GPU, debug knob gated = 2: this rank's share of the slots)
     const int slots = std::max(8, num_cus() * per_cu / (gate_sharers_ + 1));

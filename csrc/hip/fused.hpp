@@ -94,7 +94,7 @@ template <typename T>
 __device__ __forceinline__ void gate_pack(const FusedArgs& a, int pk);
 template <typename T, int BATCH>
 __device__ __forceinline__ void gate_unpack(const FusedArgs& a, int X0, int xw, int Y0, int yext,
-                                         int za, int zb);
+                                         int za, int zb, uint64_t t0);
 
 template <typename T> struct PairT;
 template <> struct PairT<float> { typedef float type __attribute__((ext_vector_type(2))); };
@@ -781,7 +781,7 @@ __device__ __forceinline__ void gate_cone(const FusedArgs& a, int tile, int* X0,
 
 // The kernel body; GATED: the gated pass's entry (k_fused_gated, sched 3), whose prologue
 // carries the halo exchange (gate.hpp).  The plain entry compiles without any of it.
-template <class C, typename T, bool GATED>
+template <class C, typename T, int GATED>
 __device__ __forceinline__ void fused_body(const typename C::V2* __restrict__ s,
                                            typename C::V2* __restrict__ d, const FusedArgs& a,
                                            const FoldCoef<T>& f, uint64_t seed) {
@@ -830,6 +830,7 @@ __device__ __forceinline__ void fused_body(const typename C::V2* __restrict__ s,
   const int b = blockIdx.x;
   const int nunits = a.ntiles * a.nchunk;
   int lu0 = 0, lu1 = 1, lstep = 1;
+  uint64_t t_gate = 0;  // (pairs tables: the workgroup's start, for the exchange's time bounds)
   if (a.sched == 1) {
     lu0 = (b % 8) * a.grpM + b / 8;
     lu1 = lu0 + 1;
@@ -845,11 +846,12 @@ __device__ __forceinline__ void fused_body(const typename C::V2* __restrict__ s,
     // start-gated one), each XCD group a contiguous range (the host orders the table by z, then
     // tile)
     const int w = (b % 8) * a.grpM + b / 8;
-    if (a.gate_pairs) {
+    if constexpr (GATED == 2) {
       if (2 * w >= a.ngunits) return;
       lu0 = 2 * w;
       lu1 = lu0 + 2;
       const GateUnit e0 = a.gunits[lu0];
+      t_gate = wall_clock64();  // the exchange's start for this workgroup (emulation, timeout)
       if (e0.pk >= 0) gate_pack<T>(a, e0.pk);  // the wait comes before the second entry
     } else {
       lu0 = w;
@@ -918,12 +920,14 @@ __device__ __forceinline__ void fused_body(const typename C::V2* __restrict__ s,
     } else if (GATED) {
       const GateUnit un = a.gunits[lu];
       if (un.tile < 0) continue;  // an empty entry of a pairs table (uniform per workgroup)
-      if (a.gate_pairs && un.wait) {
-        // the second entry of a pair: the peers' flags and the cone's ghosts, after the first
-        // entry's march (which covered the exchange)
-        int X0, xw, Y0, yext;
-        gate_cone<C>(a, un.tile, &X0, &xw, &Y0, &yext);
-        gate_unpack<T, 4>(a, X0, xw, Y0, yext, un.z0 - TL, un.z1 + TL);
+      if constexpr (GATED == 2) {
+        if (un.wait) {
+          // the second entry of a pair: the peers' flags and the cone's ghosts, after the first
+          // entry's march (which covered the exchange)
+          int X0, xw, Y0, yext;
+          gate_cone<C>(a, un.tile, &X0, &xw, &Y0, &yext);
+          gate_unpack<T, 4>(a, X0, xw, Y0, yext, un.z0 - TL, un.z1 + TL, t_gate);
+        }
       }
       u = (int64_t)un.tile * nzv + (un.z0 - a.zlo[0]);
       uend = (int64_t)un.tile * nzv + (un.z1 - a.zlo[0]);
@@ -1033,15 +1037,17 @@ __global__ __launch_bounds__(64 * C::WAVES, C::WPEU) void k_fused(const typename
                                                             typename C::V2* __restrict__ d,
                                                             FusedArgs a, FoldCoef<T> f,
                                                             uint64_t seed) {
-  fused_body<C, T, false>(s, d, a, f, seed);
+  fused_body<C, T, 0>(s, d, a, f, seed);
 }
 
-// the gated pass's entry (gate.hpp): instantiated for the shapes FCfg::GATE_OK names only
-template <class C, typename T>
+// the gated pass's entry (gate.hpp): instantiated for the shapes FCfg::GATE_OK names only;
+// PAIRS: the two-entries-per-workgroup tables (its own code object: the unpack between two
+// marches raises the register pressure the one-unit entry does not pay)
+template <class C, typename T, bool PAIRS>
 __global__ __launch_bounds__(64 * C::WAVES, C::WPEU) void k_fused_gated(
     const typename C::V2* __restrict__ s, typename C::V2* __restrict__ d, FusedArgs a,
     FoldCoef<T> f, uint64_t seed) {
-  fused_body<C, T, true>(s, d, a, f, seed);
+  fused_body<C, T, PAIRS ? 2 : 1>(s, d, a, f, seed);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1074,13 +1080,17 @@ struct FusedLaunch {
     return occ;
   }
   // resident workgroups per CU of the gated entry (the host sizes a gated table to these slots)
-  static int gated_occupancy() {
-    int o = 0;
-    if constexpr (C::GATE_OK)
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k_fused_gated<C, T>, 64 * C::WAVES, 0) !=
-          hipSuccess)
+  static int gated_occupancy(bool pairs) {
+    int o = 0, o2 = 0;
+    if constexpr (C::GATE_OK) {
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k_fused_gated<C, T, false>,
+                                                       64 * C::WAVES, 0) != hipSuccess)
         o = 0;
-    return o;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o2, k_fused_gated<C, T, true>,
+                                                       64 * C::WAVES, 0) != hipSuccess)
+        o2 = 0;
+    }
+    return pairs ? o2 : o;
   }
   static void run(const void* s, void* d, const FusedArgs& a0, const gs::Params& p,
                   hipStream_t st) {
@@ -1107,8 +1117,12 @@ struct FusedLaunch {
         a.nchunk = 1;
         a.grpM = ((a.gate_pairs ? a.ngunits / 2 : a.ngunits) + 7) / 8;
         const FoldCoef<T> f = make_fold<T>(p);
-        k_fused_gated<C, T><<<(unsigned)(8 * a.grpM), 64 * C::WAVES, 0, st>>>(
-            (const typename C::V2*)s, (typename C::V2*)d, a, f, p.seed);
+        if (a.gate_pairs)
+          k_fused_gated<C, T, true><<<(unsigned)(8 * a.grpM), 64 * C::WAVES, 0, st>>>(
+              (const typename C::V2*)s, (typename C::V2*)d, a, f, p.seed);
+        else
+          k_fused_gated<C, T, false><<<(unsigned)(8 * a.grpM), 64 * C::WAVES, 0, st>>>(
+              (const typename C::V2*)s, (typename C::V2*)d, a, f, p.seed);
       }
       return;  // (gated_shape_cfg never names a shape without the gated entry)
     }
@@ -1415,15 +1429,15 @@ void run_fused_tl(const void* s, void* d, const FusedArgs& a, const gs::Params& 
 
 // resident workgroups per CU of the gated entry that gated_shape_cfg names for depth n (0: none)
 template <typename T>
-int fused_gated_occupancy(int cfg, int n) {
+int fused_gated_occupancy(int cfg, int n, bool pairs) {
   auto one = [&](auto tl) -> int {
     constexpr int TL = decltype(tl)::value;
     if constexpr (sizeof(T) == 8) {
-      return FusedLaunch<FCfg<T, TL, 4, 8, 1, false, true, true, true>, T>::gated_occupancy();
+      return FusedLaunch<FCfg<T, TL, 4, 8, 1, false, true, true, true>, T>::gated_occupancy(pairs);
     } else {
       if (cfg == fused_cfg_lookup("4x12:1sf"))
-        return FusedLaunch<FCfg<T, TL, 4, 12, 1, false, true, true, true, 0, true>, T>::gated_occupancy();
-      return FusedLaunch<FCfg<T, TL, 4, 12, 1, false, true, true>, T>::gated_occupancy();
+        return FusedLaunch<FCfg<T, TL, 4, 12, 1, false, true, true, true, 0, true>, T>::gated_occupancy(pairs);
+      return FusedLaunch<FCfg<T, TL, 4, 12, 1, false, true, true>, T>::gated_occupancy(pairs);
     }
   };
   if (n == 2) return one(std::integral_constant<int, 2>{});

@@ -185,14 +185,13 @@ __device__ __forceinline__ void gate_pack(const FusedArgs& a, int pk) {
 // [X0, X0 + xw) x [Y0, Y0 + yext) x [za, zb) out of the landing slot
 template <typename T, int BATCH = gate_batch<T>()>
 __device__ __forceinline__ void gate_unpack(const FusedArgs& a, int X0, int xw, int Y0, int yext,
-                                         int za, int zb) {
+                                         int za, int zb, uint64_t t0) {
   using V2 = typename Vec2<T>::type;
   constexpr int B = BATCH;  // (a pairs table's second entry unpacks with the march state live)
   const GateArgs& G = *a.gate;
   const Geom& g = a.g;
   const int slot = (int)(a.gate_n & 1);
   const uint32_t nt = blockDim.x, tid = threadIdx.x;
-  const uint64_t t0 = wall_clock64();
   V2* f = (V2*)a.field;
   __shared__ GatePiece gp[gs::kMaxMsgs];
   __shared__ uint32_t gcells[gs::kMaxMsgs];
@@ -311,6 +310,7 @@ __device__ __forceinline__ void gate_unpack(const FusedArgs& a, int X0, int xw, 
 template <typename T>
 __device__ __forceinline__ void gate_start(const FusedArgs& a, int pk, bool wait, int X0, int xw,
                                         int Y0, int yext, int za, int zb) {
+  const uint64_t t0 = wall_clock64();  // the exchange's start (timeout, emulated duration)
   if (pk >= 0) gate_pack<T>(a, pk);
-  if (wait) gate_unpack<T, gate_batch<T>()>(a, X0, xw, Y0, yext, za, zb);
+  if (wait) gate_unpack<T, gate_batch<T>()>(a, X0, xw, Y0, yext, za, zb, t0);
 }

@@ -8,5 +8,5 @@ template bool launch_fused<double>(const typename Vec2<double>::type*, typename 
                                const Geom&, const gs::Params&, int, int64_t, hipStream_t, int,
                                int, int, int, int, int, int, int, bool,
                                const GateLaunch*);
-template int fused_gated_occupancy<double>(int, int);
+template int fused_gated_occupancy<double>(int, int, bool);
 }  // namespace gsk

@@ -8,5 +8,5 @@ template bool launch_fused<float>(const typename Vec2<float>::type*, typename Ve
                                const Geom&, const gs::Params&, int, int64_t, hipStream_t, int,
                                int, int, int, int, int, int, int, bool,
                                const GateLaunch*);
-template int fused_gated_occupancy<float>(int, int);
+template int fused_gated_occupancy<float>(int, int, bool);
 }  // namespace gsk

@@ -2,7 +2,7 @@
 # -- correctness, then the cost per table kind.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/${GS_OUT:-r5c29}
+O=$R/gpurun_out/${GS_OUT:-r5c30}
 mkdir -p $O
 cd $R
 export TMPDIR=/tmp
