@@ -94,6 +94,7 @@ def test_gated_loopback(which, L, fuse, prec, mode, debug_knob):
     (4, [2, 2, 1], 64, 2, "Float64", 1),
     (8, [2, 2, 2], 64, 3, "Float32", 1),   # every face, edge and corner message
     (3, [1, 1, 3], 40, 2, "Float32", 1),   # a middle rank with two receive peers
+    (4, [2, 2, 1], 48, 3, "Float64", 1),   # fp64 at depth 3 (the 243-VGPR gated entry)
     # pairs tables (an ungated chunk, then the start-gated one, per workgroup)
     (2, [1, 1, 2], 48, 3, "Float32", 2),
     (4, [2, 2, 1], 64, 2, "Float64", 2),
