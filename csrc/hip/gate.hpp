@@ -11,17 +11,23 @@
 //   * the host splits each tile column into z-chunks, one unit per workgroup (GateUnit);
 //     a unit whose level-0 cone reads a ghost cell that a neighbour fills is START-GATED, every
 //     other unit marches at once;
-//   * start-gated units are the packers: each copies its share of every outgoing message
-//     straight into the receiving peer's landing buffer (IPC-mapped; system-coherent stores
-//     across devices), waits for its stores to be acknowledged and bumps a device counter; the
-//     packer whose add completes the pass's count publishes this exchange's sequence number in
-//     every send peer's flag array;
+//   * start-gated units (or, as tuned, every unit) are the packers: each copies its share of
+//     every outgoing message straight into the receiving peer's landing buffer (IPC-mapped;
+//     system-coherent stores across devices), waits for its stores to be acknowledged and bumps
+//     a device counter; the packer whose add completes the pass's count publishes this
+//     exchange's sequence number in every send peer's flag array (gate_pack);
 //   * then each start-gated unit polls its own flags until every receive peer has published
 //     (a wall-clock bound turns a dead peer into an error, not a hang), copies the ghost cells
 //     of its own cone out of its landing slot (cones of neighbouring tiles overlap: a few cells
-//     are copied twice, with equal values) and marches;
+//     are copied twice, with equal values), drops its L1 and marches (gate_unpack);
 //   * the host sizes the chunks so that every workgroup finishes together: gated chunks are
-//     shorter by the expected exchange time (tuned on the device, backend_hip.hip gate_tune).
+//     shorter by the expected exchange time (tuned on the device, backend_hip.hip gate_tune;
+//     the planner is gs/gate_plan.h).  Pairs tables give a workgroup an ungated chunk first and
+//     run the wait and unpack between its two marches (k_fused_gated<..., PAIRS>).
+// No fence wider than the workgroup runs inside the launch (gfx950: a system release is
+// buffer_wbl2, an agent acquire buffer_inv sc1 -- the XCD's whole L2 under the marching
+// workgroups): the landing slots and flags are uncached, so nothing the protocol reads can be
+// stale in a cache, and every store is acknowledged (s_waitcnt) before the arrival it precedes.
 // The same monotonic flags and two landing slots as the stream transport (backend_hip.hip
 // ipc_*): exchange n uses slot n & 1; a rank starts packing n only after its previous launch,
 // whose gated units waited for every peer's n - 1, so the peers have consumed slot n & 1 (their
