@@ -566,9 +566,11 @@ class HipBackend final : public gs::Backend {
     landing_cells_ = std::max<int64_t>(p.recv_cells, 1);
     HIP_CHECK(hipExtMallocWithFlags((void**)&landing_, 2 * landing_cells_ * sizeof(V2),
                                     hipDeviceMallocUncached));
-    HIP_CHECK(hipExtMallocWithFlags((void**)&flags_, (size_t)nranks * sizeof(uint64_t),
+    // flags_[0, nranks): sequence flags; [nranks, 2 nranks): publication stamps (gate.hpp:
+    // emulated carried exchanges)
+    HIP_CHECK(hipExtMallocWithFlags((void**)&flags_, 2 * (size_t)nranks * sizeof(uint64_t),
                                     hipDeviceMallocUncached));
-    HIP_CHECK(hipMemset(flags_, 0, (size_t)nranks * sizeof(uint64_t)));
+    HIP_CHECK(hipMemset(flags_, 0, 2 * (size_t)nranks * sizeof(uint64_t)));
     HIP_CHECK(hipMalloc((void**)&ipc_dflag_, sizeof(int)));
     HIP_CHECK(hipMemset(ipc_dflag_, 0, sizeof(int)));
     HIP_CHECK(hipDeviceSynchronize());
@@ -833,10 +835,10 @@ class HipBackend final : public gs::Backend {
       if (u) { (void)hipFree(u); u = nullptr; }
     d_gate_ = nullptr;
     d_counter_ = nullptr;
-    cnt_host_ = 0;
+    cnt_host_[0] = cnt_host_[1] = 0;
     for (int i = 0; i < 4; ++i) {
-      gate_tuned_[i] = pairs_[i] = false;
-      nunits_[i] = npk_[i] = 0;
+      gate_tuned_[i] = pairs_[i] = carry_[i] = false;
+      nunits_[i] = npk_[i] = nprod_[i] = nwu_[i] = 0;
       gate_xp_[i] = gate_u_[i] = -1;
     }
   }
@@ -858,11 +860,17 @@ class HipBackend final : public gs::Backend {
       G.rbox[i] = p.recv[i].box;
       for (int sl = 0; sl < 2; ++sl) G.rsrc[sl][i] = landing_ + sl * landing_cells_ + p.recv[i].offset;
     }
-    for (int idx : recv_peers_) G.wflag[G.nwait++] = flags_ + peers_[idx].rank;
-    for (int idx : send_peers_) G.sflag[G.nsig++] = peers_[idx].flags + rank_;
-    HIP_CHECK(hipMalloc((void**)&d_counter_, sizeof(uint32_t)));
-    HIP_CHECK(hipMemset(d_counter_, 0, sizeof(uint32_t)));
-    cnt_host_ = 0;
+    for (int idx : recv_peers_) {
+      G.wstamp[G.nwait] = flags_ + ipc_nranks_ + peers_[idx].rank;
+      G.wflag[G.nwait++] = flags_ + peers_[idx].rank;
+    }
+    for (int idx : send_peers_) {
+      G.sstamp[G.nsig] = peers_[idx].flags + ipc_nranks_ + rank_;
+      G.sflag[G.nsig++] = peers_[idx].flags + rank_;
+    }
+    HIP_CHECK(hipMalloc((void**)&d_counter_, 2 * sizeof(uint32_t)));
+    HIP_CHECK(hipMemset(d_counter_, 0, 2 * sizeof(uint32_t)));
+    cnt_host_[0] = cnt_host_[1] = 0;
     G.counter = d_counter_;
     G.ticks = ipc_ticks_;
     G.min_ticks = ipc_emulate_ticks_;
@@ -912,17 +920,31 @@ class HipBackend final : public gs::Backend {
     HIP_CHECK(hipMemcpy(d_units_[n], u.data(), bytes, hipMemcpyHostToDevice));
     nunits_[n] = (int)u.size();
     npk_[n] = npk;
+    nprod_[n] = nwu_[n] = 0;
+    for (const gsk::GateUnit& x : u) {
+      nprod_[n] += x.prod != 0;
+      nwu_[n] += x.wait != 0;
+    }
   }
 
-  // one gated pass src -> dst on the compute stream (exchange number ++xn_)
-  void gate_launch(int src, int dst, int n, int64_t t) {
+  // one gated pass src -> dst on the compute stream (exchange number ++xn_).  pre bit 0: its
+  // exchange was carried by the previous launch (packed by its producers); bit 1: this launch's
+  // producers carry the next one (gate.hpp gate_carry)
+  void gate_launch(int src, int dst, int n, int64_t t, int pre = 0) {
     gsk::GateLaunch gl{};
     gl.units = d_units_[n];
     gl.nunits = nunits_[n];
     gl.gate = d_gate_;
     gl.n = ++xn_;
-    cnt_host_ += (uint32_t)npk_[n];
-    gl.cnt = cnt_host_;
+    if (!(pre & 1)) cnt_host_[gl.n & 1] += (uint32_t)npk_[n];
+    gl.cnt = cnt_host_[gl.n & 1];
+    if (pre & 2) {
+      // arrivals of exchange n + 1: every producer after its carry, every start-gated unit
+      // after its unpack (the peers' slot reuse waits for both)
+      cnt_host_[(gl.n + 1) & 1] += (uint32_t)(nprod_[n] + nwu_[n]);
+      gl.cnt2 = cnt_host_[(gl.n + 1) & 1];
+    }
+    gl.pre = pre;
     gl.npk = npk_[n];
     gl.pairs = pairs_[n] ? 1 : 0;
     if (d_stamps_) {  // debug knob gate_stamps: this launch's stamps only
@@ -943,17 +965,22 @@ class HipBackend final : public gs::Backend {
   void gate_tune(int src, int dst, int n, int64_t t) {
     if (!tuned_[n]) autotune(src, dst, n, t);
     gate_setup();
-    // candidates: one-unit tables (expected exchange xp, packers) and pairs tables (an ungated
-    // chunk before each start-gated one: exchange X, unpack U); every rank times the same list
-    struct Cand { int xp, U; bool all; };
+    // candidates: one-unit tables (expected exchange xp, packers), pairs tables (an ungated
+    // chunk before each start-gated one: exchange X, unpack U) and carried one-unit tables (the
+    // previous pass's producers pack: xp then covers the cone unpack and the carry); every rank
+    // times the same list
+    struct Cand { int xp, U; bool all, carry; };
     std::vector<Cand> cands;
-    const int mode = gs::debug_knobs().gate_mode;  // 1: one-unit only, 2: pairs only (tests)
+    // debug knob gate_mode (tests, A/B): 1 one-unit only, 2 pairs only, 3 carried only
+    const int mode = gs::debug_knobs().gate_mode;
+    if (mode == 0 || mode == 3)
+      for (int xp : {0, 2, 4, 6, 8, 12, 16, 24}) cands.push_back({xp, -1, false, true});
     for (int all = 0; all < 2; ++all) {
-      if (mode != 2)
-        for (int xp : {0, 4, 8, 16, 24, 32}) cands.push_back({xp, -1, all != 0});
-      if (mode != 1)
+      if (mode == 0 || mode == 1)
+        for (int xp : {0, 4, 8, 16, 24, 32}) cands.push_back({xp, -1, all != 0, false});
+      if (mode == 0 || mode == 2)
         for (int X : {8, 16, 24, 32})
-          for (int U : {4, 8}) cands.push_back({X, U, all != 0});
+          for (int U : {4, 8}) cands.push_back({X, U, all != 0, false});
     }
     float best = 1e30f;
     Cand bc = cands[0];
@@ -968,14 +995,23 @@ class HipBackend final : public gs::Backend {
       // table), so every rank takes part in the same number of exchanges
       if (u.empty()) u = gate_table(n, 0, c.all, &npk);
       gate_upload(n, u, npk, pairs);
-      gate_launch(src, dst, n, t);  // warm-up
+      // carried: a run of passes -- the first packs at its start, the timed ones find their
+      // exchange carried, the last carries none.  A producer must be start-gated (it has then
+      // seen the peers publish, i.e. finish with the slot it fills: gate.hpp gate_carry) --
+      // true for the symmetric neighbour sets of a Cartesian grid; a table where it is not
+      // runs the same launches uncarried and is not kept
+      bool carry_ok = c.carry && !pairs;
+      for (const gsk::GateUnit& x : u) carry_ok = carry_ok && (!x.prod || x.wait);
+      const int pin = carry_ok ? 1 : 0, pout = carry_ok ? 2 : 0;
+      gate_launch(src, dst, n, t, pout);  // warm-up
       HIP_CHECK(hipEventRecord(e0, stream_));
-      for (int r = 0; r < 3; ++r) gate_launch(src, dst, n, t);
+      for (int r = 0; r < 3; ++r) gate_launch(src, dst, n, t, pin | pout);
       HIP_CHECK(hipEventRecord(e1, stream_));
+      if (c.carry) gate_launch(src, dst, n, t, pin);
       wait_all(gs::comm_timeout_s());
       float ms = 0.f;
       HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
-      if (ms < best && (c.U < 0 || pairs)) { best = ms; bc = c; }
+      if (ms < best && (c.U < 0 || pairs) && (!c.carry || carry_ok)) { best = ms; bc = c; }
     }
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
@@ -985,6 +1021,9 @@ class HipBackend final : public gs::Backend {
     gate_xp_[n] = bc.xp;
     gate_u_[n] = bc.U;
     gate_allpk_[n] = bc.all;
+    bool carry = bc.carry && bc.U < 0;
+    for (const gsk::GateUnit& x : u) carry = carry && (!x.prod || x.wait);
+    carry_[n] = carry;
     gate_ms_[n] = best / 3.f;
     gate_tuned_[n] = true;
   }
@@ -993,10 +1032,13 @@ class HipBackend final : public gs::Backend {
     if (gated_supported(n) && !gate_tuned_[n]) gate_tune(src, dst, n, t);
   }
 
-  bool fused_gated(int src, int dst, int n, int64_t t) override {
+  // first / last: the pass opens / closes the engine's run of gated passes (a carried exchange
+  // never crosses a run: between runs the fields may change)
+  bool fused_gated(int src, int dst, int n, int64_t t, bool first, bool last) override {
     if (!gated_supported(n)) return false;
     if (!gate_tuned_[n]) gate_tune(src, dst, n, t);
-    gate_launch(src, dst, n, t);
+    const int pre = carry_[n] ? ((first ? 0 : 1) | (last ? 0 : 2)) : 0;
+    gate_launch(src, dst, n, t, pre);
     return true;
   }
 
@@ -1021,12 +1063,13 @@ class HipBackend final : public gs::Backend {
 
   // {tuned xp (plane-times), table entries, packers, ms per pass, pairs U (-1: one-unit
   // table)} of depth n (xp -1: not tuned)
-  void gate_info(int n, double* out5) const {
-    out5[0] = gate_xp_[n];
-    out5[1] = nunits_[n];
-    out5[2] = npk_[n];
-    out5[3] = gate_ms_[n];
-    out5[4] = gate_u_[n];
+  void gate_info(int n, double* out6) const {
+    out6[0] = gate_xp_[n];
+    out6[1] = nunits_[n];
+    out6[2] = npk_[n];
+    out6[3] = gate_ms_[n];
+    out6[4] = gate_u_[n];
+    out6[5] = carry_[n] ? nprod_[n] : -1;  // carried exchanges: the producers
   }
 
   // Forget the device transport after a failed trial (the "auto" fallback chain): abort the
@@ -1328,13 +1371,16 @@ class HipBackend final : public gs::Backend {
   int gate_u_[4] = {-1, -1, -1, -1};                   // tuned pairs U (-1: one-unit table)
   unsigned long long* d_stamps_ = nullptr;  // debug knob gate_stamps
   gsk::GateArgs* d_gate_ = nullptr;
-  uint32_t* d_counter_ = nullptr;
-  uint32_t cnt_host_ = 0;  // packer arrivals issued so far (the device counter's value after them)
+  uint32_t* d_counter_ = nullptr;  // two words: exchange m counts on word m & 1
+  uint32_t cnt_host_[2] = {0, 0};   // arrivals issued so far per word (its value after them)
   gsk::GateUnit* d_units_[4] = {nullptr, nullptr, nullptr, nullptr};
   size_t cap_units_[4] = {0, 0, 0, 0};
   int nunits_[4] = {0, 0, 0, 0};
   int npk_[4] = {0, 0, 0, 0};
   int gate_xp_[4] = {-1, -1, -1, -1};
+  int nprod_[4] = {0, 0, 0, 0};  // the table's producers (carried exchanges)
+  int nwu_[4] = {0, 0, 0, 0};    // the table's start-gated units
+  bool carry_[4] = {false, false, false, false};  // tuned: runs of passes carry their exchanges
   float gate_ms_[4] = {0.f, 0.f, 0.f, 0.f};
   bool gate_tuned_[4] = {false, false, false, false};
 };
@@ -1541,10 +1587,10 @@ int gs_fused_choice(gs_engine* e, int32_t n, int32_t dtype, int32_t* out2, float
 
 // the gated pass of depth n: out4 = {tuned expected exchange (plane-times, -1: not tuned),
 // units, packers, ms per pass measured while tuning}
-extern "C" int gs_gate_info(gs_engine* e, int32_t n, int32_t dtype, double* out5) {
+extern "C" int gs_gate_info(gs_engine* e, int32_t n, int32_t dtype, double* out6) {
   if (n < 0 || n > 3) return -1;
   try {
-    with_hip_backend(e, dtype, [&](auto* b) { b->gate_info(n, out5); });
+    with_hip_backend(e, dtype, [&](auto* b) { b->gate_info(n, out6); });
     return 0;
   } catch (const std::exception& ex) {
     g_gs_err = ex.what();

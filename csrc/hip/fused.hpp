@@ -85,6 +85,11 @@ struct FusedArgs {
   int32_t gate_npk;  // packers of this launch (its start-gated units)
   int32_t ngunits;
   int32_t gate_pairs;  // 1: two table entries per workgroup (gs::gate_plan_pairs)
+  // carried exchanges (gate.hpp gate_carry): bit 0 -- this pass's exchange was packed by the
+  // previous launch's producers (no packing here); bit 1 -- this pass's producers pack the next
+  // exchange (gate_n + 1) at their end, whose arrivals reach gate_cnt2
+  int32_t gate_pre;
+  uint32_t gate_cnt2;
 };
 
 template <typename T>
@@ -95,6 +100,9 @@ __device__ __forceinline__ void gate_pack(const FusedArgs& a, int pk);
 template <typename T, int BATCH>
 __device__ __forceinline__ void gate_unpack(const FusedArgs& a, int X0, int xw, int Y0, int yext,
                                          int za, int zb, uint64_t t0);
+template <typename T>
+__device__ __forceinline__ void gate_carry(const FusedArgs& a, const void* dv, int ox0, int ox1,
+                                           int oy0, int oy1, int z0, int z1);
 
 template <typename T> struct PairT;
 template <> struct PairT<float> { typedef float type __attribute__((ext_vector_type(2))); };
@@ -860,10 +868,11 @@ __device__ __forceinline__ void fused_body(const typename C::V2* __restrict__ s,
       // a start-gated unit packs, signals, waits and fills its cone's ghost cells first -- here,
       // before the march state below is live, so the production loop's registers are untouched
       const GateUnit un = a.gunits[lu0];
-      if (un.pk >= 0) {  // (a start-gated unit is always a packer)
+      const int pk = (a.gate_pre & 1) ? -1 : un.pk;  // a carried exchange is packed already
+      if (pk >= 0 || un.wait) {
         int X0, xw, Y0, yext;
         gate_cone<C>(a, un.tile, &X0, &xw, &Y0, &yext);
-        gate_start<T>(a, un.pk, un.wait != 0, X0, xw, Y0, yext, un.z0 - TL, un.z1 + TL);
+        gate_start<T>(a, pk, un.wait != 0, X0, xw, Y0, yext, un.z0 - TL, un.z1 + TL);
       }
     }
   }
@@ -1030,6 +1039,31 @@ __device__ __forceinline__ void fused_body(const typename C::V2* __restrict__ s,
       }
     }
   }  // work list
+  if constexpr (GATED == 1) {
+    // a pass that carries the next exchange: a producer packs its own outputs that lie in an
+    // outgoing message, now final (gate.hpp gate_carry)
+    if (a.gate_pre & 2) {
+      const GateUnit un = a.gunits[lu0];
+      if (un.prod) {
+        int X0, xw, Y0, yext;
+        gate_cone<C>(a, un.tile, &X0, &xw, &Y0, &yext);
+        // its output window, open past the sub-domain's faces: a message also holds ghost /
+        // padding cells there (z slabs send whole storage planes), set up front and unchanged
+        // by the pass, which the tiles at that face carry (gs::carry_window)
+        constexpr int kFar = 1 << 28;
+        int ox0 = max(X0 + TL, a.mx0);
+        int ox1 = min(X0 + TL + (xw == 64 ? a.xstep : 32 - 2 * TL), a.mx1);
+        int oy0 = max(Y0 + TL, a.my0);
+        int oy1 = min(Y0 + TL + (xw == 32 ? 2 : 1) * a.ystep, a.my1);
+        if (ox0 <= 0) ox0 = -kFar;
+        if (ox1 >= g.nx) ox1 = kFar;
+        if (oy0 <= 0) oy0 = -kFar;
+        if (oy1 >= g.ny) oy1 = kFar;
+        gate_carry<T>(a, d, ox0, ox1, oy0, oy1, un.z0 <= 0 ? -kFar : un.z0,
+                      un.z1 >= g.nz ? kFar : un.z1);
+      }
+    }
+  }
 }
 
 template <class C, typename T>
@@ -1467,6 +1501,8 @@ struct GateLaunch {
   uint32_t cnt;
   int32_t npk;
   int32_t pairs;  // the table holds two entries per workgroup
+  int32_t pre;    // FusedArgs::gate_pre (carried exchanges)
+  uint32_t cnt2;  // the carried exchange's arrival count (pre bit 1)
 };
 
 // The tile grid a configuration's launch enumerates (FusedLaunch::run + fold_strip), on the host:
@@ -1542,7 +1578,10 @@ bool launch_fused(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, co
     a.gate_cnt = gate->cnt;
     a.gate_npk = gate->npk;
     a.gate_pairs = gate->pairs ? 1 : 0;
+    a.gate_pre = gate->pre;
+    a.gate_cnt2 = gate->cnt2;
     if (a.gate_pairs && (gate->nunits & 1)) return false;
+    if (a.gate_pairs && gate->pre) return false;  // carried exchanges: one-unit tables only
     a.allow_block = 0;
   } else if (a.sched == 3) {
     a.sched = 2;  // the gated schedule needs its table

@@ -50,7 +50,13 @@ struct GateArgs {
   uint64_t* wflag[gs::kMaxMsgs];
   uint64_t* sflag[gs::kMaxMsgs];
   int32_t nwait, nsig;
-  uint32_t* counter;   // packer arrivals, monotonic over the engine's gated passes
+  // arrivals of exchange m on word m & 1, monotonic over the engine's gated passes (a launch
+  // may count two exchanges: its own start-packed one and the next, carried, one)
+  uint32_t* counter;
+  // debug knob ipc_emulate_us, carried exchanges: the publisher's wall clock when it published
+  // (this rank's word per receive peer / the peers' words per send peer)
+  uint64_t* wstamp[gs::kMaxMsgs];
+  uint64_t* sstamp[gs::kMaxMsgs];
   uint64_t ticks;      // wall-clock ticks a wait may take (GS_COMM_TIMEOUT)
   uint64_t min_ticks;  // debug knob ipc_emulate_us: the exchange lasts at least this long
   int* err;            // host-mapped: a wait timed out (the watchdog raises)
@@ -88,6 +94,23 @@ __device__ __forceinline__ uint32_t gate_div(uint32_t k, uint32_t d, float inv) 
   if (r < 0) --q;
   else if (r >= (int32_t)d) ++q;
   return q;
+}
+
+// one arrival (thread 0) at exchange m's counter; the arrival that completes the count publishes
+// m in every send peer's flag array.  carried: stamp the publication first (emulated exchange)
+__device__ __forceinline__ void gate_arrive(const GateArgs& G, uint64_t m, uint32_t target,
+                                            bool carried) {
+  const uint32_t old = __hip_atomic_fetch_add(G.counter + (m & 1), 1u, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+  if (old + 1u != target) return;
+  if (carried && G.min_ticks) {
+    const uint64_t now = wall_clock64();
+    for (int i = 0; i < G.nsig; ++i)
+      __hip_atomic_store(G.sstamp[i], now, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the stamp lands before the flag
+  }
+  for (int i = 0; i < G.nsig; ++i)
+    __hip_atomic_store(G.sflag[i], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // 1. pack + arrive: this packer's share of every outgoing message, then its arrival at the
@@ -179,11 +202,7 @@ __device__ __forceinline__ void gate_pack(const FusedArgs& a, int pk) {
       atomicMin(G.stamps + 0, (unsigned long long)t0);
       atomicMax(G.stamps + 1, (unsigned long long)wall_clock64());
     }
-    const uint32_t old = __hip_atomic_fetch_add(G.counter, 1u, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT);
-    if (old + 1u == a.gate_cnt)
-      for (int i = 0; i < G.nsig; ++i)
-        __hip_atomic_store(G.sflag[i], a.gate_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    gate_arrive(G, a.gate_n, a.gate_cnt, false);
   }
 }
 
@@ -241,18 +260,29 @@ __device__ __forceinline__ void gate_unpack(const FusedArgs& a, int X0, int xw, 
   // gfx950 an agent-scope acquire invalidates the XCD's L2, which the marching workgroups
   // stream through): the landing slot is uncached too, so no cache can hold a stale copy of
   // the messages, and the copies below issue only after the polls return.
+  const bool carried = (a.gate_pre & 1) != 0;
   if (tid < (uint32_t)G.nwait) {
     uint64_t* w = G.wflag[tid];
+    bool ok = true;
     while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < a.gate_n) {
       if (wall_clock64() - t0 > G.ticks) {
         __hip_atomic_store(G.dflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(G.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        ok = false;
         break;
       }
       __builtin_amdgcn_s_sleep(2);
     }
+    // emulated exchange, carried: it lands min_ticks after its publication (a later stamp --
+    // the peer's next exchange already published -- only lengthens the wait)
+    if (ok && carried && G.min_ticks) {
+      const uint64_t st = __hip_atomic_load(G.wstamp[tid], __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_SYSTEM);
+      while ((int64_t)(wall_clock64() - st) < (int64_t)G.min_ticks) __builtin_amdgcn_s_sleep(1);
+    }
   }
-  if (G.min_ticks && tid == 0)
+  // emulated exchange, packed at the start: it lands min_ticks after the unit's start
+  if (G.min_ticks && !carried && tid == 0)
     while (wall_clock64() - t0 < G.min_ticks) __builtin_amdgcn_s_sleep(1);
   unsigned long long wdone = 0;
   if (G.stamps && tid == 0) {
@@ -310,6 +340,101 @@ __device__ __forceinline__ void gate_unpack(const FusedArgs& a, int X0, int xw, 
     atomicAdd(G.stamps + 6, u - wdone);
     atomicAdd(G.stamps + 7, 1ull);
   }
+  // a pass that carries the next exchange: this unit is done with landing slot gate_n & 1, so
+  // the peers may fill it again (exchange gate_n + 2) once the next exchange is published
+  if ((a.gate_pre & 2) && tid == 0) gate_arrive(G, a.gate_n + 1, a.gate_cnt2, true);
+}
+
+// 4. carried exchange (a.gate_pre & 2): at the end of its march, a producer unit copies its own
+// outputs [ox0, ox1) x [oy0, oy1) x [z0, z1) that lie in an outgoing message -- the next
+// exchange's data, final now -- into the peers' landing slot (gate_n + 1) & 1 and arrives; the
+// producers' output boxes cover every message once (gs/gate_plan.h gate_mark_producers).  The
+// next pass then finds its exchange published at its start: no pack, no wait for the peers'
+// packers, only the cone unpack.  Slot reuse: a producer is a start-gated unit (symmetric
+// neighbours), so it has seen the peers publish gate_n, which they do only after every unit
+// of theirs that read slot gate_n + 1 & 1 (exchange gate_n - 1) arrived (gate_unpack above).
+template <typename T>
+__device__ __forceinline__ void gate_carry(const FusedArgs& a, const void* dv, int ox0, int ox1,
+                                           int oy0, int oy1, int z0, int z1) {
+  using V2 = typename Vec2<T>::type;
+  constexpr int B = gate_batch<T>();
+  const GateArgs& G = *a.gate;
+  const Geom& g = a.g;
+  const V2* d = (const V2*)dv;
+  const uint64_t m = a.gate_n + 1;
+  const int slot = (int)(m & 1);
+  const uint32_t nt = blockDim.x, tid = threadIdx.x;
+  __shared__ GatePiece gp[gs::kMaxMsgs];
+  __shared__ uint32_t gcells[gs::kMaxMsgs];
+  __shared__ uint32_t gtotal;
+  __shared__ int gnp;
+  // this workgroup's output stores acknowledged (then in its XCD's L2) before they are read
+  // back; the CU's L1 forgets what it held
+  asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
+  if (tid < (uint32_t)G.nsend) {
+    const Box b = G.sbox[tid];
+    const int x0 = max(b.x0, ox0), x1 = min(b.x0 + b.nx, ox1);
+    const int y0 = max(b.y0, oy0), y1 = min(b.y0 + b.ny, oy1);
+    const int zz0 = max(b.z0, z0), zz1 = min(b.z0 + b.nz, z1);
+    const bool any = x0 < x1 && y0 < y1 && zz0 < zz1;
+    gp[tid] = GatePiece{G.sdst[slot][tid], x0, y0, zz0, x1 - x0, y1 - y0, 0u, b.x0, b.y0, b.z0,
+                        b.nx, b.ny, (int)((G.sysmask >> tid) & 1u),
+                        any ? 1.0f / (float)(x1 - x0) : 0.f, any ? 1.0f / (float)(y1 - y0) : 0.f};
+    gcells[tid] = any ? (uint32_t)((x1 - x0) * (y1 - y0) * (zz1 - zz0)) : 0u;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t acc = 0;
+    int np = 0;
+    for (int i = 0; i < G.nsend; ++i) {
+      if (!gcells[i]) continue;
+      if (np != i) gp[np] = gp[i];
+      gp[np++].start = acc;
+      acc += gcells[i];
+    }
+    gtotal = acc;
+    gnp = np;
+  }
+  __syncthreads();
+  const uint32_t total = gtotal;
+  const int np = gnp;
+  const bool small = total < (1u << 24);
+  // (a piece index and a 32-bit offset per cell, not a pointer: this runs after the march, in
+  // the same register allocation)
+  for (uint32_t i0 = tid; i0 < total; i0 += B * nt) {
+    V2 c[B];
+    int32_t off[B], pc[B];
+    int p = 0;
+#pragma unroll
+    for (int j = 0; j < B; ++j) {
+      const uint32_t i = i0 + (uint32_t)j * nt;
+      pc[j] = -1;
+      if (i < total) {
+        while (p + 1 < np && gp[p + 1].start <= i) ++p;
+        const GatePiece& q = gp[p];
+        const uint32_t k = i - q.start;
+        const uint32_t r = small ? gate_div(k, (uint32_t)q.nx, q.inx) : k / (uint32_t)q.nx;
+        const uint32_t zz = small ? gate_div(r, (uint32_t)q.ny, q.iny) : r / (uint32_t)q.ny;
+        const int x = q.x0 + (int)(k - r * (uint32_t)q.nx);
+        const int y = q.y0 + (int)(r - zz * (uint32_t)q.ny);
+        const int z = q.z0 + (int)zz;
+        c[j] = d[gs::lin(g, x, y, z)];
+        off[j] = ((z - q.sz0) * q.sny + (y - q.sy0)) * q.snx + (x - q.sx0);
+        pc[j] = p;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < B; ++j) {
+      if (pc[j] < 0) continue;
+      const GatePiece& q = gp[pc[j]];
+      V2* dst = (V2*)q.ptr + off[j];
+      if (q.sys) store_system(dst, c[j]);
+      else *dst = c[j];
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every landing store acknowledged
+  __syncthreads();
+  if (tid == 0) gate_arrive(G, m, a.gate_cnt2, true);
 }
 
 // a start-gated unit in the one-unit table: pack (a packer), then wait and unpack (gated)

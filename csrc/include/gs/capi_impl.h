@@ -88,11 +88,12 @@ int gs_gate_plan(const gs::Geom* g, const int32_t* nbr27, int32_t n, int32_t xp,
       pairs ? gs::gate_plan_pairs(tg, *g, p, n, xp, unpack, allpk != 0, slots, &k)
             : gs::gate_plan(tg, *g, p, n, xp, allpk != 0, slots, longest != 0, &k);
   for (size_t i = 0; i < u.size() && (int64_t)i < cap; ++i) {
-    out[5 * i] = u[i].tile;
-    out[5 * i + 1] = u[i].z0;
-    out[5 * i + 2] = u[i].z1;
-    out[5 * i + 3] = u[i].pk;
-    out[5 * i + 4] = u[i].wait;
+    out[6 * i] = u[i].tile;
+    out[6 * i + 1] = u[i].z0;
+    out[6 * i + 2] = u[i].z1;
+    out[6 * i + 3] = u[i].pk;
+    out[6 * i + 4] = u[i].wait;
+    out[6 * i + 5] = u[i].prod;
   }
   if (npk) *npk = k;
   if (grid_out) {

@@ -25,8 +25,9 @@
 //   ipc_pair_same_dir 0 (default); 1: modelling only -- a loopback IPC message lands in the ghost
 //                   box of its own direction, so one rank can time a one-sided neighbour set
 //                   (+x, +y, +z: a 2x2x2 rank); the values are no wrap.  Read at connect.
-//   gate_mode       0 (default): the gated pass's tuner times one-unit and pairs tables; 1: one-unit
-//                   tables only; 2: pairs tables only (tests of each kernel path).  Read at tuning.
+//   gate_mode       0 (default): the gated pass's tuner times carried, one-unit and pairs tables;
+//                   1: one-unit tables packed at the start only; 2: pairs tables only; 3: carried
+//                   one-unit tables only (tests of each kernel path).  Read at tuning.
 //   cpu_ftz         1 (default): the CPU solver flushes fp32 denormals in its step region
 //                   (MXCSR FTZ + DAZ; ~100x faster where the reference example's v field
 //                   passes through them); 0: IEEE denormals, the reference's and the GPU's

@@ -87,8 +87,10 @@ class Backend {
   // src -> dst including the halo exchange of src.
   virtual bool gated_supported(int n) const { (void)n; return false; }
   virtual void prepare_gated(int src, int dst, int n, int64_t t) { (void)src; (void)dst; (void)n; (void)t; }
-  virtual bool fused_gated(int src, int dst, int n, int64_t t) {
-    (void)src; (void)dst; (void)n; (void)t;
+  // first / last: the pass opens / closes a run of gated passes (carried exchanges stay inside
+  // a run)
+  virtual bool fused_gated(int src, int dst, int n, int64_t t, bool first, bool last) {
+    (void)src; (void)dst; (void)n; (void)t; (void)first; (void)last;
     return false;
   }
   // in-place transport of a zplanes plan straight from / into field buffer b (no pack)
@@ -529,7 +531,7 @@ class Engine {
       plog_.begin_pass(k);
       TraceRange tr("gs.fused_gated");
       pm(kPhFused, true);
-      if (!be_->fused_gated(cur_, oth, k, t_))
+      if (!be_->fused_gated(cur_, oth, k, t_, p == 0, p + 1 == npass))
         throw std::runtime_error("gated pass: the backend refused the launch");
       pm(kPhFused, false);
       ++ncomm_;

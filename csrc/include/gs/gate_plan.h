@@ -71,12 +71,59 @@ inline void tile_window(const TileGrid& t, int tile, int n, int* X0, int* xw, in
   *Y0 = t.ybase + ty * t.ystep - n;
 }
 
+// output window of tile `tile` in x / y: [ox0, ox1) x [oy0, oy1), the cells its launch stores
+// (fused.hpp fused_body: xstep columns -- a folded tile 32 - 2n -- and ystep rows -- a folded
+// tile two y-tiles --, clipped to the sub-domain); the tiles' windows partition the interior
+inline void tile_output(const TileGrid& t, const Geom& g, int tile, int n, int* ox0, int* ox1,
+                        int* oy0, int* oy1) {
+  int X0, xw, Y0, ye;
+  tile_window(t, tile, n, &X0, &xw, &Y0, &ye);
+  const bool folded = xw == 32;
+  *ox0 = std::max(X0 + n, 0);
+  *ox1 = std::min(X0 + n + (folded ? 32 - 2 * n : t.xstep), g.nx);
+  *oy0 = std::max(Y0 + n, 0);
+  *oy1 = std::min(Y0 + n + (folded ? 2 : 1) * t.ystep, g.ny);
+}
+
 struct GateUnit {
   int32_t tile;    // tile index (the launch's enumeration)
   int32_t z0, z1;  // output planes [z0, z1)
   int32_t pk;      // >= 0: a packer, its index; -1: none (every start-gated unit packs)
   int32_t wait;    // 1: start-gated (waits for the peers, copies its cone's ghosts)
+  int32_t prod;    // 1: its outputs meet a send box (a carried exchange: it packs them at its end)
 };
+
+// The cells a unit carries into the next exchange's messages: its output box, open past the
+// sub-domain's faces (a message also holds ghost / padding cells there -- z slabs send whole
+// storage planes -- which the units at that face carry; set up front, unchanged by a pass).  The
+// boxes of all units still partition space, so every message cell is carried exactly once.
+constexpr int kCarryFar = 1 << 28;
+inline Box carry_window(const TileGrid& tg, const Geom& g, const GateUnit& x, int n) {
+  int ox0, ox1, oy0, oy1;
+  tile_output(tg, g, x.tile, n, &ox0, &ox1, &oy0, &oy1);
+  if (ox0 <= 0) ox0 = -kCarryFar;
+  if (ox1 >= g.nx) ox1 = kCarryFar;
+  if (oy0 <= 0) oy0 = -kCarryFar;
+  if (oy1 >= g.ny) oy1 = kCarryFar;
+  const int z0 = x.z0 <= 0 ? -kCarryFar : x.z0, z1 = x.z1 >= g.nz ? kCarryFar : x.z1;
+  return Box{ox0, oy0, z0, ox1 - ox0, oy1 - oy0, z1 - z0};
+}
+
+// prod of every unit: its carry window meets an outgoing message
+inline void gate_mark_producers(const TileGrid& tg, const Geom& g, const HaloPlan& p, int n,
+                                std::vector<GateUnit>* u) {
+  for (GateUnit& x : *u) {
+    x.prod = 0;
+    if (x.tile < 0) continue;
+    const Box w = carry_window(tg, g, x, n);
+    for (int i = 0; i < p.nsend && !x.prod; ++i) {
+      const Box& b = p.send[i].box;
+      if (b.x0 < w.x0 + w.nx && w.x0 < b.x0 + b.nx && b.y0 < w.y0 + w.ny &&
+          w.y0 < b.y0 + b.ny && b.z0 < w.z0 + w.nz && w.z0 < b.z0 + b.nz)
+        x.prod = 1;
+    }
+  }
+}
 
 // Which ghost reads each tile column has: strip (an x / y ghost box at interior planes: gated
 // over its whole length), lo / hi (the z ghosts below / above, read by its end chunks)
@@ -122,7 +169,7 @@ inline std::vector<GateUnit> gate_plan(const TileGrid& tg, const Geom& g, const 
       for (int i = 0; i < k; ++i) {
         const int z0 = a + (int)((int64_t)(b - a) * i / k);
         const int z1 = a + (int)((int64_t)(b - a) * (i + 1) / k);
-        if (out) out->push_back(GateUnit{t, z0, z1, gated ? 0 : -1, gated ? 1 : 0});
+        if (out) out->push_back(GateUnit{t, z0, z1, gated ? 0 : -1, gated ? 1 : 0, 0});
         ++cnt;
       }
     };
@@ -152,6 +199,7 @@ inline std::vector<GateUnit> gate_plan(const TileGrid& tg, const Geom& g, const 
   for (auto& x : u)
     if (x.wait || allpk) x.pk = k++;
   *npk = k;
+  gate_mark_producers(tg, g, p, n, &u);
   return u;
 }
 
@@ -229,7 +277,7 @@ inline std::vector<GateUnit> gate_plan_pairs(const TileGrid& tg, const Geom& g, 
   std::stable_sort(gated.begin(), gated.end(), [](const Piece& a, const Piece& b) {
     return a.z0 != b.z0 ? a.z0 < b.z0 : a.t < b.t;
   });
-  const GateUnit none{-1, 0, 0, -1, 0};
+  const GateUnit none{-1, 0, 0, -1, 0, 0};
   // cut the ungated ranges into the pairs' first chunks, then into single units; a chunk never
   // crosses a column, so a range's short remainder can waste a pair's room: raise M until the
   // workgroups fit
@@ -249,13 +297,13 @@ inline std::vector<GateUnit> gate_plan_pairs(const TileGrid& tg, const Geom& g, 
     for (const Piece& q : gated) {
       Piece a{};
       const bool first = take(M - (U + Fu + (q.z1 - q.z0)) - Fu, &a);
-      u.push_back(first ? GateUnit{a.t, a.z0, a.z1, -1, 0} : none);
-      u.push_back(GateUnit{q.t, q.z0, q.z1, -1, 1});
+      u.push_back(first ? GateUnit{a.t, a.z0, a.z1, -1, 0, 0} : none);
+      u.push_back(GateUnit{q.t, q.z0, q.z1, -1, 1, 0});
     }
     for (;;) {
       Piece a{};
       if (!take(M - Fu, &a)) break;
-      u.push_back(GateUnit{a.t, a.z0, a.z1, -1, 0});
+      u.push_back(GateUnit{a.t, a.z0, a.z1, -1, 0, 0});
       u.push_back(none);
     }
     if ((int)(u.size() / 2) <= slots) break;

@@ -214,7 +214,7 @@ def gate_plan(g: Geom, nbr27, n: int, xp: int = 0, allpk: bool = False, slots: i
               longest: bool = False, rows: int = 4, waves: int = 12, fold: bool = False,
               pairs: bool = False, unpack: int = 0):
     """The gated pass's unit table for a sub-domain (csrc/include/gs/gate_plan.h, host only):
-    ``(units, npk, grid)`` -- units as (tile, z0, z1, pk, wait) tuples, the packer count and the
+    ``(units, npk, grid)`` -- units as (tile, z0, z1, pk, wait, prod) tuples, the packer count and the
     tile grid {xstep, ystep, ybase, ntx, nty, ntxf, nfold, ntiles, rt}.  pairs: the
     two-units-per-workgroup table (entries 2w, 2w + 1; tile -1 = empty), xp the expected
     exchange and ``unpack`` the cone unpack, in plane-times."""
@@ -224,13 +224,13 @@ def gate_plan(g: Geom, nbr27, n: int, xp: int = 0, allpk: bool = False, slots: i
     grid = (c_int32 * 9)()
     npk = c_int32()
     cap = 1 << 16
-    out = (c_int32 * (5 * cap))()
+    out = (c_int32 * (6 * cap))()
     k = lib.gs_gate_plan(ctypes.byref(g), arr, int(n), int(xp), 1 if allpk else 0, int(slots),
                          1 if longest else 0, int(rows), int(waves), 1 if fold else 0,
                          1 if pairs else 0, int(unpack), out, cap, ctypes.byref(npk), grid)
     if k < 0 or k > cap:
         raise ValueError(f"gs_gate_plan failed ({k})")
-    units = [tuple(out[5 * i:5 * i + 5]) for i in range(k)]
+    units = [tuple(out[6 * i:6 * i + 6]) for i in range(k)]
     keys = ("xstep", "ystep", "ybase", "ntx", "nty", "ntxf", "nfold", "ntiles", "rt")
     return units, int(npk.value), dict(zip(keys, list(grid)))
 
@@ -333,12 +333,13 @@ class Engine:
         self._chk(self.lib.gs_set_gated(self.h, 1 if on else 0), "set_gated")
 
     def gate_info(self, k: int):
-        """{"xp", "units" (workgroups), "packers", "ms", "pairs_unpack"} of the tuned gated pass
-        of depth k (HIP only; pairs_unpack: the pairs table's U, None for a one-unit table), or
+        """{"xp", "units" (workgroups), "packers", "ms", "pairs_unpack", "carried"} of the tuned
+        gated pass of depth k (HIP only; pairs_unpack: the pairs table's U, None for a one-unit
+        table; carried: the producers when runs of passes carry their exchanges, else None), or
         None."""
         if not hasattr(self.lib, "gs_gate_info"):
             return None
-        out = (c_double * 5)()
+        out = (c_double * 6)()
         self.lib.gs_gate_info.argtypes = [c_void_p, c_int32, c_int32, POINTER(c_double)]
         self.lib.gs_gate_info.restype = c_int
         if self.lib.gs_gate_info(self.h, int(k), DTYPE_CODES[self.dtype], out) != 0 or out[0] < 0:
@@ -346,7 +347,8 @@ class Engine:
         pairs = out[4] >= 0
         return {"xp": int(out[0]), "units": int(out[1]) // (2 if pairs else 1),
                 "packers": int(out[2]), "ms": round(float(out[3]), 5),
-                "pairs_unpack": int(out[4]) if pairs else None}
+                "pairs_unpack": int(out[4]) if pairs else None,
+                "carried": int(out[5]) if out[5] >= 0 else None}
 
     def set_auto_depth(self, on: bool):
         self._chk(self.lib.gs_set_auto_depth(self.h, 1 if on else 0), "set_auto_depth")

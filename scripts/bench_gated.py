@@ -42,8 +42,9 @@ def main():
     ap.add_argument("--prec", default="Float32")
     ap.add_argument("--out", default="")
     ap.add_argument("--gate-modes", type=int, nargs="+", default=[0],
-                    help="debug knob gate_mode per gated row: 0 tuned (one-unit and pairs tables), "
-                         "1 one-unit tables only, 2 pairs tables only")
+                    help="debug knob gate_mode per gated row: 0 tuned (carried, one-unit and "
+                         "pairs tables), 1 one-unit tables packed at the start only, 2 pairs "
+                         "tables only, 3 carried one-unit tables only")
     ap.add_argument("--gated-only", action="store_true", help="skip the stream / serial rows")
     ap.add_argument("--stamps", action="store_true",
                     help="debug knob gate_stamps: the exchange's wall-clock stamps (after the "

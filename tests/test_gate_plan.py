@@ -6,7 +6,10 @@ For every sub-domain / neighbour set: the units of each tile column partition it
 [0, nz); a unit is start-gated exactly when its read box -- the tile's x / y window x
 [z0 - n, z1 + n) -- meets a ghost region a neighbour fills (H cells deep on that side); the
 units fit the slots when some plane budget allows it; the table is sorted by (z0, tile) and the
-packers are numbered 0..npk-1 (the start-gated units, or every unit)."""
+packers are numbered 0..npk-1 (the start-gated units, or every unit); a unit is a producer
+(it packs its outputs into the next exchange's messages at its end in a carried exchange)
+exactly when its output box meets a send region, and the producers' output boxes cover every
+send region's cells once."""
 import itertools
 
 import pytest
@@ -47,6 +50,63 @@ def _meets(a, b):
     return a[0] < b[1] and b[0] < a[1]
 
 
+def _send_regions(g, dirs):
+    """The outgoing messages (gs::make_halo_plan): interior side boxes, H deep; z slabs (z
+    neighbours only) send whole storage planes, ghost and padding columns / rows included."""
+    nx, ny, nz = g.nx, g.ny, g.nz
+
+    def rng(d, n):
+        return (0, H) if d < 0 else ((n - H, n) if d > 0 else (0, n))
+    zplanes = all(dx == 0 and dy == 0 for dx, dy, _ in dirs)
+    out = []
+    for dx, dy, dz in dirs:
+        sx, sy = rng(dx, nx), rng(dy, ny)
+        if zplanes:
+            sx, sy = (-g.xo, g.px - g.xo), (-H, g.py - H)
+        out.append((sx, sy, rng(dz, nz)))
+    return out
+
+
+FAR = 1 << 28
+
+
+def _carry_window(grid, tile, n, g, z0, z1):
+    """Independent copy of the cells a unit carries: the cells its tile's launch stores
+    (fused.hpp fused_body: ox1 / oy1) x [z0, z1), open past the sub-domain's faces."""
+    (x0, x1), (y0, y1) = _window(grid, tile, n)
+    folded = x1 - x0 == 32
+    ox = [max(x0 + n, 0), min(x0 + n + (32 - 2 * n if folded else grid["xstep"]), g.nx)]
+    oy = [max(y0 + n, 0), min(y0 + n + (2 if folded else 1) * grid["ystep"], g.ny)]
+    oz = [z0, z1]
+    for w, size in ((ox, g.nx), (oy, g.ny), (oz, g.nz)):
+        if w[0] <= 0:
+            w[0] = -FAR
+        if w[1] >= size:
+            w[1] = FAR
+    return ox, oy, oz
+
+
+def _check_producers(units, grid, n, g, dirs):
+    sends = _send_regions(g, dirs)
+    covered = [0] * len(sends)
+    for t, z0, z1, pk, wait, prod in units:
+        if t < 0:
+            continue
+        ox, oy, oz = _carry_window(grid, t, n, g, z0, z1)
+        meets = False
+        for i, (sx, sy, sz) in enumerate(sends):
+            cx = max(0, min(ox[1], sx[1]) - max(ox[0], sx[0]))
+            cy = max(0, min(oy[1], sy[1]) - max(oy[0], sy[0]))
+            cz = max(0, min(oz[1], sz[1]) - max(oz[0], sz[0]))
+            covered[i] += cx * cy * cz
+            meets = meets or cx * cy * cz > 0
+        assert bool(prod) == meets, (t, z0, z1, prod)
+        if prod:
+            assert wait, (t, z0, z1)  # symmetric neighbours: a producer read the same peer's ghosts
+    for (sx, sy, sz), c in zip(sends, covered):
+        assert c == (sx[1] - sx[0]) * (sy[1] - sy[0]) * (sz[1] - sz[0])
+
+
 ONE_SIDED = [d for d in itertools.product((0, 1), repeat=3) if d != (0, 0, 0)]
 ALL26 = [d for d in itertools.product((-1, 0, 1), repeat=3) if d != (0, 0, 0)]
 Z_ONLY = [(0, 0, -1), (0, 0, 1)]
@@ -71,7 +131,7 @@ def test_gate_plan_matches_independent_cones(shape, dirs, n, fold, xp, allpk, sl
     ghosts = _ghost_regions(nx, ny, nz, dirs)
     # each column's units partition [0, nz)
     by_tile = {}
-    for t, z0, z1, pk, wait in units:
+    for t, z0, z1, pk, wait, prod in units:
         assert 0 <= t < grid["ntiles"] and 0 <= z0 < z1 <= nz
         by_tile.setdefault(t, []).append((z0, z1))
     assert sorted(by_tile) == list(range(grid["ntiles"]))
@@ -80,7 +140,7 @@ def test_gate_plan_matches_independent_cones(shape, dirs, n, fold, xp, allpk, sl
         assert iv[0][0] == 0 and iv[-1][1] == nz
         assert all(a[1] == b[0] for a, b in zip(iv, iv[1:])), (t, iv)
     # start-gated exactly when the read box meets a neighbour's ghost region
-    for t, z0, z1, pk, wait in units:
+    for t, z0, z1, pk, wait, prod in units:
         xr, yr = _window(grid, t, n)
         zr = (z0 - n, z1 + n)
         need = any(_meets(xr, gx) and _meets(yr, gy) and _meets(zr, gz) for gx, gy, gz in ghosts)
@@ -98,6 +158,7 @@ def test_gate_plan_matches_independent_cones(shape, dirs, n, fold, xp, allpk, sl
         assert npk == len(units)
     else:
         assert all((u[3] >= 0) == bool(u[4]) for u in units)
+    _check_producers(units, grid, n, g, dirs)
 
 
 def test_gate_plan_tile_grid_matches_the_kernel():
@@ -131,7 +192,7 @@ def test_gate_plan_pairs(shape, dirs, n, fold, X, U, allpk, slots):
     assert units and len(units) % 2 == 0 and len(units) // 2 <= slots
     ghosts = _ghost_regions(nx, ny, nz, dirs)
     by_tile = {}
-    for i, (t, z0, z1, pk, wait) in enumerate(units):
+    for i, (t, z0, z1, pk, wait, prod) in enumerate(units):
         if t < 0:
             continue
         assert 0 <= z0 < z1 <= nz

@@ -4,7 +4,9 @@
 Start-gated workgroups pack their share of every outgoing message into the peers' landing
 buffers, the last packer publishes the exchange, and each start-gated workgroup waits for its
 peers' flags and copies the ghost cells of its own cone before marching; every other workgroup
-marches at once.  Every result must be bit-identical to the single-rank run (and to the
+marches at once.  Carried exchanges (debug knob gate_mode 3): inside a run of passes, the
+producer workgroups pack their own outputs into the NEXT exchange's messages at the end of
+their march, so a pass finds its exchange already published.  Every result must be bit-identical to the single-rank run (and to the
 stream-overlapped passes, debug knob gated = 0): chunking a tile column into units never
 changes a value.  The reference's blocking exchange-then-compute step is
 src/simulation/public.jl:58-64.
@@ -46,7 +48,10 @@ def _single(L, steps, fuse, prec="Float32", random_init=None):
                                                      ("yz", 40, 3, "Float32", 0),
                                                      ("yz", 36, 2, "Float64", 0),
                                                      ("z", 48, 3, "Float32", 2),
-                                                     ("yz", 40, 3, "Float32", 2)])
+                                                     ("yz", 40, 3, "Float32", 2),
+                                                     ("z", 48, 3, "Float32", 3),
+                                                     ("yz", 40, 3, "Float32", 3),
+                                                     ("yz", 36, 2, "Float64", 3)])
 def test_gated_loopback(which, L, fuse, prec, mode, debug_knob):
     """One process, its halos sent to ITSELF through the landing buffer on a non-periodic
     geometry (wraps as messages): z neighbours only, or the 8 directions with dx = 0 (faces,
@@ -69,7 +74,7 @@ def test_gated_loopback(which, L, fuse, prec, mode, debug_knob):
     s = Settings(L=L, precision=prec, F=0.02, k=0.048, dt=1.0, Du=0.2, Dv=0.1, noise=0.1,
                  backend="AMDGPU", seed=99, overlap="on")
     out = []
-    debug_knob("gate_mode", mode)  # 2: pairs tables only
+    debug_knob("gate_mode", mode)  # 2: pairs tables only, 3: carried exchanges only
     # the reference: the same wraps as device self copies (no loopback)
     for kw in ({}, dict(transport="ipc", loopback=True)):
         sim = GrayScott(s, loop, fuse=fuse, **kw)
@@ -83,6 +88,8 @@ def test_gated_loopback(which, L, fuse, prec, mode, debug_knob):
             sim.close()
     (u0, v0, g0, _), (u1, v1, g1, info) = out
     assert not g0 and g1 and info["units"] > 0 and info["packers"] > 0, info
+    if mode == 3:
+        assert info["carried"] and info["carried"] > 0, info
     assert np.isfinite(u1).all()
     np.testing.assert_array_equal(u1, u0)
     np.testing.assert_array_equal(v1, v0)
@@ -99,6 +106,13 @@ def test_gated_loopback(which, L, fuse, prec, mode, debug_knob):
     (2, [1, 1, 2], 48, 3, "Float32", 2),
     (4, [2, 2, 1], 64, 2, "Float64", 2),
     (8, [2, 2, 2], 64, 3, "Float32", 2),
+    # carried exchanges (the next exchange packed by the producers at the end of their march)
+    (2, [1, 1, 2], 48, 3, "Float32", 3),
+    (2, [2, 1, 1], 64, 3, "Float32", 3),
+    (4, [2, 2, 1], 64, 2, "Float64", 3),
+    (8, [2, 2, 2], 64, 3, "Float32", 3),
+    (3, [1, 1, 3], 40, 2, "Float32", 3),
+    (4, [2, 2, 1], 48, 3, "Float64", 3),
 ])
 def test_gated_matches_single_rank(world, dims, L, fuse, prec, mode):
     steps = 4 * fuse + 1  # full gated passes and a trailing partial pass (stream exchange)
@@ -112,6 +126,7 @@ def test_gated_matches_single_rank(world, dims, L, fuse, prec, mode):
         g = m["gate"]
         assert g is not None and g["units"] > 0 and 0 < g["packers"] <= g["units"], g
         assert (g["pairs_unpack"] is not None) == (mode == 2), g
+        assert (g["carried"] is not None) == (mode == 3), g
     assert np.isfinite(un).all()
     np.testing.assert_array_equal(un, u1)
     np.testing.assert_array_equal(vn, v1)
@@ -135,13 +150,14 @@ def test_gated_off_is_the_stream_overlap():
     np.testing.assert_array_equal(vg, vs)
 
 
-def test_gated_emulated_slow_exchange():
+@pytest.mark.parametrize("mode", [0, 3])
+def test_gated_emulated_slow_exchange(mode):
     """Debug knob ipc_emulate_us: every gated wait lasts at least 30 us (a slow xGMI hop
-    modelled on one GPU); the tuner sees it (its expected exchange time grows) and the result is
-    unchanged."""
-    L, steps, fuse = 64, 7, 3
+    modelled on one GPU: after the unit's start, or after a carried exchange's publication);
+    the tuner sees it (its expected exchange time grows) and the result is unchanged."""
+    L, steps, fuse = 64, 10, 3
     u1, v1, _ = _single(L, steps, fuse, random_init=3)
-    cfg = _cfg(L, steps, fuse, knobs={"ipc_emulate_us": 30}, overlap="on")
+    cfg = _cfg(L, steps, fuse, knobs={"ipc_emulate_us": 30, "gate_mode": mode}, overlap="on")
     cfg["dims"] = [2, 2, 2]
     cfg["random_init"] = 3
     un, vn, meta = run_ranks(8, cfg)
@@ -150,12 +166,13 @@ def test_gated_emulated_slow_exchange():
     np.testing.assert_array_equal(vn, v1)
 
 
-def test_gated_halo_poisoning():
+@pytest.mark.parametrize("mode", [1, 3])
+def test_gated_halo_poisoning(mode):
     """NaN in every ghost / padding cell before the run: the in-kernel exchange must refill every
     ghost cell some start-gated unit's cone reads, and no non-gated unit may read one."""
     L, steps, fuse = 48, 9, 3
     u1, v1, _ = _single(L, steps, fuse)
-    cfg = _cfg(L, steps, fuse, overlap="on")
+    cfg = _cfg(L, steps, fuse, knobs={"gate_mode": mode}, overlap="on")
     cfg["dims"] = [2, 2, 1]
     cfg["poison"] = True
     un, vn, meta = run_ranks(4, cfg)
@@ -165,12 +182,14 @@ def test_gated_halo_poisoning():
     np.testing.assert_array_equal(vn, v1)
 
 
-def test_gated_long_run():
+@pytest.mark.parametrize("mode", [1, 3])
+def test_gated_long_run(mode):
     """Soak of the in-kernel protocol: 4 ranks, 2x2x1, 300 steps of depth 3 (100 gated
-    exchanges, both landing slots reused 50 times each) -- bit-identical to one rank."""
+    exchanges, both landing slots reused 50 times each; carried: 99 of them packed by the
+    previous pass) -- bit-identical to one rank."""
     L, steps, fuse = 40, 300, 3
     u1, v1, _ = _single(L, steps, fuse, random_init=31)
-    cfg = _cfg(L, steps, fuse, overlap="on")
+    cfg = _cfg(L, steps, fuse, knobs={"gate_mode": mode}, overlap="on")
     cfg["dims"] = [2, 2, 1]
     cfg["random_init"] = 31
     un, vn, meta = run_ranks(4, cfg)
