@@ -23,7 +23,9 @@
 //   * the host sizes the chunks so that every workgroup finishes together: gated chunks are
 //     shorter by the expected exchange time (tuned on the device, backend_hip.hip gate_tune;
 //     the planner is gs/gate_plan.h).  Pairs tables give a workgroup an ungated chunk first and
-//     run the wait and unpack between its two marches (k_fused_gated<..., PAIRS>).
+//     run the wait and unpack between its two marches (k_fused_gated<..., PAIRS>);
+//   * carried exchanges (gate_carry): inside a run of passes the producers pack the NEXT
+//     exchange from their own outputs at the end of their march, so a pass only unpacks.
 // No fence wider than the workgroup runs inside the launch (gfx950: a system release is
 // buffer_wbl2, an agent acquire buffer_inv sc1 -- the XCD's whole L2 under the marching
 // workgroups): the landing slots and flags are uncached, so nothing the protocol reads can be
