@@ -1039,7 +1039,7 @@ __device__ __forceinline__ void fused_body(const typename C::V2* __restrict__ s,
       }
     }
   }  // work list
-  if constexpr (GATED == 1) {
+  if constexpr (GATED == 3) {
     // a pass that carries the next exchange: a producer packs its own outputs that lie in an
     // outgoing message, now final (gate.hpp gate_carry)
     if (a.gate_pre & 2) {
@@ -1074,14 +1074,15 @@ __global__ __launch_bounds__(64 * C::WAVES, C::WPEU) void k_fused(const typename
   fused_body<C, T, 0>(s, d, a, f, seed);
 }
 
-// the gated pass's entry (gate.hpp): instantiated for the shapes FCfg::GATE_OK names only;
-// PAIRS: the two-entries-per-workgroup tables (its own code object: the unpack between two
-// marches raises the register pressure the one-unit entry does not pay)
-template <class C, typename T, bool PAIRS>
+// the gated pass's entries (gate.hpp): instantiated for the shapes FCfg::GATE_OK names only.
+// MODE 0: one-unit tables; 1: pairs tables (the unpack between two marches raises the register
+// pressure); 2: one-unit tables whose pass carries the next exchange (gate_carry after the
+// march).  Each its own code object, so no mode pays for another's code.
+template <class C, typename T, int MODE>
 __global__ __launch_bounds__(64 * C::WAVES, C::WPEU) void k_fused_gated(
     const typename C::V2* __restrict__ s, typename C::V2* __restrict__ d, FusedArgs a,
     FoldCoef<T> f, uint64_t seed) {
-  fused_body<C, T, PAIRS ? 2 : 1>(s, d, a, f, seed);
+  fused_body<C, T, MODE == 1 ? 2 : (MODE == 2 ? 3 : 1)>(s, d, a, f, seed);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1114,17 +1115,21 @@ struct FusedLaunch {
     return occ;
   }
   // resident workgroups per CU of the gated entry (the host sizes a gated table to these slots)
+  // (one-unit tables: the lower of the plain and the carrying entry -- a run of passes uses both)
   static int gated_occupancy(bool pairs) {
-    int o = 0, o2 = 0;
+    int o = 0, o2 = 0, o3 = 0;
     if constexpr (C::GATE_OK) {
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k_fused_gated<C, T, false>,
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k_fused_gated<C, T, 0>,
                                                        64 * C::WAVES, 0) != hipSuccess)
         o = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o2, k_fused_gated<C, T, true>,
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o2, k_fused_gated<C, T, 1>,
                                                        64 * C::WAVES, 0) != hipSuccess)
         o2 = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o3, k_fused_gated<C, T, 2>,
+                                                       64 * C::WAVES, 0) != hipSuccess)
+        o3 = 0;
     }
-    return pairs ? o2 : o;
+    return pairs ? o2 : std::min(o, o3);
   }
   static void run(const void* s, void* d, const FusedArgs& a0, const gs::Params& p,
                   hipStream_t st) {
@@ -1152,10 +1157,13 @@ struct FusedLaunch {
         a.grpM = ((a.gate_pairs ? a.ngunits / 2 : a.ngunits) + 7) / 8;
         const FoldCoef<T> f = make_fold<T>(p);
         if (a.gate_pairs)
-          k_fused_gated<C, T, true><<<(unsigned)(8 * a.grpM), 64 * C::WAVES, 0, st>>>(
+          k_fused_gated<C, T, 1><<<(unsigned)(8 * a.grpM), 64 * C::WAVES, 0, st>>>(
+              (const typename C::V2*)s, (typename C::V2*)d, a, f, p.seed);
+        else if (a.gate_pre & 2)
+          k_fused_gated<C, T, 2><<<(unsigned)(8 * a.grpM), 64 * C::WAVES, 0, st>>>(
               (const typename C::V2*)s, (typename C::V2*)d, a, f, p.seed);
         else
-          k_fused_gated<C, T, false><<<(unsigned)(8 * a.grpM), 64 * C::WAVES, 0, st>>>(
+          k_fused_gated<C, T, 0><<<(unsigned)(8 * a.grpM), 64 * C::WAVES, 0, st>>>(
               (const typename C::V2*)s, (typename C::V2*)d, a, f, p.seed);
       }
       return;  // (gated_shape_cfg never names a shape without the gated entry)
