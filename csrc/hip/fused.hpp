@@ -1303,6 +1303,8 @@ inline const FusedCfgEntry* fused_cfg_table(int* n) {
       {"4x12:1s-abl2048", true, false}, // 52  non-temporal output stores (exact)
       {"4x12:1s-abl4096", true, false}, // 53  device-scope (write-through) output stores (exact)
       {"4x12:1s-abl6144", true, false}, // 54  both (exact)
+      {"4x12:2s-abl128", true, false},  // 55  2-plane prefetch + step-uniform Philox words in VGPRs
+      {"4x12:3s-abl128", true, false},  // 56  3-plane prefetch + step-uniform Philox words in VGPRs
 #endif
   };
   *n = (int)(sizeof(t) / sizeof(t[0]));
@@ -1442,6 +1444,8 @@ void run_fused_cfg(const void* s, void* d, const FusedArgs& a, const gs::Params&
       case 52: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 2048>, T>::run(s, d, a, p, st); return;
       case 53: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 4096>, T>::run(s, d, a, p, st); return;
       case 54: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 6144>, T>::run(s, d, a, p, st); return;
+      case 55: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, Q32, 128>, T>::run(s, d, a, p, st); return;
+      case 56: FusedLaunch<FCfg<T, TL, 4, 12, 3, PER, NZ, true, Q32, 128>, T>::run(s, d, a, p, st); return;
 #endif
       default: break;  // 0 and 14: the default shape below
     }
