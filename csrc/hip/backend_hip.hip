@@ -877,7 +877,8 @@ class HipBackend final : public gs::Backend {
     G.err = ipc_err_dev_;
     G.dflag = ipc_dflag_;
     if (gs::debug_knobs().gate_stamps) {
-      HIP_CHECK(hipMalloc((void**)&d_stamps_, 8 * sizeof(unsigned long long)));
+      HIP_CHECK(hipMalloc((void**)&d_stamps_, 11 * sizeof(unsigned long long)));
+      HIP_CHECK(hipMemset(d_stamps_, 0, 11 * sizeof(unsigned long long)));
       G.stamps = d_stamps_;
     }
     HIP_CHECK(hipMalloc((void**)&d_gate_, sizeof(gsk::GateArgs)));
@@ -1042,22 +1043,28 @@ class HipBackend final : public gs::Backend {
     return true;
   }
 
-  // debug knob gate_stamps: the last gated launch's exchange, µs after its first packer
-  // started -- {last arrival (packing done), first wait done, last wait done, last unpack done,
-  // the longest and the mean unpack of one unit}
-  void gate_stamps(double* out6) {
-    for (int i = 0; i < 6; ++i) out6[i] = -1.0;
+  // debug knob gate_stamps: the last gated launch's exchange, µs after its first packer or
+  // waiting unit started -- {last arrival (packing done; -1: a carried exchange), first wait
+  // done, last wait done, last unpack done, the longest and the mean unpack of one unit}, then
+  // over every launch since set-up the longest and the mean carry of one producer (-1: none)
+  void gate_stamps(double* out8) {
+    for (int i = 0; i < 8; ++i) out8[i] = -1.0;
     if (!d_stamps_) return;
     HIP_CHECK(hipStreamSynchronize(stream_));
-    unsigned long long h[8];
+    unsigned long long h[11];
     HIP_CHECK(hipMemcpy(h, d_stamps_, sizeof(h), hipMemcpyDeviceToHost));
     int khz = 0;
     HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev_));
     const double us = 1000.0 / (double)std::max(khz, 1);
+    if (h[10]) {
+      out8[6] = (double)h[8] * us;
+      out8[7] = (double)h[9] * us / (double)h[10];
+    }
     if (h[0] == ~0ull) return;
-    for (int i = 0; i < 4; ++i) out6[i] = (double)(h[i + 1] - h[0]) * us;
-    out6[4] = (double)h[5] * us;                                  // longest unit unpack
-    out6[5] = h[7] ? (double)h[6] * us / (double)h[7] : 0.0;      // mean unit unpack
+    for (int i = 0; i < 4; ++i)
+      if (h[i + 1] >= h[0]) out8[i] = (double)(h[i + 1] - h[0]) * us;
+    out8[4] = (double)h[5] * us;                                  // longest unit unpack
+    out8[5] = h[7] ? (double)h[6] * us / (double)h[7] : 0.0;      // mean unit unpack
   }
 
 
@@ -1641,9 +1648,9 @@ extern "C" int gs_snapshot(gs_engine* e, int32_t dtype, void* du, void* dv, void
   }
 }
 
-extern "C" int gs_gate_stamps(gs_engine* e, int32_t dtype, double* out6) {
+extern "C" int gs_gate_stamps(gs_engine* e, int32_t dtype, double* out8) {
   try {
-    with_hip_backend(e, dtype, [&](auto* b) { b->gate_stamps(out6); });
+    with_hip_backend(e, dtype, [&](auto* b) { b->gate_stamps(out8); });
     return 0;
   } catch (const std::exception& ex) {
     g_gs_err = ex.what();

@@ -64,8 +64,10 @@ struct GateArgs {
   int* err;            // host-mapped: a wait timed out (the watchdog raises)
   int* dflag;          // device copy: later copies write NaN instead of stale landing data
   // debug knob gate_stamps: wall-clock stamps of the launch's exchange (null: none) --
-  // [0] min start, [1] max packer arrival, [2] min / [3] max wait done, [4] max unpack done,
-  // [5] max / [6] sum of a unit's unpack duration (wait done -> unpack done), [7] units
+  // [0] min start (packer or waiting unit), [1] max packer arrival, [2] min / [3] max wait
+  // done, [4] max unpack done, [5] max / [6] sum of a unit's unpack duration (wait done ->
+  // unpack done), [7] units; over all launches since set-up: [8] max / [9] sum of a producer's
+  // carry (march done -> arrival), [10] producers
   unsigned long long* stamps;
 };
 
@@ -288,6 +290,7 @@ __device__ __forceinline__ void gate_unpack(const FusedArgs& a, int X0, int xw, 
     while (wall_clock64() - t0 < G.min_ticks) __builtin_amdgcn_s_sleep(1);
   unsigned long long wdone = 0;
   if (G.stamps && tid == 0) {
+    atomicMin(G.stamps + 0, (unsigned long long)t0);
     wdone = (unsigned long long)wall_clock64();
     atomicMin(G.stamps + 2, wdone);
     atomicMax(G.stamps + 3, wdone);
@@ -364,6 +367,7 @@ __device__ __forceinline__ void gate_carry(const FusedArgs& a, const void* dv, i
   const Geom& g = a.g;
   const V2* d = (const V2*)dv;
   const uint64_t m = a.gate_n + 1;
+  const uint64_t tc0 = wall_clock64();
   const int slot = (int)(m & 1);
   const uint32_t nt = blockDim.x, tid = threadIdx.x;
   __shared__ GatePiece gp[gs::kMaxMsgs];
@@ -436,7 +440,15 @@ __device__ __forceinline__ void gate_carry(const FusedArgs& a, const void* dv, i
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every landing store acknowledged
   __syncthreads();
-  if (tid == 0) gate_arrive(G, m, a.gate_cnt2, true);
+  if (tid == 0) {
+    if (G.stamps) {
+      const unsigned long long dt = (unsigned long long)(wall_clock64() - tc0);
+      atomicMax(G.stamps + 8, dt);
+      atomicAdd(G.stamps + 9, dt);
+      atomicAdd(G.stamps + 10, 1ull);
+    }
+    gate_arrive(G, m, a.gate_cnt2, true);
+  }
 }
 
 // a start-gated unit in the one-unit table: pack (a packer), then wait and unpack (gated)

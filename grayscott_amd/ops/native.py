@@ -315,17 +315,19 @@ class Engine:
 
     def gate_stamps(self):
         """Debug knob gate_stamps: the last gated launch's exchange in µs after its first packer
-        started -- {"packed", "first_wait_done", "last_wait_done", "unpacked", and one unit's
-        unpack: "unit_unpack_max", "unit_unpack_mean"}, or None."""
+        or waiting unit started -- {"packed" (-1: a carried exchange), "first_wait_done",
+        "last_wait_done", "unpacked", one unit's unpack: "unit_unpack_max", "unit_unpack_mean",
+        and over every launch since set-up one producer's carry: "carry_max", "carry_mean"
+        (-1: none)}, or None."""
         if not hasattr(self.lib, "gs_gate_stamps"):
             return None
-        out = (c_double * 6)()
+        out = (c_double * 8)()
         self.lib.gs_gate_stamps.argtypes = [c_void_p, c_int32, POINTER(c_double)]
         self.lib.gs_gate_stamps.restype = c_int
-        if self.lib.gs_gate_stamps(self.h, DTYPE_CODES[self.dtype], out) != 0 or out[0] < 0:
+        if self.lib.gs_gate_stamps(self.h, DTYPE_CODES[self.dtype], out) != 0 or out[1] < 0:
             return None
         return dict(zip(("packed", "first_wait_done", "last_wait_done", "unpacked",
-                         "unit_unpack_max", "unit_unpack_mean"),
+                         "unit_unpack_max", "unit_unpack_mean", "carry_max", "carry_mean"),
                         (round(float(x), 2) for x in out)))
 
     def set_gated(self, on: bool):
