@@ -566,8 +566,11 @@ def run(args) -> int:
                 "dims": dom.dims,
                 "local_extent": dom.proc_sizes,
                 "fuse_steps": sim.depth, "ghost_width": sim.H,
-                "fused_kernel": {str(n): {"tile": c[0] or "default", "sched": c[1]}
+                "fused_kernel": {str(n): {"tile": c[0] or "default", "sched": c[1],
+                                          "ms": round(float(c[2]), 4)}
                                  for n, c in sim.fused_choice().items()},
+                # the timed window's passes (engine.h plan_passes; [] = greedy by fuse_steps)
+                "pass_plan": sim.engine.plan_passes(args.steps),
                 "transport": sim.transport,
                 "overlap": sim.overlapped,
                 "gated": sim.gated,

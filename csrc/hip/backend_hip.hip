@@ -171,7 +171,7 @@ class HipBackend final : public gs::Backend {
   }
 
   bool fused(int src, int dst, int n, int64_t t) override {
-    if (n < 2 || n > 3) return false;
+    if (n < 2 || n > kMaxDepth) return false;
     if (!tuned_[n]) autotune(src, dst, n, t);
     // an explicit gs_fused_select / gs_fused_sched overrides the tuned choice at any time
     const bool pin = fused_pinned();
@@ -369,7 +369,7 @@ class HipBackend final : public gs::Backend {
   }
 
   void prepare_fused(int src, int dst, int n, int64_t t) override {
-    if (n >= 2 && n <= 3 && !tuned_[n]) autotune(src, dst, n, t);
+    if (n >= 2 && n <= kMaxDepth && !tuned_[n]) autotune(src, dst, n, t);
   }
 
   // On-device autotuning of the fused kernel's tile shape and work schedule.  The kernel only
@@ -456,7 +456,10 @@ class HipBackend final : public gs::Backend {
       for (int i = 0; i < nt; ++i)
         if ((sizeof(T) == 4 ? tab[i].f32 : tab[i].f64) && i != dflt && !strstr(tab[i].name, "-abl") &&
             (blk_ok || !gsk::fused_cfg_is_block(i)) &&
-            gsk::block_cfg_fits(i, n, (int)sizeof(V2)) && gsk::fused_cfg_applies(i, g_, n))
+            gsk::block_cfg_fits(i, n, (int)sizeof(V2)) && gsk::fused_cfg_applies(i, g_, n) &&
+            gsk::lr_cfg_fits(i, n) &&
+            // T = 4 runs the LDS-ring shapes only (0 is its default 4x12:1sl, so 29 repeats it)
+            (n < 4 || i == 0 || (gsk::fused_cfg_is_lr(i) && i != 29)))
           cfgs.push_back(i);
     }
     const int nsched = pt.zlen1 > 0 ? 1 : 3;  // two z-runs always use schedule 0
@@ -507,7 +510,7 @@ class HipBackend final : public gs::Backend {
     if (autotune_part(src, dst, n, t, whole, &cfg_[n], &sched_[n], &ms)) tuned_ms_[n] = ms;
   }
 
-  double fused_ms(int n) const override { return n >= 2 && n <= 3 ? tuned_ms_[n] : 0.0; }
+  double fused_ms(int n) const override { return n >= 2 && n <= kMaxDepth ? tuned_ms_[n] : 0.0; }
 
   void fused_choice(int n, int* cfg, int* sched, float* ms) const {
     *cfg = cfg_[n];
@@ -1362,10 +1365,12 @@ class HipBackend final : public gs::Backend {
   std::vector<int> send_peers_, recv_peers_;  // distinct peers (indices into peers_)
   int send_peer_[gs::kMaxMsgs], recv_peer_[gs::kMaxMsgs];
   int64_t send_off_[gs::kMaxMsgs];  // offset of send message i in its peer's landing slot
-  bool tuned_[4] = {false, false, false, false};
-  int cfg_[4] = {-1, -1, -1, -1};
-  int sched_[4] = {-1, -1, -1, -1};
-  float tuned_ms_[4] = {0.f, 0.f, 0.f, 0.f};
+  // per fused depth (T = 4: fp32 whole-interior passes, the LDS-ring shapes)
+  static constexpr int kMaxDepth = sizeof(T) == 4 ? 4 : 3;
+  bool tuned_[5] = {false, false, false, false, false};
+  int cfg_[5] = {-1, -1, -1, -1, -1};
+  int sched_[5] = {-1, -1, -1, -1, -1};
+  float tuned_ms_[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
   std::vector<ShellChoice> shells_;
   std::vector<PartChoice> parts_;
   // gated pass (gate_*)
@@ -1575,7 +1580,7 @@ extern "C" {
 
 // Fused-kernel choice made by the autotuner for depth n: out = {cfg, sched}, ms = timing.
 int gs_fused_choice(gs_engine* e, int32_t n, int32_t dtype, int32_t* out2, float* ms) {
-  if (n < 0 || n > 3) return -1;
+  if (n < 0 || n > 4) return -1;
   try {
     int c = -1, s = -1;
     float t = 0.f;
@@ -1619,13 +1624,21 @@ extern "C" void gs_event_destroy(void* ev) {
 // while the stepping thread enqueues its next launches, and a blocking event wait inside the
 // runtime stalled those (the output step's snapshot call took ~85 us in the loop vs ~25 us
 // alone, scripts/profile_output.py)
+// (bounded: a device copy that never completes is an error after GS_COMM_TIMEOUT, like every
+// other device wait of the runtime -- the output writer thread's wait_fn, csrc/io/bp4.cpp)
 extern "C" int gs_event_sync(void* ev) {
   int sleep_us = 5;
+  const auto t0 = std::chrono::steady_clock::now();
+  const double tmo = gs::comm_timeout_s();
   for (;;) {
     const hipError_t r = hipEventQuery((hipEvent_t)ev);
     if (r == hipSuccess) return 0;
     if (r != hipErrorNotReady) {
       g_gs_err = std::string("event sync: ") + hipGetErrorString(r);
+      return -1;
+    }
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > tmo) {
+      g_gs_err = "event sync: not complete after GS_COMM_TIMEOUT = " + std::to_string(tmo) + " s";
       return -1;
     }
     std::this_thread::sleep_for(std::chrono::microseconds(sleep_us));

@@ -383,9 +383,22 @@ struct FCfg {
   // for.  Bit-identical.
   static constexpr bool NSYNC = (OPT_ & 2) != 0;
   static_assert(!NSYNC || SKEW_, "neighbour sync replaces the skewed pipeline's single barrier");
+  // LDS-resident level-0 ring (OPT bit 2): the level-0 planes stream into an LDS ring of PF + 2
+  // planes by gfx950 LDS-DMA (buffer_load_dwordx4 ... lds, 16 B per lane: one wave instruction
+  // = two 64-pair tile rows), issued PF planes ahead right after the plane's barrier, and the
+  // level-0 update reads its rows, y-neighbours and centre plane back with ds_read_b64.  No
+  // VGPR ring (the register-ring design holds (PF + 2) x ROWS pairs per lane), no level-0 row
+  // exchange, and the prefetch depth costs LDS instead of registers -- what makes T = 4 fit
+  // the 12-wave workgroup's 168-VGPR budget.  Bit-identical to the register ring.
+  static constexpr bool LR = (OPT_ & 4) != 0;
+  static_assert(!LR || (SKEW_ && ROWS_ == 4 && sizeof(T_) == 4 && !NSYNC && !LX),
+                "the LDS ring is built for the skewed fp32 4-row pipeline");
   static_assert(!FOLD_ || (Q32_ && !PERIODIC_ && ROWS_ == 4),
                 "folded strips need Q32, a non-periodic grid and 4-row waves");
-  static constexpr int R = PF + 2;                    // level-0 ring slots
+  static constexpr int R = PF + 2;                    // level-0 ring slots (VGPRs or LDS)
+  static constexpr int XL = LR ? (TL > 1 ? TL - 1 : 1) : TL;  // levels with an xch row exchange
+  // the row-exchange slot of consumer level l (LR: level 0 reads the LDS ring instead)
+  static constexpr int xi(int l) { return LR ? l - 1 : l; }
   // level-l output ring / xch buffers: 2 slots.  Skewed: level l+1 reads level l's outputs of
   // the two previous iterations (input and centre), and the levels run top-down within an
   // iteration, so level l overwrites its p-2 output only after level l+1 has consumed it.
@@ -414,12 +427,21 @@ struct FCfg {
   // single-prefetch KV shapes (4x12:1s: 161 VGPRs at T=3, inside the 168 budget); the 2-deep
   // prefetch shapes would exceed it.  L=512 T=3 random init: 4x12:1s 726k -> 746k MLUPS
   // (profiles/r4_fused_ab.txt).  ABL bit 7 forces it on, bit 8 turns it off (both exact).
-  static constexpr bool PU =
-      NOISE_ && KV && Q32_ && ((ABL_ & 128) != 0 || (PF_ == 1 && (ABL_ & 256) == 0));
+  static constexpr bool PU_ANY =
+      NOISE_ && KV && Q32_ && ((ABL_ & 128) != 0 || ((PF_ == 1 || LR) && (ABL_ & 256) == 0));
+  // ... and where they live: VGPRs, or (PUL: the LDS-ring shapes at T >= 4, whose OUT / A rings
+  // take the registers) an LDS table of 8 words per level, read back per draw by one broadcast
+  // ds_read_b128 + ds_read_b32 (every lane the same address: no bank conflict)
+  static constexpr bool PUL = PU_ANY && LR && TL_ >= 4;
+  static constexpr bool PU = PU_ANY && !PUL;
+  // KVL: the round keys too (the folded T >= 4 LDS-ring shape: its per-lane row store offsets
+  // leave no room for them), 16 words read back per draw by four broadcast ds_read_b128
+  static constexpr bool KVL = false;
   // pipeline-fill level skip (fused_iter FILL periods): its second copy of the unrolled body
   // costs ~16 VGPRs, free only where the budget is 168 or 256 (WPEU 3 / 2); with 128 it spills
   // or halves the occupancy (4x8:1s: -10 % at L=512, profiles/r2_fill_skip.txt)
-  static constexpr bool FILLSKIP = (WPEU == 3 || WPEU == 2) && !(ABL_ & 16);
+  // (not on the folded T >= 4 LDS-ring shape: the second body copy does not fit its registers)
+  static constexpr bool FILLSKIP = (WPEU == 3 || WPEU == 2) && !(ABL_ & 16) && !(LR && FOLD_ && TL_ >= 4);
   // ABL bit 9 (exact): every level's Philox block of the iteration drawn before the workgroup
   // barrier (three independent chains interleaved, overlapping the barrier wait) instead of at
   // the top of each level's branch (4-row tiles, the PU form)
@@ -449,9 +471,9 @@ struct FusedState {
   using V2 = typename C::V2;
   typename C::T ar31;  // dt * noise * 2^-31 held in a VGPR (an SGPR copy spills)
   typename C::V2 kc;   // (dt F, 0) held in VGPRs (the first packed FMA's addend)
-  uint32_t kv[C::KV ? 14 : 1];  // Philox round keys of rounds 4-10 (C::KV)
+  uint32_t kv[(C::KV && !C::KVL) ? 14 : 1];  // Philox round keys of rounds 4-10 (C::KV)
   uint32_t pu[C::PU ? 5 * C::TL : 1];  // step-uniform Philox words per level (C::PU)
-  V2 LD[C::R][C::ROWS];
+  V2 LD[C::LR ? 1 : C::R][C::ROWS];  // (FCfg::LR: unused, the ring lives in LDS)
   V2 OUT[C::NO][C::NS][C::ROWS];
   V2 A[C::TL][C::ROWS];
 };
@@ -464,6 +486,8 @@ struct FusedSeg {
   int voff, svoff, pitchb;
   int srow0, srow1;
   int soff[4];               // FOLD: per-lane store offset of each row (out of range: masked)
+  int srows;                 // FOLD + LR at T >= 4: bit j set = this lane stores row j (offsets
+                             // then rebuilt per store: 4 VGPRs fewer)
   int pzb;                   // bytes per storage plane
   const char* ldp;           // source plane of the next prefetch (p + PF)
   char* stp;                 // destination plane of this iteration's last-level output
@@ -475,7 +499,48 @@ struct FusedSeg {
   int* seq;                  // FCfg::NSYNC: the workgroup's per-wave sequence words (LDS)
   int it;                    // FCfg::NSYNC: pipeline iterations run by this workgroup so far
   bool wait_up, wait_dn;     // FCfg::NSYNC: whether this wave waits for its up / down partner
+  int dvoff;                 // FCfg::LR: this lane's source offset of the wave's first DMA piece
+                             // (the second: + 2 rows)
+  uint32_t rbase;            // FCfg::LR: LDS address of ring slot 0, this wave's first row
+  bool lst;                  // FCfg::LR: this wave stores the last level (its VMEM count)
+  const uint32_t* puw;       // FCfg::PUL: the step-uniform Philox words (LDS, 8 per level)
 };
+
+// gfx950 LDS-DMA of 16 bytes per lane: buffer rsrc r at byte offset voff -> LDS address
+// lds + 16 * lane (one wave instruction moves 1 KiB).  Inline asm rather than the builtin: the
+// compiler orders every later LDS access and barrier behind a builtin DMA with s_waitcnt
+// vmcnt(0), which drains the prefetch each plane; FCfg::LR counts its DMAs itself (lr_wait).
+// M0 is saved and restored around it (the compiler reserves it).
+// soff: a wave-uniform byte offset added to voff (the scalar offset field).
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, int voff, int soff, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %1\n\t"
+      "buffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(lds), "v"(voff), "s"(r), "s"(soff)
+      : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void vmcnt_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt field");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// FCfg::LR: wait until this wave's DMA of the plane consumed next has landed.  Per pipeline
+// iteration a wave issues 2 DMA pieces right after the barrier and then S stores (ROWS when it
+// stores the last level, else 0; constant per wave: the fill periods store to an empty
+// descriptor), so the DMA of plane p (issued PF iterations back) has S + (PF - 1)(2 + S) younger
+// VMEM operations (the segment prologue pads its DMAs with S empty stores to keep the count).
+template <class C>
+__device__ __forceinline__ void lr_wait(const FusedSeg& sg) {
+  constexpr int S = C::ROWS, PF = C::PF;
+  if (sg.lst) vmcnt_wait<S + (PF - 1) * (2 + S)>();
+  else vmcnt_wait<(PF - 1) * 2>();
+}
 
 template <class C>
 __device__ __forceinline__ int64_t gwrap(int64_t v, int64_t L) {
@@ -571,9 +636,24 @@ __device__ __forceinline__ typename C::V2 cell_update(typename C::V2& A, typenam
 // Non-skewed: level l+1 is computed from level l of the SAME iteration (one barrier per level).
 // Skewed: level l+1 consumes level l's output of the PREVIOUS iteration, so every level's
 // input rows are published before a single barrier; level l produces plane p - (2l + 1).
+// FCfg::LR: issue the wave's two DMA pieces of level-0 plane p + PF (rows 4w .. 4w + 3) into ring
+// slot `slot`.  Unconditional (an empty descriptor past the segment): constant VMEM count.
+template <class C>
+__device__ __forceinline__ void lr_dma(FusedSeg& sg, int slot, bool ok) {
+  const __amdgpu_buffer_rsrc_t r = plane_rsrc(sg.ldp, ok ? sg.pzb : 0);
+  constexpr uint32_t kSlot = C::RT * 64 * sizeof(typename C::V2);
+  // (the second piece's offset goes through voffset too: the range check of a raw buffer access
+  // does not include soffset, and a first piece above the plane must not drag a valid second
+  // piece out of range with it)
+  dma16(r, sg.dvoff, 0, sg.rbase + (uint32_t)slot * kSlot);
+  dma16(r, sg.dvoff + 2 * sg.pitchb, 0, sg.rbase + (uint32_t)slot * kSlot + 1024u);
+  sg.ldp += sg.pzb;
+}
+
 template <class C, typename T, int IR, int IS, bool FILL>
 __device__ __forceinline__ void fused_iter(FusedState<C>& S,
                                            typename C::V2 (*xch)[C::NS][C::WAVES][2][64],
+                                           typename C::V2 (*ring)[C::RT][64],
                                            const FusedArgs& a, const FoldCoef<T>& f,
                                            uint64_t seed, FusedSeg& sg) {
   using V2 = typename C::V2;
@@ -582,8 +662,9 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
   const int p = sg.p;
   // prefetch level-0 plane p+PF into the ring slot of plane p-2.  Issued unconditionally
   // (an empty descriptor past the segment) so every iteration has the same VMEM count and
-  // the compiler's s_waitcnt vmcnt(N) can leave the prefetch in flight.
-  {
+  // the compiler's s_waitcnt vmcnt(N) can leave the prefetch in flight.  (FCfg::LR: after the
+  // barrier below, into the LDS ring.)
+  if constexpr (!C::LR) {
     const bool pf_ok = p + C::PF < sg.ldend;
     const __amdgpu_buffer_rsrc_t r =
         plane_rsrc((C::ABL & 2) ? sg.ldp - (int64_t)(p + C::PF + g.H) * sg.pzb : sg.ldp,
@@ -607,12 +688,18 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
   }
   if constexpr (C::SKEW) {
 #pragma unroll
-    for (int l = 0; l < TL; ++l) {
-      const V2* in = l == 0 ? S.LD[IR] : S.OUT[l == 0 ? 0 : l - 1][(IS + NS - 1) % NS];
-      xch[l][IS][sg.wave][0][sg.lane] = in[0];
-      xch[l][IS][sg.wave][1][sg.lane] = in[ROWS - 1];
+    for (int l = C::LR ? 1 : 0; l < TL; ++l) {
+      const V2* in = l == 0 ? S.LD[C::LR ? 0 : IR] : S.OUT[l == 0 ? 0 : l - 1][(IS + NS - 1) % NS];
+      xch[C::xi(l)][IS][sg.wave][0][sg.lane] = in[0];
+      xch[C::xi(l)][IS][sg.wave][1][sg.lane] = in[ROWS - 1];
     }
-    if constexpr (C::NSYNC) {
+    if constexpr (C::LR) {
+      // this wave's DMA of plane p has landed; after the barrier every wave's has, and every
+      // wave is done with plane p - 2's slot, which the DMA of plane p + PF then overwrites
+      lr_wait<C>(sg);
+      __syncthreads();
+      lr_dma<C>(sg, (IR + C::PF) % C::R, p + C::PF < sg.ldend);
+    } else if constexpr (C::NSYNC) {
       // publish this iteration's rows, then wait for the partners' (see FCfg::NSYNC)
       const int it = ++sg.it;
       asm volatile("" ::: "memory");
@@ -638,8 +725,8 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
     // input plane of consumer l and the centre plane one before it
     constexpr int kIn = C::SKEW ? (IS + NS - 1) % NS : IS;
     constexpr int kC = C::SKEW ? (IS + NS - 2) % NS : (IS + NS - 1) % NS;
-    V2* in = l == 0 ? S.LD[IR] : S.OUT[l == 0 ? 0 : l - 1][kIn];
-    V2* Cc = l == 0 ? S.LD[(IR + C::R - 1) % C::R] : S.OUT[l == 0 ? 0 : l - 1][kC];
+    V2* in = l == 0 ? S.LD[C::LR ? 0 : IR] : S.OUT[l == 0 ? 0 : l - 1][kIn];
+    V2* Cc = l == 0 ? S.LD[C::LR ? 0 : (IR + C::R - 1) % C::R] : S.OUT[l == 0 ? 0 : l - 1][kC];
     if constexpr (!C::SKEW) {
       xch[l][IS][sg.wave][0][sg.lane] = in[0];
       xch[l][IS][sg.wave][1][sg.lane] = in[ROWS - 1];
@@ -666,8 +753,27 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
       }
     }
     if (need && !((sg.skip >> l) & 1)) {  // wave-uniform
-      const V2 up = lds_load2(&xch[l][IS][sg.wup][1][sg.lane]);
-      const V2 dn = lds_load2(&xch[l][IS][sg.wdn][0][sg.lane]);
+      V2 up, dn;
+      V2 r0[C::LR ? ROWS : 1], c0[C::LR ? ROWS : 1];
+      if (C::LR && l == 0) {
+        // level 0 from the LDS ring: this plane's rows and the rows next to them (the wrap-around
+        // rows of waves 0 / last are tile-halo rows whose values never reach an output), and
+        // the centre plane before it
+        constexpr int RT = C::RT;
+        const int r = sg.wave * ROWS;
+        up = lds_load2(&ring[IR][(r + RT - 1) % RT][sg.lane]);
+        dn = lds_load2(&ring[IR][(r + ROWS) % RT][sg.lane]);
+#pragma unroll
+        for (int j = 0; j < (C::LR ? ROWS : 1); ++j) {
+          r0[j] = lds_load2(&ring[IR][r + j][sg.lane]);
+          c0[j] = lds_load2(&ring[(IR + C::R - 1) % C::R][r + j][sg.lane]);
+        }
+        in = r0;
+        Cc = c0;
+      } else {
+        up = lds_load2(&xch[C::xi(l)][IS][sg.wup][1][sg.lane]);
+        dn = lds_load2(&xch[C::xi(l)][IS][sg.wdn][0][sg.lane]);
+      }
       V2* xl = (V2*)sg.xl;
       if constexpr (C::LX) {
         // this wave's input rows out to LDS and the x neighbours back (one wave: LDS executes
@@ -698,6 +804,21 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
             const uint32_t qu = (uint32_t)g.Lx * (gy4 + Ly4 * (uint32_t)gz);
             if (C::hoisted(l)) blk = pre[l];
             else if constexpr (C::PU) blk = philox_lane_v(qu + sg.gx32, &S.pu[5 * l], S.kv);
+            else if constexpr (C::PUL) {
+              const gs_u4 w = *(const gs_u4*)__builtin_assume_aligned(sg.puw + 8 * l, 16);
+              const uint32_t u[5] = {w.x, w.y, w.z, w.w, sg.puw[8 * l + 4]};
+              if constexpr (C::KVL) {
+                uint32_t kv[16];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                  const gs_u4 k4 = *(const gs_u4*)__builtin_assume_aligned(sg.puw + 8 * TL + 4 * i, 16);
+                  kv[4 * i] = k4.x; kv[4 * i + 1] = k4.y; kv[4 * i + 2] = k4.z; kv[4 * i + 3] = k4.w;
+                }
+                blk = philox_lane_v(qu + sg.gx32, u, kv);
+              } else {
+                blk = philox_lane_v(qu + sg.gx32, u, S.kv);
+              }
+            }
             else blk = philox_dev<true, C::KV>(qu + sg.gx32, 0u, tstep, seed, S.kv);
           } else {
             const int64_t gyq = gwrap<C>(sg.gy0 + 4 * m, g.Ly);
@@ -730,7 +851,9 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
           const bool xout = sg.gxu < 0 || sg.gxu >= g.Lx;
 #pragma unroll
           for (int j = 0; j < ROWS; ++j) {
-            const int64_t gyj = sg.gy0 + j + (C::FOLD ? sg.gdy : 0);
+            int gdy = C::FOLD ? sg.gdy : 0;
+            if constexpr (C::FOLD && C::LR && TL >= 4) gdy = (sg.srows & 16) ? a.ystep : 0;
+            const int64_t gyj = sg.gy0 + j + gdy;
             if (zout || xout || gyj < 0 || gyj >= g.Ly) res[j] = V2{bu, (T)0};
           }
         }
@@ -742,7 +865,9 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
 #pragma unroll
         for (int j = 0; j < ROWS; ++j) {
           int off;
-          if constexpr (C::FOLD) off = sg.soff[j];  // per lane (a folded pair's halves differ)
+          if constexpr (C::FOLD && C::LR && TL >= 4)
+            off = ((sg.srows >> j) & 1) ? sg.svoff + j * sg.pitchb : (int)0x80000000;
+          else if constexpr (C::FOLD) off = sg.soff[j];  // per lane (a folded pair's halves differ)
           else off = (j >= sg.srow0 && j < sg.srow1) ? sg.svoff + j * sg.pitchb : (int)0x80000000;
           bstore<C::STORE_AUX>(w, off, res[j]);
         }
@@ -756,14 +881,15 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
 template <class C, typename T, int I, bool FILL>
 __device__ __forceinline__ bool fused_period(FusedState<C>& S,
                                              typename C::V2 (*xch)[C::NS][C::WAVES][2][64],
+                                             typename C::V2 (*ring)[C::RT][64],
                                              const FusedArgs& a, const FoldCoef<T>& f,
                                              uint64_t seed, FusedSeg& sg) {
   if constexpr (I == C::PERIOD) {
     return true;
   } else {
-    fused_iter<C, T, I % C::R, I % C::NS, FILL>(S, xch, a, f, seed, sg);
+    fused_iter<C, T, I % C::R, I % C::NS, FILL>(S, xch, ring, a, f, seed, sg);
     if (++sg.p >= sg.pend) return false;
-    return fused_period<C, T, I + 1, FILL>(S, xch, a, f, seed, sg);
+    return fused_period<C, T, I + 1, FILL>(S, xch, ring, a, f, seed, sg);
   }
 }
 
@@ -795,7 +921,9 @@ __device__ __forceinline__ void fused_body(const typename C::V2* __restrict__ s,
                                            const FoldCoef<T>& f, uint64_t seed) {
   constexpr int ROWS = C::ROWS, WAVES = C::WAVES, TL = C::TL;
   static_assert(ROWS % 4 == 0, "rows per wave must hold whole noise quads");
-  __shared__ typename C::V2 xch[TL][C::NS][WAVES][2][64];  // [level][ring][wave][row][lane]
+  __shared__ typename C::V2 xch[C::XL][C::NS][WAVES][2][64];  // [level][ring][wave][row][lane]
+  // FCfg::LR: the level-0 plane ring [slot][tile row][column]
+  __shared__ typename C::V2 ring[C::LR ? C::R : 1][C::LR ? C::RT : 1][64];
   __shared__ typename C::V2 xrow[C::LX ? WAVES * ROWS * 66 : 1];  // FCfg::LX rows, 1-lane pads
   const Geom& g = a.g;
   FusedSeg sg;
@@ -827,6 +955,10 @@ __device__ __forceinline__ void fused_body(const typename C::V2* __restrict__ s,
     if (sg.wave * ROWS > C::need_hi(l) || sg.wave * ROWS + ROWS - 1 < l + 1) sg.skip |= 1 << l;
   sg.pitchb = g.px * (int)sizeof(typename C::V2);
   sg.pzb = (int)(gs::plane_elems(g) * (int64_t)sizeof(typename C::V2));
+  sg.lst = !((sg.skip >> (TL - 1)) & 1);
+  sg.rbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&ring[0][C::LR ? sg.wave * ROWS : 0][0];
+  sg.dvoff = 0;
+  typename C::V2 (*const ringp)[C::RT][64] = (typename C::V2 (*)[C::RT][64])ring;
   const int nzv = a.nzv;
   // Work list of this workgroup: logical units lu = chunk * ntiles + tile, lu0, lu0 + lstep, ...
   // (sched 0: one "unit", the even share [u, uend) of all tile-planes).
@@ -894,13 +1026,36 @@ __device__ __forceinline__ void fused_body(const typename C::V2* __restrict__ s,
       asm volatile("v_mov_b64 %0, %1" : "=v"(S.kc.y) : "s"(k1));
     }
   }
-  if constexpr (C::KV) {
+  if constexpr (C::KV && !C::KVL) {
 #pragma unroll
     for (int r = 3; r < 10; ++r) {
       const uint32_t k0 = (uint32_t)seed + (uint32_t)r * kPhW0;
       const uint32_t k1 = (uint32_t)(seed >> 32) + (uint32_t)r * kPhW1;
       asm volatile("v_mov_b32 %0, %1" : "=v"(S.kv[2 * (r - 3)]) : "s"(k0));
       asm volatile("v_mov_b32 %0, %1" : "=v"(S.kv[2 * (r - 3) + 1]) : "s"(k1));
+    }
+  }
+  __shared__ __attribute__((aligned(16))) uint32_t puw[C::PUL ? 8 * TL + 16 : 4];
+  sg.puw = puw;
+  if constexpr (C::PUL) {
+    // written by wave 0 before the first segment's barrier (FCfg::LR opens every segment with one)
+    if (sg.wave == 0 && sg.lane == 0) {
+#pragma unroll
+      for (int l = 0; l < TL; ++l) {
+        const PhiloxU u = philox_uniform((uint64_t)(a.t + l), seed);
+        puw[8 * l + 0] = u.x1;
+        puw[8 * l + 1] = u.x2;
+        puw[8 * l + 2] = u.x3;
+        puw[8 * l + 3] = u.k3;
+        puw[8 * l + 4] = u.x4;
+      }
+      if constexpr (C::KVL) {
+#pragma unroll
+        for (int r = 3; r < 10; ++r) {
+          puw[8 * TL + 2 * (r - 3)] = (uint32_t)seed + (uint32_t)r * kPhW0;
+          puw[8 * TL + 2 * (r - 3) + 1] = (uint32_t)(seed >> 32) + (uint32_t)r * kPhW1;
+        }
+      }
     }
   }
   if constexpr (C::PU) {
@@ -999,6 +1154,10 @@ __device__ __forceinline__ void fused_body(const typename C::V2* __restrict__ s,
 #pragma unroll
         for (int j = 0; j < ROWS; ++j)
           sg.soff[j] = (xin && j >= r0 && j < r1) ? sg.voff + j * sg.pitchb : (int)0x80000000;
+        sg.srows = 0;
+#pragma unroll
+        for (int j = 0; j < ROWS; ++j) sg.srows |= (xin && j >= r0 && j < r1) ? 1 << j : 0;
+        if (dy) sg.srows |= 16;  // (bit 4: the upper half's y offset, for the edge resets)
       }
       const int yext = WAVES * ROWS + (xw == 32 ? a.ystep : 0);
       sg.edge = a.bcfix &&
@@ -1016,6 +1175,34 @@ __device__ __forceinline__ void fused_body(const typename C::V2* __restrict__ s,
       const int qlast = C::SKEW ? sg.p - (2 * TL - 1) : sg.p - TL;
       sg.ldp = (const char*)s + (int64_t)(sg.p + C::PF + g.H) * sg.pzb;
       sg.stp = (char*)d + (int64_t)(qlast + g.H) * sg.pzb;
+      if constexpr (C::LR) {
+        // the wave's DMA pieces: lane i moves pairs 2(i & 31), +1 of tile row 4w + 2k + i / 32
+        // (folded tiles: image columns >= 32 are the upper y-tile's columns 0..31)
+        const int c = 2 * (sg.lane & 31);
+        const int cx = (C::FOLD && xw == 32) ? (c & 31) : c;
+        const int cdy = (C::FOLD && c >= 32 && live && xw == 32) ? a.ystep : 0;
+        sg.dvoff = ((Y0 + sg.wave * ROWS + (sg.lane >> 5) + cdy + g.H) * g.px + X0 + cx + g.xo) *
+                   (int)sizeof(typename C::V2);
+        // every wave is past the previous segment's ring reads and its own DMAs have landed
+        // (a DMA of the old segment's drain must not land after this segment's prologue)
+        vmcnt_wait<0>();
+        __syncthreads();
+        // prologue: planes p .. p + PF - 1 into slots 0 .. PF - 1, each followed by the S empty
+        // stores a pipeline iteration issues (lr_wait's count)
+        const char* keep = sg.ldp;
+        sg.ldp = (const char*)s + (int64_t)(sg.p + g.H) * sg.pzb;
+#pragma unroll
+        for (int k = 0; k < C::PF; ++k) {
+          lr_dma<C>(sg, k, sg.p + k < sg.ldend);
+          if (sg.lst) {
+            const __amdgpu_buffer_rsrc_t w = plane_rsrc(sg.stp, 0);
+#pragma unroll
+            for (int j = 0; j < ROWS; ++j)
+              bstore<C::STORE_AUX>(w, (int)0x80000000, typename C::V2{(T)0, (T)0});
+          }
+        }
+        sg.ldp = keep;
+      } else {
 #pragma unroll
       for (int k = 0; k < C::PF; ++k) {
         const int pl = (C::ABL & 2) ? 0 : sg.p + k + g.H;
@@ -1025,6 +1212,7 @@ __device__ __forceinline__ void fused_body(const typename C::V2* __restrict__ s,
         for (int j = 0; j < ROWS; ++j)
           S.LD[k][j] = bload(r, sg.voff + j * sg.pitchb, (typename C::V2*)nullptr);
       }
+      }
       // pipeline fill: the first periods skip level work outside the outputs' dependency
       // cone (fused_iter, FILL); every level is needed from iteration 3T-1 (skewed) / 2T on
       bool more = true;
@@ -1033,12 +1221,13 @@ __device__ __forceinline__ void fused_body(const typename C::V2* __restrict__ s,
         constexpr int kFillPeriods = (kFillIters + C::PERIOD - 1) / C::PERIOD;
 #pragma unroll 1
         for (int np = 0; np < kFillPeriods && more; ++np)
-          more = fused_period<C, T, 0, true>(S, xch, a, f, seed, sg);
+          more = fused_period<C, T, 0, true>(S, xch, ringp, a, f, seed, sg);
       }
-      while (more && fused_period<C, T, 0, false>(S, xch, a, f, seed, sg)) {
+      while (more && fused_period<C, T, 0, false>(S, xch, ringp, a, f, seed, sg)) {
       }
     }
   }  // work list
+  if constexpr (C::LR) vmcnt_wait<0>();  // the drain's DMAs land before the wave ends
   if constexpr (GATED == 3) {
     // a pass that carries the next exchange: a producer packs its own outputs that lie in an
     // outgoing message, now final (gate.hpp gate_carry)
@@ -1272,39 +1461,45 @@ inline const FusedCfgEntry* fused_cfg_table(int* n) {
       {"blk8x2w16l", true, false}, // 25  last level in half-quad items
       {"blk4x4w16l", true, false}, // 26  last level in half-quad items
       {"4x12:1sf", true, false},   // 27  the last x strip folded into half-wave tiles (FCfg::FOLD)
+      // the level-0 ring in LDS, filled by LDS-DMA (FCfg::LR); the only shapes with a T = 4 entry
+      {"4x12:2sl", true, false},   // 28  2-plane prefetch
+      {"4x12:1sl", true, false},   // 29  1-plane prefetch (T = 4 default: the ring + 3 levels' xch fit)
+      {"4x12:1sfl", true, false},  // 30  folded last strip
+      {"4x12:3sl", true, false},   // 31  3-plane prefetch (T = 2 only: LDS)
+      {"4x12:2sfl", true, false},  // 32  2-plane prefetch, folded last strip
 #ifdef GS_ABLATION
       // measured and rejected in round 5 (exact; kept for reproduction in the ablation build):
       // fp64 LDS x-sums 4-6 % slower, neighbour-only sync 5-6 % slower (profiles/r5_f64_counters.txt,
       // r5_nsync_rejected.txt)
-      {"4x8:1sx", false, true},    // 28  fp64: x-neighbour sums through LDS (FCfg::LX)
-      {"4x6:2sx", false, true},    // 29  fp64: x-neighbour sums through LDS (FCfg::LX)
-      {"4x8:1x", false, true},     // 30  fp64: x-neighbour sums through LDS, unskewed
-      {"4x12:1sn", true, false},   // 31  neighbour-only LDS sync instead of the barrier (NSYNC)
-      {"4x12:1sfn", true, false},  // 32  folded last strip + neighbour-only sync
-      {"4x12:2sn", true, false},   // 33  2-plane prefetch + neighbour-only sync
-      {"4x8:1sxn", false, true},   // 34  fp64: LDS x-sums + neighbour-only sync
-      {"4x8:1sn", false, true},    // 35  fp64: neighbour-only sync
-      {"4x12:2s-abl1", true, false},  // 36  no barriers
-      {"4x12:2s-abl2", true, false},  // 37  L2-resident loads
-      {"4x12:1s-abl4", true, false},  // 38  Philox keys in VGPRs (exact)
-      {"4x12:2s-abl4", true, false},  // 39  Philox keys in VGPRs (exact)
-      {"4x12:1s-abl8", true, false},  // 40  DPP sums with the s_nop (exact)
-      {"4x12:1s-abl12", true, false}, // 41  abl4 + abl8 (exact)
-      {"4x12:1s-abl16", true, false}, // 42  pipeline fill computes every level (exact)
-      {"4x8:1s-abl16", true, true},   // 43  pipeline fill computes every level (exact)
-      {"4x6:2s-abl16", true, true},   // 44  pipeline fill computes every level (exact)
-      {"4x12:1s-abl32", true, false}, // 45  Philox only on lanes in the x cone (exact)
-      {"4x12:2s-abl64", true, false}, // 46  Philox keys rebuilt on the SALU (exact)
-      {"4x12:1s-abl64", true, false}, // 47  Philox keys rebuilt on the SALU (exact)
-      {"4x12:1s-abl256", true, false}, // 48  step-uniform Philox words on the SALU (exact)
-      {"4x12:1s-abl512", true, false}, // 49  Philox blocks of all levels before the barrier (exact)
-      {"4x12:1s-abl1024", true, false}, // 50  the top level's Philox block before the barrier (exact)
-      {"4x12:1s-abl1536", true, false}, // 51  the top two levels' Philox blocks before the barrier
-      {"4x12:1s-abl2048", true, false}, // 52  non-temporal output stores (exact)
-      {"4x12:1s-abl4096", true, false}, // 53  device-scope (write-through) output stores (exact)
-      {"4x12:1s-abl6144", true, false}, // 54  both (exact)
-      {"4x12:2s-abl128", true, false},  // 55  2-plane prefetch + step-uniform Philox words in VGPRs
-      {"4x12:3s-abl128", true, false},  // 56  3-plane prefetch + step-uniform Philox words in VGPRs
+      {"4x8:1sx", false, true},    // 33  fp64: x-neighbour sums through LDS (FCfg::LX)
+      {"4x6:2sx", false, true},    // 34  fp64: x-neighbour sums through LDS (FCfg::LX)
+      {"4x8:1x", false, true},     // 35  fp64: x-neighbour sums through LDS, unskewed
+      {"4x12:1sn", true, false},   // 36  neighbour-only LDS sync instead of the barrier (NSYNC)
+      {"4x12:1sfn", true, false},  // 37  folded last strip + neighbour-only sync
+      {"4x12:2sn", true, false},   // 38  2-plane prefetch + neighbour-only sync
+      {"4x8:1sxn", false, true},   // 39  fp64: LDS x-sums + neighbour-only sync
+      {"4x8:1sn", false, true},    // 40  fp64: neighbour-only sync
+      {"4x12:2s-abl1", true, false},  // 41  no barriers
+      {"4x12:2s-abl2", true, false},  // 42  L2-resident loads
+      {"4x12:1s-abl4", true, false},  // 43  Philox keys in VGPRs (exact)
+      {"4x12:2s-abl4", true, false},  // 44  Philox keys in VGPRs (exact)
+      {"4x12:1s-abl8", true, false},  // 45  DPP sums with the s_nop (exact)
+      {"4x12:1s-abl12", true, false}, // 46  abl4 + abl8 (exact)
+      {"4x12:1s-abl16", true, false}, // 47  pipeline fill computes every level (exact)
+      {"4x8:1s-abl16", true, true},   // 48  pipeline fill computes every level (exact)
+      {"4x6:2s-abl16", true, true},   // 49  pipeline fill computes every level (exact)
+      {"4x12:1s-abl32", true, false}, // 50  Philox only on lanes in the x cone (exact)
+      {"4x12:2s-abl64", true, false}, // 51  Philox keys rebuilt on the SALU (exact)
+      {"4x12:1s-abl64", true, false}, // 52  Philox keys rebuilt on the SALU (exact)
+      {"4x12:1s-abl256", true, false}, // 53  step-uniform Philox words on the SALU (exact)
+      {"4x12:1s-abl512", true, false}, // 54  Philox blocks of all levels before the barrier (exact)
+      {"4x12:1s-abl1024", true, false}, // 55  the top level's Philox block before the barrier (exact)
+      {"4x12:1s-abl1536", true, false}, // 56  the top two levels' Philox blocks before the barrier
+      {"4x12:1s-abl2048", true, false}, // 57  non-temporal output stores (exact)
+      {"4x12:1s-abl4096", true, false}, // 58  device-scope (write-through) output stores (exact)
+      {"4x12:1s-abl6144", true, false}, // 59  both (exact)
+      {"4x12:2s-abl128", true, false},  // 60  2-plane prefetch + step-uniform Philox words in VGPRs
+      {"4x12:3s-abl128", true, false},  // 61  3-plane prefetch + step-uniform Philox words in VGPRs
 #endif
   };
   *n = (int)(sizeof(t) / sizeof(t[0]));
@@ -1316,8 +1511,9 @@ inline const FusedCfgEntry* fused_cfg_table(int* n) {
 inline bool fused_cfg_applies(int i, const Geom& g, int k) {
   int n = 0;
   const FusedCfgEntry* t = fused_cfg_table(&n);
-  if (i < 0 || i >= n || (strcmp(t[i].name, "4x12:1sf") != 0 && strcmp(t[i].name, "4x12:1sfn") != 0))
-    return true;
+  if (i < 0 || i >= n) return true;
+  const char* colon = strchr(t[i].name, ':');
+  if (!colon || !strchr(colon, 'f')) return true;  // (folded shapes: "<rows>x<waves>:<pf>sf...")
   const int xstep = 64 - 2 * k;
   const int ntx = (g.nx + xstep - 1) / xstep;
   return ntx >= 2 && g.nx - (ntx - 1) * xstep <= 32 - 2 * k;
@@ -1371,9 +1567,43 @@ inline int fused_cfg_env() {
   return v;
 }
 
+// whether an LDS-ring shape (FCfg::LR, 12 waves of 4 rows) fits the CU's 160 KiB at depth tl with
+// a pf-plane prefetch: the ring's pf + 2 planes plus the tl - 1 levels' row exchange (2 slots)
+constexpr bool lr_fits(int tl, int pf) {
+  return ((pf + 2) * 48 * 64 + (tl > 1 ? tl - 1 : 1) * 2 * 12 * 2 * 64) * 8 <= 160 * 1024;
+}
+// the LDS-ring table entries (28 .. 32) as (prefetch, folded)
+constexpr int kLrPF[5] = {2, 1, 1, 3, 2};
+constexpr bool kLrFold[5] = {false, false, true, false, true};
+inline bool fused_cfg_is_lr(int i) { return i >= 28 && i <= 32; }
+inline bool lr_cfg_fits(int i, int tl) { return !fused_cfg_is_lr(i) || lr_fits(tl, kLrPF[i - 28]); }
+
+// one LDS-ring shape: its launch where it fits the LDS at this depth, else false
+template <typename T, int TL, bool PER, bool NZ, bool Q32, int PF, bool FOLD>
+bool run_lr(const void* s, void* d, const FusedArgs& a, const gs::Params& p, hipStream_t st) {
+  if constexpr (sizeof(T) == 4 && lr_fits(TL, PF) && (!FOLD || (Q32 && !PER))) {
+    FusedLaunch<FCfg<T, TL, 4, 12, PF, PER, NZ, true, Q32, 0, FOLD, 4>, T>::run(s, d, a, p, st);
+    return true;
+  } else {
+    return false;
+  }
+}
+
 template <typename T, int TL, bool PER, bool NZ, bool Q32>
 void run_fused_cfg(const void* s, void* d, const FusedArgs& a, const gs::Params& p,
                    hipStream_t st) {
+  // T = 4: the LDS-ring shapes only (the register ring does not fit 168 VGPRs at this depth);
+  // default 4x12:1sl
+  if constexpr (TL == 4) {
+    if constexpr (sizeof(T) == 4 && !PER && NZ && Q32) {
+      switch (a.cfg) {
+        case 30: if (run_lr<T, TL, PER, NZ, Q32, 1, true>(s, d, a, p, st)) return; break;
+        default: break;
+      }
+    }
+    run_lr<T, TL, PER, NZ, Q32, 1, false>(s, d, a, p, st);
+    return;
+  } else {
   // tile variants: non-periodic runs with noise and a 32-bit counter (the tuned production
   // path); everything else runs the default shape
   if constexpr (sizeof(T) == 8 && !PER && NZ && Q32) {
@@ -1384,13 +1614,13 @@ void run_fused_cfg(const void* s, void* d, const FusedArgs& a, const gs::Params&
       case 16: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
       case 17: FusedLaunch<FCfg<T, TL, 4, 4, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
 #ifdef GS_ABLATION
-      case 28: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 0, false, 1>, T>::run(s, d, a, p, st); return;
-      case 29: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 0, false, 1>, T>::run(s, d, a, p, st); return;
-      case 30: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, false, true, 0, false, 1>, T>::run(s, d, a, p, st); return;
-      case 34: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 0, false, 3>, T>::run(s, d, a, p, st); return;
-      case 35: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 0, false, 2>, T>::run(s, d, a, p, st); return;
-      case 43: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
-      case 44: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 33: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 0, false, 1>, T>::run(s, d, a, p, st); return;
+      case 34: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 0, false, 1>, T>::run(s, d, a, p, st); return;
+      case 35: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, false, true, 0, false, 1>, T>::run(s, d, a, p, st); return;
+      case 39: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 0, false, 3>, T>::run(s, d, a, p, st); return;
+      case 40: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 0, false, 2>, T>::run(s, d, a, p, st); return;
+      case 48: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 49: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
 #endif
       default: break;
     }
@@ -1421,31 +1651,36 @@ void run_fused_cfg(const void* s, void* d, const FusedArgs& a, const gs::Params&
       case 25: if (block_supported(a) && run_block<BCfg<T, TL, 8, 2, 16, NZ, true, true>>(s, d, a, p, st)) return; break;
       case 26: if (block_supported(a) && run_block<BCfg<T, TL, 4, 4, 16, NZ, true, true>>(s, d, a, p, st)) return; break;
       case 27: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 0, true>, T>::run(s, d, a, p, st); return;
+      case 28: if (run_lr<T, TL, PER, NZ, Q32, 2, false>(s, d, a, p, st)) return; break;
+      case 29: if (run_lr<T, TL, PER, NZ, Q32, 1, false>(s, d, a, p, st)) return; break;
+      case 30: if (run_lr<T, TL, PER, NZ, Q32, 1, true>(s, d, a, p, st)) return; break;
+      case 31: if (run_lr<T, TL, PER, NZ, Q32, 3, false>(s, d, a, p, st)) return; break;
+      case 32: if (run_lr<T, TL, PER, NZ, Q32, 2, true>(s, d, a, p, st)) return; break;
 #ifdef GS_ABLATION
-      case 31: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 0, false, 2>, T>::run(s, d, a, p, st); return;
-      case 32: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 0, true, 2>, T>::run(s, d, a, p, st); return;
-      case 33: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 0, false, 2>, T>::run(s, d, a, p, st); return;
-      case 36: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 1>, T>::run(s, d, a, p, st); return;
-      case 37: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 2>, T>::run(s, d, a, p, st); return;
-      case 38: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;
-      case 39: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;
-      case 40: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 8>, T>::run(s, d, a, p, st); return;
-      case 41: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 12>, T>::run(s, d, a, p, st); return;
-      case 42: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
-      case 43: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
-      case 44: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
-      case 45: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 32>, T>::run(s, d, a, p, st); return;
-      case 46: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 64>, T>::run(s, d, a, p, st); return;
-      case 47: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 64>, T>::run(s, d, a, p, st); return;
-      case 48: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 256>, T>::run(s, d, a, p, st); return;
-      case 49: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 512>, T>::run(s, d, a, p, st); return;
-      case 50: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 1024>, T>::run(s, d, a, p, st); return;
-      case 51: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 1536>, T>::run(s, d, a, p, st); return;
-      case 52: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 2048>, T>::run(s, d, a, p, st); return;
-      case 53: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 4096>, T>::run(s, d, a, p, st); return;
-      case 54: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 6144>, T>::run(s, d, a, p, st); return;
-      case 55: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, Q32, 128>, T>::run(s, d, a, p, st); return;
-      case 56: FusedLaunch<FCfg<T, TL, 4, 12, 3, PER, NZ, true, Q32, 128>, T>::run(s, d, a, p, st); return;
+      case 36: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 0, false, 2>, T>::run(s, d, a, p, st); return;
+      case 37: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 0, true, 2>, T>::run(s, d, a, p, st); return;
+      case 38: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 0, false, 2>, T>::run(s, d, a, p, st); return;
+      case 41: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 1>, T>::run(s, d, a, p, st); return;
+      case 42: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 2>, T>::run(s, d, a, p, st); return;
+      case 43: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;
+      case 44: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;
+      case 45: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 8>, T>::run(s, d, a, p, st); return;
+      case 46: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 12>, T>::run(s, d, a, p, st); return;
+      case 47: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 48: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 49: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 50: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 32>, T>::run(s, d, a, p, st); return;
+      case 51: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 64>, T>::run(s, d, a, p, st); return;
+      case 52: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 64>, T>::run(s, d, a, p, st); return;
+      case 53: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 256>, T>::run(s, d, a, p, st); return;
+      case 54: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 512>, T>::run(s, d, a, p, st); return;
+      case 55: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 1024>, T>::run(s, d, a, p, st); return;
+      case 56: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 1536>, T>::run(s, d, a, p, st); return;
+      case 57: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 2048>, T>::run(s, d, a, p, st); return;
+      case 58: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 4096>, T>::run(s, d, a, p, st); return;
+      case 59: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 6144>, T>::run(s, d, a, p, st); return;
+      case 60: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, Q32, 128>, T>::run(s, d, a, p, st); return;
+      case 61: FusedLaunch<FCfg<T, TL, 4, 12, 3, PER, NZ, true, Q32, 128>, T>::run(s, d, a, p, st); return;
 #endif
       default: break;  // 0 and 14: the default shape below
     }
@@ -1454,6 +1689,7 @@ void run_fused_cfg(const void* s, void* d, const FusedArgs& a, const gs::Params&
     FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, Q32>, T>::run(s, d, a, p, st);
   } else {
     FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, Q32>, T>::run(s, d, a, p, st);
+  }
   }
 }
 
@@ -1491,8 +1727,10 @@ int fused_gated_occupancy(int cfg, int n, bool pairs) {
   return 0;
 }
 
-inline bool fused_supported(const Geom& g, int n) {
-  if (n < 2 || n > 3 || g.H < n) return false;
+// depths 2..3 on every path; 4 (fp32 only: the LDS-ring shapes) where max_n allows it -- whole-
+// interior launches; the overlapped pass's shell kernels (slab.hpp) stop at 3
+inline bool fused_supported(const Geom& g, int n, int max_n = 3) {
+  if (n < 2 || n > max_n || n > 4 || g.H < n) return false;
   return !(g.periodic && (g.Ly % 4 != 0));  // noise quads would straddle the wrap
 }
 
@@ -1542,8 +1780,8 @@ inline TileGrid fused_tile_grid(const char* name, const Geom& g, int n) {
   const int rows = atoi(name);
   const char* xp = strchr(name, 'x');
   const int waves = xp ? atoi(xp + 1) : 12;
-  const size_t len = strlen(name);
-  return gs::tile_grid(rows, waves, len > 0 && name[len - 1] == 'f', g, n);
+  const char* colon = strchr(name, ':');
+  return gs::tile_grid(rows, waves, colon && strchr(colon, 'f'), g, n);
 }
 
 template <typename T>
@@ -1552,7 +1790,9 @@ bool launch_fused(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, co
                   int sched = -1, int zlo0 = 0, int zlen0 = -1, int zlo1 = 0, int zlen1 = 0,
                   int reserve = 0, int mask = 0, bool allow_block = false,
                   const GateLaunch* gate = nullptr) {
-  if (!fused_supported(g, n)) return false;
+  if (!fused_supported(g, n, sizeof(T) == 4 ? 4 : 3)) return false;
+  if (n == 4 && (zlo0 != 0 || (zlen0 >= 0 && zlen0 != g.nz) || zlen1 > 0 || mask || gate))
+    return false;  // T = 4: whole-interior launches only
   FusedArgs a{};
   a.allow_block = allow_block ? 1 : 0;
   if (zlen0 < 0) zlen0 = g.nz;
@@ -1600,6 +1840,7 @@ bool launch_fused(const typename Vec2<T>::type* s, typename Vec2<T>::type* d, co
   }
   a.bcfix = g.periodic ? 0 : 1;
   if (n == 2) run_fused_tl<T, 2>(s, d, a, p, st);
-  else run_fused_tl<T, 3>(s, d, a, p, st);
+  else if (n == 3) run_fused_tl<T, 3>(s, d, a, p, st);
+  else if constexpr (sizeof(T) == 4) run_fused_tl<T, 4>(s, d, a, p, st);
   return true;
 }

@@ -26,6 +26,7 @@ int gs_set_loopback(gs_engine* e, int32_t on);  // self messages via the device 
 int gs_overlapped(gs_engine* e, int32_t k);      // 1 if a k-step pass overlaps its exchange
 int gs_chained(gs_engine* e, int32_t k);         // 1 if runs of k-step passes are chained on two streams
 int gs_set_gated(gs_engine* e, int32_t on);      // allow (1) / forbid (0) gated passes
+int gs_set_gated_depth(gs_engine* e, int32_t k, int32_t on);  // the same for depth k only
 int gs_gate_plan(const gs::Geom* g, const int32_t* nbr27, int32_t n, int32_t xp, int32_t allpk,
                  int32_t slots, int32_t longest, int32_t rows, int32_t waves, int32_t fold,
                  int32_t pairs, int32_t unpack, int32_t* out, int32_t cap, int32_t* npk,
@@ -33,6 +34,12 @@ int gs_gate_plan(const gs::Geom* g, const int32_t* nbr27, int32_t n, int32_t xp,
 int gs_gated(gs_engine* e, int32_t k);           // 1 if k-step passes carry the exchange in-kernel (gate.hpp)
 int gs_depth(gs_engine* e);                      // steps per pass (fuse, or the measured depth)
 int gs_set_auto_depth(gs_engine* e, int32_t on);  // let prepare() pick the depth (single rank)
+int gs_set_plan(gs_engine* e, int32_t on);        // pass-depth planner on (default) / off (greedy)
+// the pass depths advance(nsteps) would run (engine.h plan_passes; 0: the greedy schedule); at
+// most cap written, the plan's length returned
+int gs_plan_passes(gs_engine* e, int64_t nsteps, int32_t* out, int32_t cap);
+// gs::plan_depths for given pass times cost[0..kmax] (cost[k]: depth k; kmax <= 7)
+int gs_plan_depths(const double* cost, int32_t kmax, int64_t nsteps, int32_t* out, int32_t cap);
 int gs_plan_zplanes(gs_engine* e);               // 1 if halos are whole contiguous z planes
 int gs_fused_runs_raw(gs_engine* e, int32_t k, int32_t zlo0, int32_t zlen0, int32_t zlo1,
                       int32_t zlen1, int32_t mask, int32_t leave_room);  // timing (state unchanged)

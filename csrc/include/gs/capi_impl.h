@@ -73,14 +73,16 @@ int gs_chained(gs_engine* e, int32_t k) { return e->eng->chained(k) ? 1 : 0; }
 int gs_gated(gs_engine* e, int32_t k) { return e->eng->gated(k) ? 1 : 0; }
 
 // The gated pass's unit table (gs/gate_plan.h) for a sub-domain and neighbour set, host only:
-// tests check it on the CPU.  out: up to cap units of 5 int32 (tile, z0, z1, pk, wait); returns
-// the unit count (may exceed cap), -1 on bad arguments.  grid_out (9 int32): the TileGrid.
+// tests check it on the CPU.  out: up to cap units of 6 int32 (tile, z0, z1, pk, wait, prod), so
+// it must hold 6 * cap; returns the unit count (may exceed cap), -1 on bad arguments (including a
+// tile with no output rows: (rows * waves - 2n) & ~3 <= 0).  grid_out (9 int32): the TileGrid.
 // pairs: the two-units-per-workgroup table (xp = the expected exchange X, unpack = U).
 int gs_gate_plan(const gs::Geom* g, const int32_t* nbr27, int32_t n, int32_t xp, int32_t allpk,
                  int32_t slots, int32_t longest, int32_t rows, int32_t waves, int32_t fold,
                  int32_t pairs, int32_t unpack, int32_t* out, int32_t cap, int32_t* npk,
                  int32_t* grid_out) {
   if (!g || !nbr27 || n < 1 || n > g->H || rows < 4 || waves < 1) return -1;
+  if (((rows * waves - 2 * n) & ~3) <= 0) return -1;  // no output rows: tile_grid's ystep <= 0
   const gs::HaloPlan p = gs::make_halo_plan(*g, nbr27, true);
   const gs::TileGrid tg = gs::tile_grid(rows, waves, fold != 0, *g, n);
   int k = 0;
@@ -106,8 +108,29 @@ int gs_set_gated(gs_engine* e, int32_t on) {
   e->eng->set_gated(on != 0);
   return 0;
 }
+int gs_set_gated_depth(gs_engine* e, int32_t k, int32_t on) {
+  e->eng->set_gated_depth(k, on != 0);
+  return 0;
+}
 int gs_depth(gs_engine* e) { return e->eng->depth(); }
 int gs_set_auto_depth(gs_engine* e, int32_t on) { GS_TRY(e->eng->set_auto_depth(on != 0)) }
+int gs_set_plan(gs_engine* e, int32_t on) { GS_TRY(e->eng->set_plan(on != 0)) }
+int gs_plan_depths(const double* cost, int32_t kmax, int64_t nsteps, int32_t* out, int32_t cap) {
+  if (kmax < 2 || kmax > 7) return -1;
+  const std::vector<int> p = gs::plan_depths(cost, kmax, nsteps);
+  for (size_t i = 0; i < p.size() && (int32_t)i < cap; ++i) out[i] = p[i];
+  return (int)p.size();
+}
+int gs_plan_passes(gs_engine* e, int64_t nsteps, int32_t* out, int32_t cap) {
+  try {
+    const std::vector<int> p = e->eng->plan_passes(nsteps);
+    for (size_t i = 0; i < p.size() && (int32_t)i < cap; ++i) out[i] = p[i];
+    return (int)p.size();
+  } catch (const std::exception& ex) {
+    g_gs_err = ex.what();
+    return -1;
+  }
+}
 int gs_plan_zplanes(gs_engine* e) { return e->eng->plan().zplanes; }
 // Timing primitives: one fused k-step update of the given z-runs (store mask: engine.h
 // fused_runs) / of the shell slabs at `sides`, from the current buffer into the other one

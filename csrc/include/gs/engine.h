@@ -13,6 +13,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <algorithm>
 #include <chrono>
 #include <stdexcept>
 #include <string>
@@ -159,6 +160,39 @@ class Backend {
  private:
   std::vector<double> host_us_;
 };
+
+// The cheapest partition of nsteps into passes of depth 2..kmax, given each depth's pass time
+// cost[k] (all > 0, else an empty plan), deepest passes first: an exact dynamic programme over the
+// last kPlanTail steps, before them passes of the depth with the lowest time per step.  nsteps = 1
+// is a lone single step (depth 1).  (Engine::plan_passes; tests/test_planner.py.)
+constexpr int64_t kPlanTail = 240;
+inline std::vector<int> plan_depths(const double* cost, int kmax, int64_t nsteps) {
+  std::vector<int> out;
+  if (nsteps < 1 || kmax < 2) return out;
+  int dbest = 0;
+  for (int k = 2; k <= kmax; ++k) {
+    if (!(cost[k] > 0.0)) return out;
+    if (dbest == 0 || cost[k] / k < cost[dbest] / dbest) dbest = k;
+  }
+  const int64_t head = nsteps > kPlanTail ? (nsteps - kPlanTail) / dbest : 0;
+  const int tail = (int)(nsteps - head * dbest);
+  std::vector<double> best((size_t)tail + 1, 1e300);
+  std::vector<int> how((size_t)tail + 1, 0);
+  best[0] = 0.0;
+  for (int m = 2; m <= tail; ++m)
+    for (int k = kmax; k >= 2; --k)  // ties: the deeper pass (fewer launches)
+      if (k <= m && best[(size_t)(m - k)] + cost[k] < best[(size_t)m] * (1.0 - 1e-12)) {
+        best[(size_t)m] = best[(size_t)(m - k)] + cost[k];
+        how[(size_t)m] = k;
+      }
+  out.assign((size_t)head, dbest);
+  std::vector<int> t;
+  for (int m = tail; m >= 2; m -= how[(size_t)m]) t.push_back(how[(size_t)m]);
+  if (tail == 1) t.push_back(1);
+  std::sort(t.begin(), t.end(), [](int x, int y) { return x > y; });
+  out.insert(out.end(), t.begin(), t.end());
+  return out;
+}
 
 struct EngineConfig {
   Geom g;
@@ -418,13 +452,23 @@ class Engine {
   // (gate.hpp; the IPC transport).  Taken before the stream-overlapped modes; the debug knob
   // gated = 0 (tests, A/B) or overlap off disable it.
   bool gated(int k) const {
-    return gate_ && overlap_ != 0 && cfg_.use_fused && k > 1 && has_remote_ && tfn_ == nullptr &&
-           be_->gated_supported(k);
+    return gate_ && overlap_ != 0 && cfg_.use_fused && k > 1 && k < 32 &&
+           ((gate_depths_ >> k) & 1) && has_remote_ && tfn_ == nullptr && be_->gated_supported(k);
   }
 
   // gated passes off for this engine (the ranks of a job agree: either every rank's passes
   // carry the exchange in-kernel or none does -- models/grayscott.py)
   void set_gated(bool on) { gate_ = on && debug_knobs().gated != 0; }
+  // gated passes of depth k only (off: that depth's passes -- prepare()'s tuning of it, a
+  // remainder pass -- take the stream-overlapped or plain path).  The ranks agree per depth:
+  // gated_supported(k) depends on per-rank state (gate_fits, the per-depth occupancy, shared
+  // landing slots), and a rank that tunes or runs a gated depth its peers do not waits for
+  // exchanges that never come (models/grayscott.py _agree_gated_depths).
+  void set_gated_depth(int k, bool on) {
+    if (k < 0 || k >= 32) return;
+    if (on) gate_depths_ |= (1u << k);
+    else gate_depths_ &= ~(1u << k);
+  }
 
   // whether full-depth passes run as a chain on two streams (advance_chained): any device
   // transport (RCCL in place or packed, IPC peer writes) -- a host callback serialises anyway
@@ -441,8 +485,36 @@ class Engine {
     if (!on) depth_ = 0;
   }
 
+  // Pass-depth plan of one advance() on a single rank (no halo exchange to amortise): the
+  // partition of nsteps into passes of depth 2..fuse with the lowest summed tuned pass time
+  // (Backend::fused_ms, timed by prepare() on the live state), deepest passes first.  The greedy
+  // min(nsteps, depth) schedule ends a 20-step window at depth 3 with a depth-2 pass for the
+  // last two steps, which moves as many HBM bytes as a full pass; here every depth's measured
+  // cost decides (20 = 6 x 3 + 2, 4 x 3 + 2 x 4 or 5 x 4).  Exact dynamic programme over the last
+  // kPlanTail steps; before that, passes of the depth with the lowest time per step.  Empty when
+  // the depths are not all timed (tuning off, a pinned configuration): the greedy schedule then.
+  std::vector<int> plan_passes(int64_t nsteps) const {
+    if (!planner_ || !auto_depth_ || has_remote_ || !cfg_.use_fused || cfg_.fuse < 3 || nsteps < 2)
+      return {};
+    double cost[8] = {0.0};
+    const int kmax = cfg_.fuse < 7 ? cfg_.fuse : 7;
+    for (int k = 2; k <= kmax; ++k) cost[k] = be_->fused_ms(k);
+    return plan_depths(cost, kmax, nsteps);
+  }
+  // planner off (tests, A/B): the greedy min(nsteps, depth) schedule
+  void set_plan(bool on) { planner_ = on; }
+
   void advance(int64_t nsteps) {
-    const int kmax = depth();
+    const std::vector<int> plan = plan_passes(nsteps);
+    if (!plan.empty()) {
+      for (int k : plan) advance_depth(k, k);
+      return;
+    }
+    advance_depth(nsteps, depth());
+  }
+
+ private:
+  void advance_depth(int64_t nsteps, const int kmax) {
     while (nsteps > 0) {
       const int k = (int)(nsteps < kmax ? nsteps : kmax);
       const int oth = 1 - cur_;
@@ -649,6 +721,8 @@ class Engine {
   bool chain_ = debug_knobs().overlap_chain != 0;
   // debug knob gated = 0 (tests, A/B): no gated passes (gs/debug.h)
   bool gate_ = debug_knobs().gated != 0;
+  uint32_t gate_depths_ = 0xffffffffu;  // set_gated_depth
+  bool planner_ = true;  // plan_passes (set_plan)
   enum { kNone, kUnpack, kCallback };
   int xpending_ = kNone;
   int cur_ = 0;

@@ -28,7 +28,9 @@
 #include <cmath>
 #include <condition_variable>
 #include <deque>
+#include <chrono>
 #include <map>
+#include <set>
 #include <mutex>
 #include <thread>
 #include <limits>
@@ -162,6 +164,7 @@ struct Async {
   std::condition_variable cv, done;
   std::deque<AsyncJob> q;
   std::map<int64_t, AsyncResult> results;
+  std::set<int64_t> taken;  // tickets whose result was returned (a second call is an error)
   int64_t next = 0;
   bool stop = false;
   std::string last;  // the blob of the last bp4_async_result (valid until the next call)
@@ -796,7 +799,10 @@ static void async_loop(Writer* w) {
     }
     AsyncResult r{0, {}};
     if (j.wait_fn && j.wait_fn(j.wait_arg) != 0) {
-      r = {-1, "waiting for the step's device copy failed"};
+      // (libgs_hip's gs_event_sync: a device error, or no completion within GS_COMM_TIMEOUT)
+      r = {-1, "output step " + std::to_string(j.step) +
+                   ": waiting for its device copy failed (a device error, or the copy did not "
+                   "complete within GS_COMM_TIMEOUT)"};
     } else if (bp4_write_step_uv(w, j.var_step, j.step, j.var_u, j.u, j.var_v, j.v, j.part,
                                  j.nmm) != 0) {
       r = {-1, g_err};
@@ -844,9 +850,27 @@ int bp4_async_result(void* h, int64_t ticket, const char** out, int64_t* n) {
     return -1;
   }
   std::unique_lock<std::mutex> lk(a->mu);
-  a->done.wait(lk, [&] { return a->results.count(ticket) != 0; });
+  if (ticket < 0 || ticket >= a->next || a->taken.count(ticket)) {
+    g_err = "bp4_async_result: unknown or already consumed ticket " + std::to_string(ticket);
+    return -1;
+  }
+  // bounded like every other blocking wait of the runtime (GS_COMM_TIMEOUT, default 900 s): the
+  // writer thread's own waits are bounded too, so only a wedged file system can reach this
+  const char* e = getenv("GS_COMM_TIMEOUT");
+  const double tmo = (e && atof(e) > 0.0) ? atof(e) : 900.0;
+  // (a system_clock deadline: the steady_clock form lowers to pthread_cond_clockwait, which the
+  // toolchain's ThreadSanitizer does not intercept -- make tsan)
+  const auto until = std::chrono::system_clock::now() +
+                     std::chrono::duration_cast<std::chrono::system_clock::duration>(
+                         std::chrono::duration<double>(tmo + 60.0));
+  if (!a->done.wait_until(lk, until, [&] { return a->results.count(ticket) != 0; })) {
+    g_err = "bp4_async_result: output step still not written after " + std::to_string(tmo + 60.0) +
+            " s";
+    return -1;
+  }
   AsyncResult r = std::move(a->results[ticket]);
   a->results.erase(ticket);
+  a->taken.insert(ticket);
   lk.unlock();
   if (r.rc != 0) {
     g_err = r.blob_or_error;

@@ -46,10 +46,11 @@ def default_fuse(backend: str, domain: CartDomain, dtype: str = "float32") -> in
     # profiles/r3_f64_depth.txt; round 1 measured the opposite, profiles/r1_tune_f64.txt).
     nx, ny, nz = domain.proc_sizes
     if not any(r >= 0 and r != domain.rank for i, r in enumerate(domain.nbr27) if i != 13):
-        # no halo exchange to amortise: H = 3 ghost layers, and prepare() runs the depth (2 or
-        # 3) with the lower measured kernel time per step (engine.h depth()) -- the block
+        # no halo exchange to amortise: H = 3 ghost layers (fp32: 4, the LDS-ring kernel's T = 4
+        # entry), prepare() times every depth and each iterate(n) runs the partition of n into
+        # passes with the lowest summed measured time (engine.h plan_passes) -- the block
         # kernel (csrc/hip/block.hpp) moved the small-grid crossover
-        return max(1, min(3, nx, ny, nz))
+        return max(1, min(4 if dtype == "float32" else 3, nx, ny, nz))
     t = 2 if min(nx, ny) < 160 else 3
     return max(1, min(t, nx, ny, nz))
 
@@ -72,6 +73,26 @@ def critical_path(ph: dict, xch: float, per_pass: dict, chained: bool) -> float:
             return max(inner, xch + shell) + bc
         return max(inner, xch) + shell + bc
     return xch + ph.get("fused", 0.0) + ph.get("step", 0.0) + bc
+
+
+def _agree_gated_depths(engine, ctx, fuse: int) -> dict:
+    """Gated passes (csrc/hip/gate.hpp) per depth on every rank or on none.  Every depth 2..fuse
+    can run gated -- prepare() tunes each, and a planned or remainder pass of any depth takes the
+    gated path where gated(k) holds -- and gated_supported(k) depends on per-rank state (the
+    sub-domain's planes, the per-depth occupancy, shared landing slots).  One allreduce of the
+    per-depth mask (min over ranks); the depths some rank cannot run gated are switched off on
+    every rank (engine.h set_gated_depth).  Returns {depth: agreed}."""
+    ks = list(range(2, max(2, int(fuse)) + 1))
+    mine = [1.0 if engine.gated(k) else 0.0 for k in ks]
+    agreed = ctx.allreduce_array(mine, "min")
+    out = {}
+    for k, a in zip(ks, agreed):
+        on = a > 0
+        if not on:
+            engine.set_gated_depth(k, False)
+        out[k] = on
+    return out
+
 
 class GrayScott:
     """One rank's Gray-Scott state and stepping engine."""
@@ -211,9 +232,7 @@ class GrayScott:
             # run them (too few planes, a peer it cannot map) keeps the stream-overlapped passes,
             # and so must every peer -- the tuning passes and exchange counts must match
             if self.ctx.is_distributed:
-                g = self.engine.gated(self.engine.depth())
-                if self.ctx.allreduce(1.0 if g else 0.0, "min") <= 0:
-                    self.engine.set_gated(False)
+                _agree_gated_depths(self.engine, self.ctx, self.fuse)
         elif kind in ("torch", "host"):
             stage = kind == "host" and self.backend == "hip"
             group = self.ctx.nccl_group() if (self.backend == "hip" and not stage) else None

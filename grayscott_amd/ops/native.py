@@ -235,6 +235,22 @@ def gate_plan(g: Geom, nbr27, n: int, xp: int = 0, allpk: bool = False, slots: i
     return units, int(npk.value), dict(zip(keys, list(grid)))
 
 
+def plan_depths(cost: dict, nsteps: int) -> list:
+    """gs::plan_depths (engine.h): the cheapest partition of ``nsteps`` into fused passes of
+    depth 2..max(cost), given each depth's pass time ``cost[k]``; deepest passes first."""
+    lib = load("core")
+    kmax = max(cost)
+    arr = (c_double * 8)(*[float(cost.get(k, 0.0)) for k in range(8)])
+    lib.gs_plan_depths.argtypes = [POINTER(c_double), c_int32, c_int64, POINTER(c_int32), c_int32]
+    lib.gs_plan_depths.restype = c_int
+    cap = 1 << 16
+    out = (c_int32 * cap)()
+    n = lib.gs_plan_depths(arr, int(kmax), int(nsteps), out, cap)
+    if n < 0:
+        raise ValueError("plan_depths: depths must be 2..7")
+    return [int(out[i]) for i in range(min(n, cap))]
+
+
 def noise_block(gx, gy, gz4, Lx, Ly, step, seed):
     out = (c_uint32 * 4)()
     load("core").gs_noise_block(gx, gy, gz4, Lx, Ly, step, seed, out)
@@ -334,6 +350,12 @@ class Engine:
         """Allow / forbid gated passes on this engine (the job's ranks agree on it)."""
         self._chk(self.lib.gs_set_gated(self.h, 1 if on else 0), "set_gated")
 
+    def set_gated_depth(self, k: int, on: bool):
+        """Allow / forbid gated passes of depth k only (the ranks agree per depth)."""
+        self.lib.gs_set_gated_depth.argtypes = [c_void_p, c_int32, c_int32]
+        self.lib.gs_set_gated_depth.restype = c_int
+        self._chk(self.lib.gs_set_gated_depth(self.h, int(k), 1 if on else 0), "set_gated_depth")
+
     def gate_info(self, k: int):
         """{"xp", "units" (workgroups), "packers", "ms", "pairs_unpack", "carried"} of the tuned
         gated pass of depth k (HIP only; pairs_unpack: the pairs table's U, None for a one-unit
@@ -358,6 +380,24 @@ class Engine:
     def depth(self) -> int:
         """Steps per pass: the fuse depth, or the cheaper one measured by prepare()."""
         return int(self.lib.gs_depth(self.h))
+
+    def set_plan(self, on: bool):
+        """Pass-depth planner (engine.h plan_passes) on (default) or off (greedy schedule)."""
+        self.lib.gs_set_plan.argtypes = [c_void_p, c_int32]
+        self.lib.gs_set_plan.restype = c_int
+        self._chk(self.lib.gs_set_plan(self.h, 1 if on else 0), "set_plan")
+
+    def plan_passes(self, nsteps: int) -> list:
+        """The pass depths advance(nsteps) runs ([] = the greedy min(nsteps, depth) schedule:
+        multi-rank, an explicit fuse, or untimed depths)."""
+        self.lib.gs_plan_passes.argtypes = [c_void_p, c_int64, POINTER(c_int32), c_int32]
+        self.lib.gs_plan_passes.restype = c_int
+        cap = 4096
+        out = (c_int32 * cap)()
+        n = self.lib.gs_plan_passes(self.h, int(nsteps), out, cap)
+        if n < 0:
+            self._chk(n, "plan_passes")
+        return [int(out[i]) for i in range(min(n, cap))]
 
     def advance(self, n: int):
         self._chk(self.lib.gs_advance(self.h, int(n)), "advance")

@@ -172,12 +172,13 @@ def test_random_init_is_decomposition_invariant(world, L):
 
 def test_default_fuse_policy():
     """Steps per pass when fuse_steps = 0 (models/grayscott.py default_fuse): one rank without
-    neighbours gets 3 ghost layers and lets the engine measure the depth; with neighbours the
+    neighbours gets 4 ghost layers in fp32 (3 in fp64: the T = 4 entry is the fp32 LDS-ring
+    kernel) and lets the engine measure the depths and plan the passes; with neighbours the
     depth follows the plane size (T=3 from 160^2 x-y planes, fp32 and fp64 alike since round 3,
     profiles/r3_f64_depth.txt); the CPU backend steps one at a time."""
     from grayscott_amd.models.grayscott import default_fuse
 
-    assert default_fuse("hip", init_domain(64, 1, 0)) == 3
+    assert default_fuse("hip", init_domain(64, 1, 0)) == 4
     assert default_fuse("hip", init_domain(64, 1, 0), "float64") == 3
     assert default_fuse("hip", init_domain(2, 1, 0)) == 2  # capped by the sub-domain extent
     big = init_domain(512, 8, 0, dims=[2, 2, 2])

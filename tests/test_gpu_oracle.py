@@ -80,6 +80,46 @@ def test_pinned_tile_l512_vs_torch_oracle():
     assert err < TOL, err
 
 
+@pytest.mark.parametrize("cfg,fuse,L,steps", [
+    ("4x12:1sl", 4, 200, 8),    # T = 4, LDS-ring level-0 planes (FCfg::LR), edge tiles in x and y
+    ("4x12:1sfl", 4, 512, 8),   # T = 4 folded last strip: the shape the autotuner picks at L=512
+    ("4x12:2sl", 3, 256, 9),    # LDS ring at T = 3 with a 2-plane DMA prefetch
+    ("4x12:3sl", 2, 200, 8),    # LDS ring at T = 2 with a 3-plane DMA prefetch
+    ("4x12:1sfl", 2, 256, 8)])  # folded LDS ring at T = 2 (ghost rows above the first tile)
+def test_lds_ring_and_t4_vs_torch_oracle(cfg, fuse, L, steps):
+    """The gfx950 LDS-DMA ring shapes, T = 4 included (csrc/hip/fused.hpp FCfg::LR), pinned."""
+    u, v, choice, depth = _kernel_run(L, fuse, steps, cfg=cfg, sched=2)
+    assert depth == fuse
+    err = _err((u, v), _oracle(L, steps))
+    print(f"L={L} T={fuse} {cfg} max|d| {err}")
+    assert err < TOL, err
+
+
+def test_planned_driver_window_vs_torch_oracle():
+    """The driver's window (bench.py --steps 20) through the pass-depth planner: the default fp32
+    single-rank set-up (4 ghost layers, every depth timed), whatever partition of the 20 steps it
+    plans (engine.h plan_passes; round 6: 4 + 4 + 3 + 3 + 3 + 3), against the oracle at L=512."""
+    from grayscott_amd.ops import native
+    L, steps = 512, 20
+    s = Settings(L=L, precision="Float32", noise=0.1, backend="AMDGPU", seed=2024, **PHYS)
+    sim = GrayScott(s, init_domain(L, 1, 0))
+    try:
+        sim.init_fields()
+        assert sim.H == 4
+        plan = sim.engine.plan_passes(steps)
+        sim.randomize_fields(seed=7)
+        sim.iterate(steps)
+        u, v = sim.get_fields_device()
+        torch.cuda.synchronize()
+        choice = sim.fused_choice()
+    finally:
+        sim.close()
+    assert sum(plan) == steps and all(2 <= k <= 4 for k in plan), plan
+    err = _err((u, v), _oracle(L, steps))
+    print("planned", plan, choice, "max|d|", err)
+    assert err < TOL, (err, plan)
+
+
 @pytest.mark.parametrize("cfg,fuse", [("blk8x2w16l", 3), ("blk4x4w8", 2), (None, 3)])
 def test_block_kernel_l64_vs_torch_oracle(cfg, fuse):
     """k_block at the reference example's size (None: the autotuner's pick among all shapes)."""
