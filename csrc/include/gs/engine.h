@@ -328,8 +328,9 @@ class Engine {
       }
       // nothing timed (GS_AUTOTUNE=0 or a pinned configuration): the plane-size rule measured
       // with the default tile -- T=2 below 160^2 x-y planes (L=64: 54k vs 42k MLUPS at T=3,
-      // profiles/r2_fuse_small.txt), else the full depth
-      if (best == 0.0) depth_ = (cfg_.g.nx < 160 || cfg_.g.ny < 160) ? 2 : 0;
+      // profiles/r2_fuse_small.txt), else the full depth up to T=3 (the untuned T=4 tile is the
+      // unfolded one, 10 % under T=3 at L=512: profiles/r6_t4.txt)
+      if (best == 0.0) depth_ = (cfg_.g.nx < 160 || cfg_.g.ny < 160) ? 2 : (cfg_.fuse > 3 ? 3 : 0);
     }
     // the timing runs scribbled over the other buffer: restore the reference's zeroed
     // u_temp/v_temp (ghosts included) so the ghost-parity bookkeeping stays exact
