@@ -433,7 +433,21 @@ def run(args) -> int:
     dims = choose_dims(args.L, ctx.world_size, args.decomposition, backend)
     _PROGRESS["phase"] = "data-path tuning"
     tuning = None
+    link = None
     t_tune = time.perf_counter()
+    if ctx.world_size > 1 and backend == "hip" and os.environ.get("GS_LINK_PROBE", "1") != "0":
+        # every pair of ranks measures its own link (IPC peer stores and RCCL send / receive at
+        # the candidates' message sizes) before anything is timed: reported as link_probe, and
+        # the tuner's model skips the candidates it says lose by > 20 % (parallel/linkprobe.py)
+        _PROGRESS["phase"] = "link probe"
+        from grayscott_amd.parallel.linkprobe import probe_links
+        link = probe_links(ctx, log=lambda m: print(f"bench.py: {m}", file=sys.stderr,
+                                                     flush=True))
+        if link and link.get("rccl_failed"):
+            # the engines' "auto" transport chain starts after RCCL (agreed: same dict everywhere)
+            from grayscott_amd.models import grayscott as _gsm
+            _gsm._RCCL_FAILED[0] = True
+        _PROGRESS["phase"] = "data-path tuning"
     if ctx.world_size > 1:
         # Verify every candidate multi-rank data path against the golden model, then time a
         # short run of each on this problem and keep the fastest (parallel/autotune.py): the
@@ -445,7 +459,7 @@ def run(args) -> int:
         log = (lambda m: print(f"bench.py: {m}", file=sys.stderr, flush=True))
         tuning = tune_data_path(settings, ctx, args.L, backend, cands=cands, log=log,
                                 budget_s=args.tune_budget,
-                                on_row=_progress_row if ctx.rank == 0 else None)
+                                on_row=_progress_row if ctx.rank == 0 else None, link=link)
         dims = tuning["dims"]
         settings.fuse_steps = tuning["fuse"]
         settings.transport, settings.overlap = tuning["transport"], tuning["overlap"]
@@ -586,6 +600,7 @@ def run(args) -> int:
             "tuning_s": round(tuning_s, 2),
             "wall_s": round(time.perf_counter() - T_START, 2),
             "data_path_tuning": tuning and tuning["table"],
+            "link_probe": link,
             "reference_grid": ref_grid,
             "check": {"mean_u": stats["mean_u"], "mean_v": stats["mean_v"],
                       "finite": all(map(lambda x: x == x, stats.values())), **check},

@@ -1680,3 +1680,4 @@ extern "C" const char* gs_fused_cfg_name(int32_t index) {
 // index of a fused-kernel configuration name in this build (-1: unknown, e.g. an ablation
 // variant in the production library)
 extern "C" int gs_fused_cfg_lookup(const char* name) { return gsk::fused_cfg_lookup(name); }
+#include "probe.hpp"

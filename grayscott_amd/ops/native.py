@@ -11,8 +11,8 @@ from __future__ import annotations
 import ctypes
 import os
 import threading
-from ctypes import (CFUNCTYPE, POINTER, Structure, c_char_p, c_double, c_int, c_int32, c_int64,
-                    c_uint32, c_uint64, c_void_p)
+from ctypes import (CFUNCTYPE, POINTER, Structure, byref, c_char_p, c_double, c_int, c_int32,
+                    c_int64, c_uint32, c_uint64, c_void_p)
 from typing import Optional
 
 _LIB_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_lib")
@@ -715,3 +715,61 @@ def fused_cfg_name(index: int) -> str:
     lib.gs_fused_cfg_name.restype = c_char_p
     r = lib.gs_fused_cfg_name(int(index))
     return r.decode() if r is not None else f"#{index}"
+
+
+class LinkProbe:
+    """The link probe's device buffers (csrc/hip/probe.hpp): IPC peer-store puts and RCCL
+    send / receive pairs, timed on the device.  ``nbytes``: the largest message it times."""
+
+    def __init__(self, nbytes: int):
+        lib = self.lib = load("hip")
+        lib.gs_probe_create.argtypes = [ctypes.c_int64]
+        lib.gs_probe_create.restype = c_void_p
+        lib.gs_probe_destroy.argtypes = [c_void_p]
+        lib.gs_probe_export.argtypes = [c_void_p, ctypes.c_char_p]
+        lib.gs_probe_export.restype = c_int
+        lib.gs_probe_ipc.argtypes = [c_void_p, ctypes.c_char_p, ctypes.c_int64, c_int32,
+                                     POINTER(c_double)]
+        lib.gs_probe_ipc.restype = c_int
+        lib.gs_probe_rccl_init.argtypes = [c_void_p, ctypes.c_char_p, c_int32, c_int32]
+        lib.gs_probe_rccl_init.restype = c_int
+        lib.gs_probe_rccl.argtypes = [c_void_p, c_int32, ctypes.c_int64, c_int32,
+                                      POINTER(c_double)]
+        lib.gs_probe_rccl.restype = c_int
+        self.h = lib.gs_probe_create(int(nbytes))
+        if not self.h:
+            raise RuntimeError(f"link probe: {last_error(lib)}")
+
+    def export(self) -> bytes:
+        buf = ctypes.create_string_buffer(512)
+        n = self.lib.gs_probe_export(self.h, buf)
+        if n < 0:
+            raise RuntimeError(f"link probe export: {last_error(self.lib)}")
+        return buf.raw[:n]
+
+    def ipc_us(self, peer_export: bytes, nbytes: int, reps: int = 5) -> float:
+        out = c_double()
+        if self.lib.gs_probe_ipc(self.h, peer_export, int(nbytes), int(reps), byref(out)) != 0:
+            raise RuntimeError(last_error(self.lib))
+        return float(out.value)
+
+    def rccl_init(self, uid: bytes, nranks: int, rank: int) -> None:
+        if self.lib.gs_probe_rccl_init(self.h, uid, int(nranks), int(rank)) != 0:
+            raise RuntimeError(last_error(self.lib))
+
+    def rccl_us(self, peer: int, nbytes: int, reps: int = 5) -> float:
+        out = c_double()
+        if self.lib.gs_probe_rccl(self.h, int(peer), int(nbytes), int(reps), byref(out)) != 0:
+            raise RuntimeError(last_error(self.lib))
+        return float(out.value)
+
+    def close(self) -> None:
+        h, self.h = getattr(self, "h", None), None
+        if h:
+            self.lib.gs_probe_destroy(h)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # pragma: no cover - interpreter teardown
+            pass

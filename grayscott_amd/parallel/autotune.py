@@ -124,10 +124,75 @@ def candidates(L: int, nprocs: int, backend: str) -> List[Tuple]:
     return out
 
 
+# A candidate the model says loses by more than this factor is not timed (link-probe pruning)
+MODEL_PRUNE = 1.20
+# Overlapped passes: the split launches and the face-slab shell cost about this share of a pass
+# on top of max(inner update, exchange) (profiles/r3_overlap_split.txt: 11-28 us of ~560 us)
+OVERLAP_COST = 0.05
+
+
+def pass_messages(dom, H: int) -> List[int]:
+    """Cells this rank sends to each neighbour per pass of depth ``H``: a face H x n x n, an edge
+    H x H x n, a corner H^3 -- and on z slabs (process grid 1 x 1 x N) whole storage planes,
+    x / y ghosts included (the in-place plane halos, engine.h halo plan)."""
+    nx, ny, nz = dom.proc_sizes
+    zslab = dom.dims[0] == 1 and dom.dims[1] == 1
+    out = []
+    for i, r in enumerate(dom.nbr27):
+        if i == 13 or r < 0 or r == dom.rank:
+            continue
+        dx, dy, dz = i // 9 - 1, (i // 3) % 3 - 1, i % 3 - 1
+        if zslab:
+            out.append(H * (nx + 2 * H) * (ny + 2 * H))
+            continue
+        ex = H if dx else nx
+        ey = H if dy else ny
+        ez = H if dz else nz
+        out.append(ex * ey * ez)
+    return out
+
+
+def model_step_ms(L: int, nprocs: int, dims, fuse: int, overlap: str, transport: str,
+                  link: Optional[Dict], comp_step_ms: float, pair_bytes: int = 8) -> Optional[float]:
+    """Modelled ms per step of a candidate: every rank's pass is its update (``fuse`` steps of
+    ``comp_step_ms``, the same local volume on every candidate) plus its exchange -- the slowest
+    of its neighbour messages over the slowest probed link of ``transport`` (xGMI links are
+    point to point: the messages to different neighbours move at once) -- in sequence, or
+    overlapped (max of the two plus OVERLAP_COST of the update) unless ``overlap`` is "off".
+    The slowest rank sets the pace.  None if the link probe has no rates for ``transport``."""
+    from .linkprobe import transfer_us
+    H = max(1, int(fuse))
+    comp = comp_step_ms * H
+    worst = 0.0
+    for r in range(nprocs):
+        dom = init_domain(L, nprocs, r, periodic=False, dims=dims)
+        xs = [transfer_us(link, transport, c * pair_bytes) for c in pass_messages(dom, H)]
+        if any(x is None for x in xs):
+            return None
+        xch = max(xs, default=0.0) * 1e-3
+        t = comp + xch if overlap == "off" else max(comp, xch) + OVERLAP_COST * comp
+        worst = max(worst, t)
+    return worst / H
+
+
+def prune_by_model(pred: Dict[int, float], protected: Sequence[int],
+                   factor: float = MODEL_PRUNE) -> Dict[int, float]:
+    """The candidates (index -> modelled ms per step) the model rules out: those slower than
+    ``factor`` x the best modelled candidate, except the ``protected`` ones (the reference's
+    Dims_create grid is always timed).  Returns index -> modelled slowdown."""
+    if not pred:
+        return {}
+    best = min(pred.values())
+    return {i: round(t / best, 3) for i, t in pred.items()
+            if i not in protected and best > 0 and t > factor * best}
+
+
 def time_data_path(settings, ctx, L: int, dims, fuse: int, steps: int = 30, warmup: int = 6,
-                   seed: int = 2024, skip_rccl: bool = False):
+                   seed: int = 2024, skip_rccl: bool = False, info: Optional[Dict] = None):
     """(seconds for ``steps`` steps of the real problem on this data path (max over ranks),
-    whether its passes overlap the halo exchange)."""
+    whether its passes overlap the halo exchange).  ``info`` (optional) receives
+    ``comp_ms_per_step``: the update alone, the fused pass time the engine's autotuner measured
+    on this rank's block at the pass depth, per step (max over ranks; 0 if untimed)."""
     import torch
 
     from ..models.grayscott import GrayScott
@@ -153,15 +218,21 @@ def time_data_path(settings, ctx, L: int, dims, fuse: int, steps: int = 30, warm
         sync()
         el = time.perf_counter() - t0
         ovd = "gated" if sim.gated else bool(sim.overlapped)  # gated: the exchange in-kernel
+        c = sim.fused_choice().get(int(sim.depth)) if sim.backend == "hip" else None
+        comp = float(c[2]) / max(1, int(sim.depth)) if c and c[2] else 0.0
     finally:
         sim.close()
+    comp = ctx.allreduce(comp, "max")
+    if info is not None:
+        info["comp_ms_per_step"] = comp
     return ctx.allreduce(el, "max"), ovd
 
 
 def tune_data_path(settings, ctx, L: int, backend: str,
                    cands: Optional[Sequence[Tuple]] = None,
                    steps: int = 120, warmup: int = 12, log=None,
-                   budget_s: Optional[float] = None, on_row=None) -> Dict:
+                   budget_s: Optional[float] = None, on_row=None,
+                   link: Optional[Dict] = None) -> Dict:
     """Self-check and time every candidate ``(dims, fuse[, overlap[, env]])``; returns
     ``{"dims", "fuse", "transport", "overlap", "inplace_halos", "env", "table"}`` for the fastest
     correct one (identical on every rank; ``env`` must be set for the run that uses it).
@@ -178,12 +249,50 @@ def tune_data_path(settings, ctx, L: int, backend: str,
     per IPC row.  A numerical mismatch is the candidate's own (its grid, overlap mode or tile):
     later rows on the same transport are still tried.  Likewise, once RCCL failed to set up,
     later candidates' fallback chains start after it (``skip_rccl``).  ``on_row(row)`` is
-    called with every finished table row (bench.py streams them for a failure report)."""
+    called with every finished table row (bench.py streams them for a failure report).
+
+    Link-probe pruning (``link``: parallel/linkprobe.py probe_links, the same dict on every
+    rank):
+      * once a row is timed, the fused pass time its engine's autotuner measured on the rank's
+        block fixes the update cost per step (``model_comp_ms_per_step``), and every later
+        candidate gets a modelled time (``model_ms_per_step``, model_step_ms).  Those more than
+        MODEL_PRUNE x the best modelled candidate are recorded as ``"skipped": "model"`` instead
+        of being checked and timed; the reference's Dims_create grid rows never are (BASELINE
+        config 3 is always measured);
+      * where the probe found RCCL unusable but IPC working, the IPC rows are timed first, and
+        once one passed, the rows without a pinned transport (whose "auto" chain would fall back
+        to the host-staged transport) are skipped (``"skipped": "rccl unavailable"``).
+    GS_TUNE_MODEL=0 turns the pruning off (the predictions are still recorded)."""
     from ..models.grayscott import default_fuse
 
     cands = list(cands) if cands is not None else candidates(L, ctx.world_size, backend)
     table = []
     best = None
+    bal = dims_create(ctx.world_size)
+    pair_bytes = 8 if settings.dtype_name == "float32" else 16
+    use_model = link is not None and os.environ.get("GS_TUNE_MODEL", "1") != "0"
+    comp_step = None  # ms per step of the update alone (from the first timed row)
+    no_rccl = bool(use_model and link.get("rccl_failed") and link.get("ipc") == "ok")
+    if no_rccl:
+        # the IPC rows first (stable: the reference grid's IPC rows lead them)
+        cands = ([c for c in cands if len(c) > 4 and c[4] == "ipc"] +
+                 [c for c in cands if not (len(c) > 4 and c[4] == "ipc")])
+
+    def resolved(cand):
+        dom = init_domain(L, ctx.world_size, ctx.rank, periodic=False, dims=cand[0])
+        f = cand[1] if cand[1] > 0 else default_fuse(backend, dom, settings.dtype_name)
+        f = max(1, min(f, min(dom.proc_sizes)))
+        ov = cand[2] if len(cand) > 2 else settings.overlap
+        tr = cand[4] if len(cand) > 4 and cand[4] else "rccl"
+        return f, ov, tr
+
+    def predict(cand):
+        if comp_step is None or link is None:
+            return None
+        f, ov, tr = resolved(cand)
+        return model_step_ms(L, ctx.world_size, cand[0], f, ov, tr, link, comp_step, pair_bytes)
+
+    pruned: Dict[int, float] = {}
     t_start = time.perf_counter()
     proven = None  # transport that passed a check on this node
     failed: Dict[str, str] = {}  # pinned transport -> why it failed on this node
@@ -199,6 +308,19 @@ def tune_data_path(settings, ctx, L: int, backend: str,
             finish({"dims": list(cand[0]), "fuse": cand[1],
                     "overlap_req": cand[2] if len(cand) > 2 else settings.overlap,
                     "skipped": "budget"})
+            continue
+        if no_rccl and not (len(cand) > 4 and cand[4]) and any(
+                r.get("ok") and r.get("transport") == "ipc" for r in table):
+            finish({"dims": list(cand[0]), "fuse": resolved(cand)[0],
+                    "overlap_req": cand[2] if len(cand) > 2 else settings.overlap,
+                    "skipped": "rccl unavailable (link probe): host fallback not timed"})
+            continue
+        if ci in pruned:
+            finish({"dims": list(cand[0]), "fuse": resolved(cand)[0],
+                    "overlap_req": cand[2] if len(cand) > 2 else settings.overlap,
+                    **({"transport_req": cand[4]} if len(cand) > 4 and cand[4] else {}),
+                    "skipped": "model", "model_ms_per_step": round(predict(cand), 4),
+                    "model_slowdown": pruned[ci]})
             continue
         dims, fuse = cand[0], cand[1]
         ov0 = cand[2] if len(cand) > 2 else settings.overlap
@@ -268,10 +390,11 @@ def tune_data_path(settings, ctx, L: int, backend: str,
             continue
         s = copy.copy(settings)
         s.transport, s.overlap = chosen[0], chosen[1]
+        tinfo: Dict = {}
         with _env(chosen[2]):
             try:
                 el, ovd = time_data_path(s, ctx, L, dims, f, steps=steps, warmup=warmup,
-                                         skip_rccl=skip_rccl)
+                                         skip_rccl=skip_rccl, info=tinfo)
                 ran = 1.0
             except Exception as ex:  # e.g. out of memory at the real size: skip this path
                 el, ovd, ran = float("inf"), False, 0.0
@@ -283,6 +406,25 @@ def tune_data_path(settings, ctx, L: int, backend: str,
         row.update(ok=True, transport=chosen[0], overlap=chosen[1], overlapped=ovd,
                    inplace_halos=chosen[2].get("GS_INPLACE_HALO") != "0",
                    ms_per_step=round(1e3 * el / steps, 4), steps=steps)
+        if link is not None and comp_step is None and tinfo.get("comp_ms_per_step", 0) > 0:
+            # the update's own cost per step: the tuned fused pass on this row's blocks (every
+            # candidate updates the same L^3 / N cells per rank)
+            ms = 1e3 * el / steps
+            comp_step = float(tinfo["comp_ms_per_step"])
+            row["model_comp_ms_per_step"] = round(comp_step, 4)
+            preds = {}
+            for cj, cc in enumerate(cands):
+                if cj > ci:
+                    pj = predict(cc)
+                    if pj is not None:
+                        preds[cj] = pj
+            preds[ci] = predict(cand) or ms
+            protected = [cj for cj, cc in enumerate(cands) if list(cc[0]) == list(bal)]
+            if use_model:
+                pruned = prune_by_model(preds, protected)
+        pj = predict(cand)
+        if pj is not None:
+            row["model_ms_per_step"] = round(pj, 4)
         finish(row)
         if log is not None and ctx.rank == 0:
             log(f"data path {row}")

@@ -220,3 +220,23 @@ def test_bench_two_ranks_gated_data_path():
     d = json.loads(lines[-1])
     assert d["value"] > 0 and d["check"]["golden_ok"], d.get("check")
     assert d["config"]["gated"] and "gated" in d["config"]["parallelism"], d["config"]
+
+
+@pytest.mark.parametrize("gated", [2, 0])
+def test_config3_geometry_l512_matches_single_rank(gated):
+    """BASELINE config 3's geometry on one GPU: 8 ranks of 256^3 (2 x 2 x 2, L=512 fp32, ~1 GB
+    each), gated passes (gated = 2) or stream-overlapped ones (gated = 0), 12 steps from the
+    random init, bit for bit equal to one rank at L=512 (the multi-rank
+    tests above use L <= 96)."""
+    L, steps, fuse = 512, 12, 3
+    u1, v1, _ = _single(L, steps, fuse, random_init=5)
+    cfg = _cfg(L, steps, fuse, overlap="on")
+    cfg["knobs"]["gated"] = gated
+    cfg["dims"] = [2, 2, 2]
+    cfg["random_init"] = 5
+    un, vn, meta = run_ranks(8, cfg, timeout=300)
+    assert all(m["transport"] == "ipc" for m in meta), meta
+    assert all(m["gated"] == (gated == 2) for m in meta), meta
+    assert np.isfinite(un).all() and np.isfinite(vn).all()
+    np.testing.assert_array_equal(un, u1)
+    np.testing.assert_array_equal(vn, v1)
