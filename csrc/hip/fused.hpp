@@ -391,11 +391,20 @@ struct FCfg {
   // exchange, and the prefetch depth costs LDS instead of registers -- what makes T = 4 fit
   // the 12-wave workgroup's 168-VGPR budget.  Bit-identical to the register ring.
   static constexpr bool LR = (OPT_ & 4) != 0;
-  static_assert(!LR || (SKEW_ && ROWS_ == 4 && sizeof(T_) == 4 && !NSYNC && !LX),
-                "the LDS ring is built for the skewed fp32 4-row pipeline");
+  static_assert(!LR || (SKEW_ && ROWS_ == 4 && !NSYNC && !LX && (sizeof(T_) == 4 || !FOLD_)),
+                "the LDS ring is built for the skewed 4-row pipeline (fp64: unfolded tiles)");
+  // fp64 LDS ring (LRC): the centre plane comes from registers -- the previous iteration's
+  // level-0 rows, which are exactly the next iteration's centre -- so the ring holds only the
+  // current plane and the prefetch (PF + 1 slots of 16-B pairs: a 4x8 tile's ring + two levels'
+  // row exchange then fit the 160 KiB, 64 + 64 KiB at PF = 1).  fp32 reads the centre back from
+  // the ring instead (PF + 2 slots; its registers are the tighter budget).
+  static constexpr bool LRC = LR && sizeof(T_) == 8;
+  // DMA pieces per wave and plane (16 B per lane, 1 KiB per wave instruction): fp32 two rows per
+  // piece, fp64 one
+  static constexpr int ND = LR ? ROWS_ * 64 * (int)sizeof(typename PairT<T_>::type) / 1024 : 0;
   static_assert(!FOLD_ || (Q32_ && !PERIODIC_ && ROWS_ == 4),
                 "folded strips need Q32, a non-periodic grid and 4-row waves");
-  static constexpr int R = PF + 2;                    // level-0 ring slots (VGPRs or LDS)
+  static constexpr int R = LRC ? PF + 1 : PF + 2;     // level-0 ring slots (VGPRs or LDS)
   static constexpr int XL = LR ? (TL > 1 ? TL - 1 : 1) : TL;  // levels with an xch row exchange
   // the row-exchange slot of consumer level l (LR: level 0 reads the LDS ring instead)
   static constexpr int xi(int l) { return LR ? l - 1 : l; }
@@ -419,8 +428,10 @@ struct FCfg {
   // (the 128-VGPR shapes would spill, the fp64 ones are near 256).  L=512 T=3, random init, the
   // driver's window: 4x12:2s 689k -> 719k, 4x12:1s 695-698k -> 703-705k MLUPS (profiles/
   // r4_fused_ab.txt).  ABL bit 6 turns it off (A/B), bit 2 forces it on.
+  // (fp64: the LDS-ring shapes, whose freed ring registers pay for the keys and the step words;
+  // the register-ring fp64 tiles sit at ~247 VGPRs)
   static constexpr bool KV =
-      (ABL_ & 4) != 0 || (sizeof(T) == 4 && WPEU == 3 && (ABL_ & 64) == 0);
+      (ABL_ & 4) != 0 || ((sizeof(T) == 4 ? WPEU == 3 : LRC) && (ABL_ & 64) == 0);
   // The step-uniform Philox words of rounds 1-3 (philox_uniform) computed once per kernel and
   // held in VGPRs, 5 per level, instead of rebuilt on the SALU at every draw (the SALU is
   // shared by the CU's four SIMDs and was the co-bottleneck of the noise path).  Default on the
@@ -474,6 +485,7 @@ struct FusedState {
   uint32_t kv[(C::KV && !C::KVL) ? 14 : 1];  // Philox round keys of rounds 4-10 (C::KV)
   uint32_t pu[C::PU ? 5 * C::TL : 1];  // step-uniform Philox words per level (C::PU)
   V2 LD[C::LR ? 1 : C::R][C::ROWS];  // (FCfg::LR: unused, the ring lives in LDS)
+  V2 C0[C::LRC ? C::ROWS : 1];       // FCfg::LRC: the centre plane's rows (last iteration's input)
   V2 OUT[C::NO][C::NS][C::ROWS];
   V2 A[C::TL][C::ROWS];
 };
@@ -524,6 +536,16 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, int voff, int so
       : "memory");
 }
 
+// One vector-memory store to an empty descriptor (num_records 0: dropped) that the compiler can
+// neither merge nor delete.  FCfg::LR's counted waits (lr_wait) assume ROWS stores per pipeline
+// iteration on the storing waves; builtin stores of the same value to the same out-of-range offset
+// were merged -- the segment prologue issued one of its four padding stores, so the first
+// iteration's lr_wait let three of the wave's DMA pieces still be in flight when the level-0 rows
+// were read (an intermittent fp64 mismatch at segment starts, profiles/r6_f64_lr.txt).
+__device__ __forceinline__ void pad_store(__amdgpu_buffer_rsrc_t r) {
+  asm volatile("buffer_store_dword %0, off, %1, 0" ::"v"(0u), "s"(r) : "memory");
+}
+
 template <int N>
 __device__ __forceinline__ void vmcnt_wait() {
   static_assert(N >= 0 && N < 64, "vmcnt field");
@@ -531,15 +553,16 @@ __device__ __forceinline__ void vmcnt_wait() {
 }
 
 // FCfg::LR: wait until this wave's DMA of the plane consumed next has landed.  Per pipeline
-// iteration a wave issues 2 DMA pieces right after the barrier and then S stores (ROWS when it
-// stores the last level, else 0; constant per wave: the fill periods store to an empty
-// descriptor), so the DMA of plane p (issued PF iterations back) has S + (PF - 1)(2 + S) younger
-// VMEM operations (the segment prologue pads its DMAs with S empty stores to keep the count).
+// iteration a wave issues ND DMA pieces (fp32 2, fp64 4) right after the barrier and then S
+// stores (ROWS when it stores the last level, else 0; constant per wave: the fill periods store to
+// an empty descriptor), so the DMA of plane p (issued PF iterations back) has S + (PF - 1)(ND + S)
+// younger VMEM operations (the segment prologue pads its DMAs with S empty stores to keep the
+// count).
 template <class C>
 __device__ __forceinline__ void lr_wait(const FusedSeg& sg) {
-  constexpr int S = C::ROWS, PF = C::PF;
-  if (sg.lst) vmcnt_wait<S + (PF - 1) * (2 + S)>();
-  else vmcnt_wait<(PF - 1) * 2>();
+  constexpr int S = C::ROWS, PF = C::PF, ND = C::ND;
+  if (sg.lst) vmcnt_wait<S + (PF - 1) * (ND + S)>();
+  else vmcnt_wait<(PF - 1) * ND>();
 }
 
 template <class C>
@@ -636,17 +659,19 @@ __device__ __forceinline__ typename C::V2 cell_update(typename C::V2& A, typenam
 // Non-skewed: level l+1 is computed from level l of the SAME iteration (one barrier per level).
 // Skewed: level l+1 consumes level l's output of the PREVIOUS iteration, so every level's
 // input rows are published before a single barrier; level l produces plane p - (2l + 1).
-// FCfg::LR: issue the wave's two DMA pieces of level-0 plane p + PF (rows 4w .. 4w + 3) into ring
+// FCfg::LR: issue the wave's DMA pieces of level-0 plane p + PF (rows 4w .. 4w + 3) into ring
 // slot `slot`.  Unconditional (an empty descriptor past the segment): constant VMEM count.
 template <class C>
 __device__ __forceinline__ void lr_dma(FusedSeg& sg, int slot, bool ok) {
   const __amdgpu_buffer_rsrc_t r = plane_rsrc(sg.ldp, ok ? sg.pzb : 0);
   constexpr uint32_t kSlot = C::RT * 64 * sizeof(typename C::V2);
-  // (the second piece's offset goes through voffset too: the range check of a raw buffer access
-  // does not include soffset, and a first piece above the plane must not drag a valid second
-  // piece out of range with it)
-  dma16(r, sg.dvoff, 0, sg.rbase + (uint32_t)slot * kSlot);
-  dma16(r, sg.dvoff + 2 * sg.pitchb, 0, sg.rbase + (uint32_t)slot * kSlot + 1024u);
+  // (every piece's offset goes through voffset: the range check of a raw buffer access does not
+  // include soffset, and a first piece above the plane must not drag a valid later piece out of
+  // range with it).  fp32: piece k = rows 2k, 2k + 1; fp64: piece k = row k.
+  constexpr int kRows = C::ROWS / C::ND;
+#pragma unroll
+  for (int k = 0; k < C::ND; ++k)
+    dma16(r, sg.dvoff + k * kRows * sg.pitchb, 0, sg.rbase + (uint32_t)slot * kSlot + 1024u * k);
   sg.ldp += sg.pzb;
 }
 
@@ -746,10 +771,16 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
     if constexpr (FILL) {
       const int d = p - sg.z0, e = sg.pend - p;
       need = d >= (C::SKEW ? 3 * l + 1 - TL : 2 * l + 1 - TL) && (!C::SKEW || e > TL - 1 - l);
+      // (LRC: level 0 runs from the first iteration on -- it hands its rows on as the next
+      // iteration's centre; the one extra level-0 update per segment feeds no needed plane)
+      if constexpr (C::LRC) need = need || l == 0;
       if (!need && l + 1 == TL && !((sg.skip >> l) & 1)) {
         const __amdgpu_buffer_rsrc_t w = plane_rsrc(sg.stp, 0);
 #pragma unroll
-        for (int j = 0; j < ROWS; ++j) bstore<C::STORE_AUX>(w, (int)0x80000000, in[j]);
+        for (int j = 0; j < ROWS; ++j) {
+          if constexpr (C::LR) pad_store(w);  // (counted by lr_wait: never merged)
+          else bstore<C::STORE_AUX>(w, (int)0x80000000, in[j]);
+        }
       }
     }
     if (need && !((sg.skip >> l) & 1)) {  // wave-uniform
@@ -766,10 +797,10 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
 #pragma unroll
         for (int j = 0; j < (C::LR ? ROWS : 1); ++j) {
           r0[j] = lds_load2(&ring[IR][r + j][sg.lane]);
-          c0[j] = lds_load2(&ring[(IR + C::R - 1) % C::R][r + j][sg.lane]);
+          if constexpr (!C::LRC) c0[j] = lds_load2(&ring[(IR + C::R - 1) % C::R][r + j][sg.lane]);
         }
         in = r0;
-        Cc = c0;
+        Cc = C::LRC ? S.C0 : c0;  // (LRC: the rows become the next centre after the update)
       } else {
         up = lds_load2(&xch[C::xi(l)][IS][sg.wup][1][sg.lane]);
         dn = lds_load2(&xch[C::xi(l)][IS][sg.wdn][0][sg.lane]);
@@ -844,6 +875,12 @@ __device__ __forceinline__ void fused_iter(FusedState<C>& S,
         }
       }
       if constexpr (C::LX) asm volatile("" ::: "memory");
+      if constexpr (C::LRC) {
+        if (l == 0) {
+#pragma unroll
+          for (int j = 0; j < ROWS; ++j) S.C0[j] = in[j];  // the next iteration's centre
+        }
+      }
       if (l + 1 < TL) {
         if (sg.edge) {
           const T bu = (T)gs::bc_u(a.t + l + 1);
@@ -1168,6 +1205,10 @@ __device__ __forceinline__ void fused_body(const typename C::V2* __restrict__ s,
       for (int l = 0; l < TL; ++l)
 #pragma unroll
         for (int j = 0; j < ROWS; ++j) S.A[l][j] = typename C::V2{(T)0, (T)0};
+      if constexpr (C::LRC) {
+#pragma unroll
+        for (int j = 0; j < ROWS; ++j) S.C0[j] = typename C::V2{(T)0, (T)0};
+      }
       sg.p = z0 - TL;
       sg.ldend = z1 + TL;
       sg.pend = C::SKEW ? z1 + 2 * TL - 1 : z1 + TL;
@@ -1176,12 +1217,14 @@ __device__ __forceinline__ void fused_body(const typename C::V2* __restrict__ s,
       sg.ldp = (const char*)s + (int64_t)(sg.p + C::PF + g.H) * sg.pzb;
       sg.stp = (char*)d + (int64_t)(qlast + g.H) * sg.pzb;
       if constexpr (C::LR) {
-        // the wave's DMA pieces: lane i moves pairs 2(i & 31), +1 of tile row 4w + 2k + i / 32
+        // the wave's DMA pieces: fp32 lane i moves pairs 2(i & 31), +1 of tile row 4w + 2k + i / 32
         // (folded tiles: image columns >= 32 are the upper y-tile's columns 0..31)
-        const int c = 2 * (sg.lane & 31);
+        // (fp64: lane i moves pair i of row 4w + k)
+        const int c = C::ND == 2 ? 2 * (sg.lane & 31) : sg.lane;
         const int cx = (C::FOLD && xw == 32) ? (c & 31) : c;
         const int cdy = (C::FOLD && c >= 32 && live && xw == 32) ? a.ystep : 0;
-        sg.dvoff = ((Y0 + sg.wave * ROWS + (sg.lane >> 5) + cdy + g.H) * g.px + X0 + cx + g.xo) *
+        const int crow = C::ND == 2 ? (sg.lane >> 5) : 0;
+        sg.dvoff = ((Y0 + sg.wave * ROWS + crow + cdy + g.H) * g.px + X0 + cx + g.xo) *
                    (int)sizeof(typename C::V2);
         // every wave is past the previous segment's ring reads and its own DMAs have landed
         // (a DMA of the old segment's drain must not land after this segment's prologue)
@@ -1197,8 +1240,7 @@ __device__ __forceinline__ void fused_body(const typename C::V2* __restrict__ s,
           if (sg.lst) {
             const __amdgpu_buffer_rsrc_t w = plane_rsrc(sg.stp, 0);
 #pragma unroll
-            for (int j = 0; j < ROWS; ++j)
-              bstore<C::STORE_AUX>(w, (int)0x80000000, typename C::V2{(T)0, (T)0});
+            for (int j = 0; j < ROWS; ++j) pad_store(w);
           }
         }
         sg.ldp = keep;
@@ -1467,39 +1509,42 @@ inline const FusedCfgEntry* fused_cfg_table(int* n) {
       {"4x12:1sfl", true, false},  // 30  folded last strip
       {"4x12:3sl", true, false},   // 31  3-plane prefetch (T = 2 only: LDS)
       {"4x12:2sfl", true, false},  // 32  2-plane prefetch, folded last strip
+      // fp64 LDS ring (FCfg::LRC: PF + 1 slots, the centre plane from registers); the freed ring
+      // registers hold the Philox round keys and step words (KV / PU)
+      {"4x8:1sl", false, true},    // 33
 #ifdef GS_ABLATION
       // measured and rejected in round 5 (exact; kept for reproduction in the ablation build):
       // fp64 LDS x-sums 4-6 % slower, neighbour-only sync 5-6 % slower (profiles/r5_f64_counters.txt,
       // r5_nsync_rejected.txt)
-      {"4x8:1sx", false, true},    // 33  fp64: x-neighbour sums through LDS (FCfg::LX)
-      {"4x6:2sx", false, true},    // 34  fp64: x-neighbour sums through LDS (FCfg::LX)
-      {"4x8:1x", false, true},     // 35  fp64: x-neighbour sums through LDS, unskewed
-      {"4x12:1sn", true, false},   // 36  neighbour-only LDS sync instead of the barrier (NSYNC)
-      {"4x12:1sfn", true, false},  // 37  folded last strip + neighbour-only sync
-      {"4x12:2sn", true, false},   // 38  2-plane prefetch + neighbour-only sync
-      {"4x8:1sxn", false, true},   // 39  fp64: LDS x-sums + neighbour-only sync
-      {"4x8:1sn", false, true},    // 40  fp64: neighbour-only sync
-      {"4x12:2s-abl1", true, false},  // 41  no barriers
-      {"4x12:2s-abl2", true, false},  // 42  L2-resident loads
-      {"4x12:1s-abl4", true, false},  // 43  Philox keys in VGPRs (exact)
-      {"4x12:2s-abl4", true, false},  // 44  Philox keys in VGPRs (exact)
-      {"4x12:1s-abl8", true, false},  // 45  DPP sums with the s_nop (exact)
-      {"4x12:1s-abl12", true, false}, // 46  abl4 + abl8 (exact)
-      {"4x12:1s-abl16", true, false}, // 47  pipeline fill computes every level (exact)
-      {"4x8:1s-abl16", true, true},   // 48  pipeline fill computes every level (exact)
-      {"4x6:2s-abl16", true, true},   // 49  pipeline fill computes every level (exact)
-      {"4x12:1s-abl32", true, false}, // 50  Philox only on lanes in the x cone (exact)
-      {"4x12:2s-abl64", true, false}, // 51  Philox keys rebuilt on the SALU (exact)
-      {"4x12:1s-abl64", true, false}, // 52  Philox keys rebuilt on the SALU (exact)
-      {"4x12:1s-abl256", true, false}, // 53  step-uniform Philox words on the SALU (exact)
-      {"4x12:1s-abl512", true, false}, // 54  Philox blocks of all levels before the barrier (exact)
-      {"4x12:1s-abl1024", true, false}, // 55  the top level's Philox block before the barrier (exact)
-      {"4x12:1s-abl1536", true, false}, // 56  the top two levels' Philox blocks before the barrier
-      {"4x12:1s-abl2048", true, false}, // 57  non-temporal output stores (exact)
-      {"4x12:1s-abl4096", true, false}, // 58  device-scope (write-through) output stores (exact)
-      {"4x12:1s-abl6144", true, false}, // 59  both (exact)
-      {"4x12:2s-abl128", true, false},  // 60  2-plane prefetch + step-uniform Philox words in VGPRs
-      {"4x12:3s-abl128", true, false},  // 61  3-plane prefetch + step-uniform Philox words in VGPRs
+      {"4x8:1sx", false, true},    // 34  fp64: x-neighbour sums through LDS (FCfg::LX)
+      {"4x6:2sx", false, true},    // 35  fp64: x-neighbour sums through LDS (FCfg::LX)
+      {"4x8:1x", false, true},     // 36  fp64: x-neighbour sums through LDS, unskewed
+      {"4x12:1sn", true, false},   // 37  neighbour-only LDS sync instead of the barrier (NSYNC)
+      {"4x12:1sfn", true, false},  // 38  folded last strip + neighbour-only sync
+      {"4x12:2sn", true, false},   // 39  2-plane prefetch + neighbour-only sync
+      {"4x8:1sxn", false, true},   // 40  fp64: LDS x-sums + neighbour-only sync
+      {"4x8:1sn", false, true},    // 41  fp64: neighbour-only sync
+      {"4x12:2s-abl1", true, false},  // 42  no barriers
+      {"4x12:2s-abl2", true, false},  // 43  L2-resident loads
+      {"4x12:1s-abl4", true, false},  // 44  Philox keys in VGPRs (exact)
+      {"4x12:2s-abl4", true, false},  // 45  Philox keys in VGPRs (exact)
+      {"4x12:1s-abl8", true, false},  // 46  DPP sums with the s_nop (exact)
+      {"4x12:1s-abl12", true, false}, // 47  abl4 + abl8 (exact)
+      {"4x12:1s-abl16", true, false}, // 48  pipeline fill computes every level (exact)
+      {"4x8:1s-abl16", true, true},   // 49  pipeline fill computes every level (exact)
+      {"4x6:2s-abl16", true, true},   // 50  pipeline fill computes every level (exact)
+      {"4x12:1s-abl32", true, false}, // 51  Philox only on lanes in the x cone (exact)
+      {"4x12:2s-abl64", true, false}, // 52  Philox keys rebuilt on the SALU (exact)
+      {"4x12:1s-abl64", true, false}, // 53  Philox keys rebuilt on the SALU (exact)
+      {"4x12:1s-abl256", true, false}, // 54  step-uniform Philox words on the SALU (exact)
+      {"4x12:1s-abl512", true, false}, // 55  Philox blocks of all levels before the barrier (exact)
+      {"4x12:1s-abl1024", true, false}, // 56  the top level's Philox block before the barrier (exact)
+      {"4x12:1s-abl1536", true, false}, // 57  the top two levels' Philox blocks before the barrier
+      {"4x12:1s-abl2048", true, false}, // 58  non-temporal output stores (exact)
+      {"4x12:1s-abl4096", true, false}, // 59  device-scope (write-through) output stores (exact)
+      {"4x12:1s-abl6144", true, false}, // 60  both (exact)
+      {"4x12:2s-abl128", true, false},  // 61  2-plane prefetch + step-uniform Philox words in VGPRs
+      {"4x12:3s-abl128", true, false},  // 62  3-plane prefetch + step-uniform Philox words in VGPRs
 #endif
   };
   *n = (int)(sizeof(t) / sizeof(t[0]));
@@ -1567,16 +1612,21 @@ inline int fused_cfg_env() {
   return v;
 }
 
-// whether an LDS-ring shape (FCfg::LR, 12 waves of 4 rows) fits the CU's 160 KiB at depth tl with
-// a pf-plane prefetch: the ring's pf + 2 planes plus the tl - 1 levels' row exchange (2 slots)
-constexpr bool lr_fits(int tl, int pf) {
-  return ((pf + 2) * 48 * 64 + (tl > 1 ? tl - 1 : 1) * 2 * 12 * 2 * 64) * 8 <= 160 * 1024;
+// whether an LDS-ring shape (FCfg::LR, 4-row waves) fits the CU's 160 KiB at depth tl with a
+// pf-plane prefetch: the ring (fp32 pf + 2 planes, fp64 pf + 1: FCfg::LRC) plus the tl - 1 levels'
+// row exchange (2 slots), with 1 KiB to spare for the small tables
+constexpr bool lr_fits(int tl, int pf, int waves = 12, int pair_bytes = 8) {
+  return ((pf + (pair_bytes == 16 ? 1 : 2)) * 4 * waves * 64 +
+          (tl > 1 ? tl - 1 : 1) * 2 * waves * 2 * 64) * pair_bytes <= 159 * 1024;
 }
-// the LDS-ring table entries (28 .. 32) as (prefetch, folded)
-constexpr int kLrPF[5] = {2, 1, 1, 3, 2};
-constexpr bool kLrFold[5] = {false, false, true, false, true};
-inline bool fused_cfg_is_lr(int i) { return i >= 28 && i <= 32; }
-inline bool lr_cfg_fits(int i, int tl) { return !fused_cfg_is_lr(i) || lr_fits(tl, kLrPF[i - 28]); }
+// the LDS-ring table entries (28 .. 33) as (prefetch, folded); 33 is the fp64 4x8 shape
+constexpr int kLrPF[6] = {2, 1, 1, 3, 2, 1};
+constexpr bool kLrFold[6] = {false, false, true, false, true, false};
+inline bool fused_cfg_is_lr(int i) { return i >= 28 && i <= 33; }
+inline bool lr_cfg_fits(int i, int tl) {
+  if (!fused_cfg_is_lr(i)) return true;
+  return i == 33 ? lr_fits(tl, kLrPF[i - 28], 8, 16) : lr_fits(tl, kLrPF[i - 28]);
+}
 
 // one LDS-ring shape: its launch where it fits the LDS at this depth, else false
 template <typename T, int TL, bool PER, bool NZ, bool Q32, int PF, bool FOLD>
@@ -1613,14 +1663,21 @@ void run_fused_cfg(const void* s, void* d, const FusedArgs& a, const gs::Params&
       case 15: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true>, T>::run(s, d, a, p, st); return;
       case 16: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
       case 17: FusedLaunch<FCfg<T, TL, 4, 4, 2, PER, NZ>, T>::run(s, d, a, p, st); return;
+      case 33:
+        if constexpr (lr_fits(TL, 1, 8, 16)) {
+          FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, Q32, 0, false, 4>, T>::run(s, d, a, p, st);
+          return;
+        }
+        break;
+
 #ifdef GS_ABLATION
-      case 33: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 0, false, 1>, T>::run(s, d, a, p, st); return;
-      case 34: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 0, false, 1>, T>::run(s, d, a, p, st); return;
-      case 35: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, false, true, 0, false, 1>, T>::run(s, d, a, p, st); return;
-      case 39: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 0, false, 3>, T>::run(s, d, a, p, st); return;
-      case 40: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 0, false, 2>, T>::run(s, d, a, p, st); return;
-      case 48: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
-      case 49: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 34: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 0, false, 1>, T>::run(s, d, a, p, st); return;
+      case 35: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 0, false, 1>, T>::run(s, d, a, p, st); return;
+      case 36: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, false, true, 0, false, 1>, T>::run(s, d, a, p, st); return;
+      case 40: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 0, false, 3>, T>::run(s, d, a, p, st); return;
+      case 41: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 0, false, 2>, T>::run(s, d, a, p, st); return;
+      case 49: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 50: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
 #endif
       default: break;
     }
@@ -1657,30 +1714,30 @@ void run_fused_cfg(const void* s, void* d, const FusedArgs& a, const gs::Params&
       case 31: if (run_lr<T, TL, PER, NZ, Q32, 3, false>(s, d, a, p, st)) return; break;
       case 32: if (run_lr<T, TL, PER, NZ, Q32, 2, true>(s, d, a, p, st)) return; break;
 #ifdef GS_ABLATION
-      case 36: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 0, false, 2>, T>::run(s, d, a, p, st); return;
-      case 37: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 0, true, 2>, T>::run(s, d, a, p, st); return;
-      case 38: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 0, false, 2>, T>::run(s, d, a, p, st); return;
-      case 41: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 1>, T>::run(s, d, a, p, st); return;
-      case 42: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 2>, T>::run(s, d, a, p, st); return;
-      case 43: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;
-      case 44: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;
-      case 45: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 8>, T>::run(s, d, a, p, st); return;
-      case 46: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 12>, T>::run(s, d, a, p, st); return;
-      case 47: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
-      case 48: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
-      case 49: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
-      case 50: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 32>, T>::run(s, d, a, p, st); return;
-      case 51: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 64>, T>::run(s, d, a, p, st); return;
-      case 52: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 64>, T>::run(s, d, a, p, st); return;
-      case 53: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 256>, T>::run(s, d, a, p, st); return;
-      case 54: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 512>, T>::run(s, d, a, p, st); return;
-      case 55: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 1024>, T>::run(s, d, a, p, st); return;
-      case 56: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 1536>, T>::run(s, d, a, p, st); return;
-      case 57: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 2048>, T>::run(s, d, a, p, st); return;
-      case 58: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 4096>, T>::run(s, d, a, p, st); return;
-      case 59: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 6144>, T>::run(s, d, a, p, st); return;
-      case 60: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, Q32, 128>, T>::run(s, d, a, p, st); return;
-      case 61: FusedLaunch<FCfg<T, TL, 4, 12, 3, PER, NZ, true, Q32, 128>, T>::run(s, d, a, p, st); return;
+      case 37: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 0, false, 2>, T>::run(s, d, a, p, st); return;
+      case 38: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 0, true, 2>, T>::run(s, d, a, p, st); return;
+      case 39: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 0, false, 2>, T>::run(s, d, a, p, st); return;
+      case 42: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 1>, T>::run(s, d, a, p, st); return;
+      case 43: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 2>, T>::run(s, d, a, p, st); return;
+      case 44: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;
+      case 45: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 4>, T>::run(s, d, a, p, st); return;
+      case 46: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 8>, T>::run(s, d, a, p, st); return;
+      case 47: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 12>, T>::run(s, d, a, p, st); return;
+      case 48: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 49: FusedLaunch<FCfg<T, TL, 4, 8, 1, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 50: FusedLaunch<FCfg<T, TL, 4, 6, 2, PER, NZ, true, true, 16>, T>::run(s, d, a, p, st); return;
+      case 51: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 32>, T>::run(s, d, a, p, st); return;
+      case 52: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, true, 64>, T>::run(s, d, a, p, st); return;
+      case 53: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, true, 64>, T>::run(s, d, a, p, st); return;
+      case 54: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 256>, T>::run(s, d, a, p, st); return;
+      case 55: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 512>, T>::run(s, d, a, p, st); return;
+      case 56: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 1024>, T>::run(s, d, a, p, st); return;
+      case 57: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 1536>, T>::run(s, d, a, p, st); return;
+      case 58: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 2048>, T>::run(s, d, a, p, st); return;
+      case 59: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 4096>, T>::run(s, d, a, p, st); return;
+      case 60: FusedLaunch<FCfg<T, TL, 4, 12, 1, PER, NZ, true, Q32, 6144>, T>::run(s, d, a, p, st); return;
+      case 61: FusedLaunch<FCfg<T, TL, 4, 12, 2, PER, NZ, true, Q32, 128>, T>::run(s, d, a, p, st); return;
+      case 62: FusedLaunch<FCfg<T, TL, 4, 12, 3, PER, NZ, true, Q32, 128>, T>::run(s, d, a, p, st); return;
 #endif
       default: break;  // 0 and 14: the default shape below
     }

@@ -217,3 +217,36 @@ def test_snapshot_minmax_equals_host_scan(prec, L):
     np.testing.assert_array_equal(u, gu)
     np.testing.assert_array_equal(v, gv)
     g.close()
+
+
+@pytest.mark.parametrize("L,fuse,sched", [(200, 3, 2), (256, 3, 1), (200, 2, 0), (96, 3, 2),
+                                          (256, 2, 2)])
+def test_fp64_lds_ring_bitwise_vs_register_ring(L, fuse, sched):
+    """The fp64 LDS-ring shape (csrc/hip/fused.hpp "4x8:1sl": FCfg::LR + LRC -- level-0 planes by
+    LDS-DMA into a PF + 1 ring, the centre plane from registers, Philox keys / step words in
+    VGPRs) equals the register-ring production shape 4x8:1s bit for bit: edge tiles in x and y
+    (L = 200), a z extent that leaves short chunks (L = 96), every schedule."""
+    from grayscott_amd.models.grayscott import GrayScott
+    from grayscott_amd.ops import native
+    from grayscott_amd.parallel.decomp import init_domain
+    from grayscott_amd.utils.config import Settings
+    out = []
+    try:
+        for cfg in ("4x8:1s", "4x8:1sl"):
+            native.fused_select(cfg)
+            native.fused_sched(sched)
+            s = Settings(L=L, precision="Float64", F=0.02, k=0.048, dt=1.0, Du=0.2, Dv=0.1,
+                         noise=0.1, backend="AMDGPU", seed=31)
+            sim = GrayScott(s, init_domain(L, 1, 0), fuse=fuse)
+            try:
+                sim.init_fields()
+                sim.randomize_fields(seed=3)
+                sim.iterate(4 * fuse + 1)
+                out.append(sim.get_fields())
+            finally:
+                sim.close()
+    finally:
+        native.fused_unpin()
+    assert np.isfinite(out[1][0]).all()
+    np.testing.assert_array_equal(out[1][0], out[0][0])
+    np.testing.assert_array_equal(out[1][1], out[0][1])
