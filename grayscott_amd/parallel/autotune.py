@@ -126,9 +126,20 @@ def candidates(L: int, nprocs: int, backend: str) -> List[Tuple]:
 
 # A candidate the model says loses by more than this factor is not timed (link-probe pruning)
 MODEL_PRUNE = 1.20
-# Overlapped passes: the split launches and the face-slab shell cost about this share of a pass
-# on top of max(inner update, exchange) (profiles/r3_overlap_split.txt: 11-28 us of ~560 us)
-OVERLAP_COST = 0.05
+# What an overlapped pass costs on top of max(update, exchange), as a share of the update, per
+# halo layout and transport (measured on one GPU with the exchange in flight):
+#   IPC: gated passes (the exchange inside the pass's launch) -- z slab 1.05-1.07x, 2x2x2 rank
+#        1.11-1.15x the full pass (profiles/r5_gated.txt);
+#   RCCL: stream-overlapped passes (inner box, then the face-slab shell) -- 2x2x2 rank 1.34x
+#        (README round-4 item 3, profiles/r4_shell.txt); z slabs only split off their two faces
+#        (profiles/r3_overlap_split.txt: 11-28 us shells on ~560 us passes)
+OVERLAP_COST = {("zslab", "ipc"): 0.07, ("zslab", "rccl"): 0.10,
+                ("packed", "ipc"): 0.15, ("packed", "rccl"): 0.34}
+
+
+def overlap_cost(dims, transport: str) -> float:
+    zslab = int(dims[0]) == 1 and int(dims[1]) == 1
+    return OVERLAP_COST[("zslab" if zslab else "packed", "ipc" if transport == "ipc" else "rccl")]
 
 
 def pass_messages(dom, H: int) -> List[int]:
@@ -158,11 +169,12 @@ def model_step_ms(L: int, nprocs: int, dims, fuse: int, overlap: str, transport:
     ``comp_step_ms``, the same local volume on every candidate) plus its exchange -- the slowest
     of its neighbour messages over the slowest probed link of ``transport`` (xGMI links are
     point to point: the messages to different neighbours move at once) -- in sequence, or
-    overlapped (max of the two plus OVERLAP_COST of the update) unless ``overlap`` is "off".
+    overlapped (max of the two plus overlap_cost of the update) unless ``overlap`` is "off".
     The slowest rank sets the pace.  None if the link probe has no rates for ``transport``."""
     from .linkprobe import transfer_us
     H = max(1, int(fuse))
     comp = comp_step_ms * H
+    oc = overlap_cost(dims, transport)
     worst = 0.0
     for r in range(nprocs):
         dom = init_domain(L, nprocs, r, periodic=False, dims=dims)
@@ -170,7 +182,7 @@ def model_step_ms(L: int, nprocs: int, dims, fuse: int, overlap: str, transport:
         if any(x is None for x in xs):
             return None
         xch = max(xs, default=0.0) * 1e-3
-        t = comp + xch if overlap == "off" else max(comp, xch) + OVERLAP_COST * comp
+        t = comp + xch if overlap == "off" else max(comp, xch) + oc * comp
         worst = max(worst, t)
     return worst / H
 

@@ -87,12 +87,17 @@ def test_model_prefers_the_grid_on_slow_links_and_slabs_never_win_more_than_over
     # 20 GB/s: a 6.4 MB slab message is ~320 us per pass against 79 us for a 1.6 MB face; in
     # sequence the grid wins, overlapped the slab's exchange hides under its 480 us pass
     assert grid < zs and zs_ov < zs
-    assert zs_ov == pytest.approx(comp * (1 + autotune.OVERLAP_COST))
+    assert zs_ov == pytest.approx(comp * (1 + autotune.overlap_cost([1, 1, 8], "rccl")))
     assert grid == pytest.approx(comp + 1e3 * (3 * 256 * 256 * 8) / 20e9 / 3, rel=0.02)
     # fast links: the exchange hides under the update when overlapped
     fast = _link({4096: 5.0, 8 << 20: 1e6 * (8 << 20) / 400e9})
     zs_fast = autotune.model_step_ms(512, 8, [1, 1, 8], 3, "auto", "rccl", fast, comp)
-    assert zs_fast == pytest.approx(comp * (1 + autotune.OVERLAP_COST))
+    assert zs_fast == pytest.approx(comp * (1 + autotune.overlap_cost([1, 1, 8], "rccl")))
+    # a 2x2x2 rank's stream-overlapped pass costs a third more than its update (RCCL), so on
+    # fast links the pass in sequence is the better model row
+    g_ov = autotune.model_step_ms(512, 8, [2, 2, 2], 3, "auto", "rccl", fast, comp)
+    g_off = autotune.model_step_ms(512, 8, [2, 2, 2], 3, "off", "rccl", fast, comp)
+    assert g_off < g_ov == pytest.approx(comp * 1.34)
 
 
 def test_prune_rule_protects_the_reference_grid():
@@ -107,7 +112,9 @@ def test_candidate_table_is_pruned_by_the_model_on_slow_links():
     """The whole decision for an 8-rank L=512 job: with 8 GB/s links (a z-slab message then
     takes 800 us, more than the 480 us pass it could hide under) every z-slab candidate is
     modelled > 20 % slower than the best grid row and would be skipped; the reference grid rows
-    are protected.  With 400 GB/s links nothing is pruned."""
+    are protected.  With 400 GB/s links no z slab is pruned; the only rows ruled out are the
+    stream-overlapped packed grids on RCCL, whose split pass costs a third more than the update
+    (overlap_cost) while the exchange they would hide is short."""
     comp = 0.16
     bal = dims_create(8)
     cands = autotune.candidates(512, 8, "hip")
@@ -126,7 +133,11 @@ def test_candidate_table_is_pruned_by_the_model_on_slow_links():
         if expect_pruned:
             assert set(zslab) <= set(out), (pred, out)
         else:
-            assert out == {}, (pred, out)
+            assert not set(out) & set(zslab), (pred, out)
+            for i in out:
+                c = cands[i]
+                assert c[2] != "off" and not (len(c) > 4 and c[4] == "ipc"), c
+                assert list(c[0]) not in ([1, 1, 8], list(bal)), c
 
 
 class _OneRankView:
@@ -185,4 +196,8 @@ def test_tuner_skips_what_the_model_rules_out(monkeypatch, rate, rccl_failed):
         host = [r for r in tab if r.get("skipped", "").startswith("rccl unavailable")]
         assert host and not any(t == "auto" for *_, t in timed)
     else:
-        assert not any(r.get("skipped") for r in tab)
+        # fast links: only the RCCL stream-overlapped packed grids (1.34x passes) may be ruled out
+        for r in tab:
+            if r.get("skipped"):
+                assert r["skipped"] == "model" and r["dims"] not in ([1, 1, 8], bal), r
+                assert r["overlap_req"] != "off" and r.get("transport_req") != "ipc", r
