@@ -29,6 +29,7 @@ def _worker(rank, world, port, outdir, cfg):
         os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": "0",
                            "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
                            "OMP_NUM_THREADS": "1"})
+        os.environ.update(cfg.get("env") or {})
         from grayscott_amd.models.grayscott import GrayScott
         from grayscott_amd.parallel import dist as gdist
         from grayscott_amd.parallel.decomp import choose_dims, init_domain
@@ -76,9 +77,19 @@ def run_ranks(world: int, cfg: dict, timeout: float = 240.0):
     with tempfile.TemporaryDirectory() as outdir:
         ctx = mp.start_processes(_worker, args=(world, port, outdir, cfg), nprocs=world,
                                  join=False, start_method="spawn")
+        # bounded: ranks still running after 3 x timeout are killed and the test fails (a hung
+        # rank must end the test, not the GPU-test run).  join() returns False each time one
+        # rank of several exits, so it is called until all have or the time is up
+        import time
+        deadline = time.monotonic() + 3 * timeout
         ok = ctx.join(timeout)
-        while not ok:
-            ok = ctx.join(timeout)
+        while not ok and time.monotonic() < deadline:
+            ok = ctx.join(max(1.0, deadline - time.monotonic()))
+        if not ok:
+            for p in ctx.processes:
+                if p.is_alive():
+                    p.kill()
+            raise RuntimeError(f"{world} ranks did not finish within {3 * timeout:g} s")
         errs = [f for f in os.listdir(outdir) if f.startswith("error")]
         if errs:
             raise RuntimeError(open(os.path.join(outdir, errs[0])).read())
