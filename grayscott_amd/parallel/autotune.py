@@ -284,7 +284,10 @@ def tune_data_path(settings, ctx, L: int, backend: str,
     pair_bytes = 8 if settings.dtype_name == "float32" else 16
     use_model = link is not None and os.environ.get("GS_TUNE_MODEL", "1") != "0"
     comp_step = None  # ms per step of the update alone (from the first timed row)
-    no_rccl = bool(use_model and link.get("rccl_failed") and link.get("ipc") == "ok")
+    # (only where the run's own transport would try RCCL first: an explicit host / torch / IPC
+    # transport is what the user asked to time)
+    no_rccl = bool(use_model and link.get("rccl_failed") and link.get("ipc") == "ok" and
+                   str(settings.transport).lower() in ("auto", "rccl"))
     if no_rccl:
         # the IPC rows first (stable: the reference grid's IPC rows lead them)
         cands = ([c for c in cands if len(c) > 4 and c[4] == "ipc"] +

@@ -201,3 +201,29 @@ def test_tuner_skips_what_the_model_rules_out(monkeypatch, rate, rccl_failed):
             if r.get("skipped"):
                 assert r["skipped"] == "model" and r["dims"] not in ([1, 1, 8], bal), r
                 assert r["overlap_req"] != "off" and r.get("transport_req") != "ipc", r
+
+
+def test_explicit_transport_rows_are_timed_even_without_rccl(monkeypatch):
+    """--transport host (or torch / ipc): the rows the user pinned the run's transport for are
+    timed although the probe found RCCL unusable (only "auto" / "rccl" runs skip their host
+    fallbacks)."""
+    from grayscott_amd.utils.config import Settings
+    timed = []
+
+    def fake_check(ctx, backend, dims, f, tr, ov, **kw):
+        return True, 0.0, tr, None
+
+    def fake_time(s, ctx, L, dims, f, steps=0, warmup=0, skip_rccl=False, info=None):
+        timed.append(s.transport)
+        if info is not None:
+            info["comp_ms_per_step"] = 0.16
+        return 0.2 * steps * 1e-3, False
+
+    monkeypatch.setattr(autotune, "selfcheck", fake_check)
+    monkeypatch.setattr(autotune, "time_data_path", fake_time)
+    link = {"summary": {"ipc_us_max": {"4096": 10.0, str(8 << 20): 30.0}},
+            "rccl_failed": True, "ipc": "ok"}
+    s = Settings(L=512, precision="Float32", backend="AMDGPU", transport="host")
+    out = autotune.tune_data_path(s, _OneRankView(), 512, "hip", steps=10, warmup=1, link=link)
+    assert not any(str(r.get("skipped", "")).startswith("rccl unavailable") for r in out["table"])
+    assert "host" in timed
