@@ -96,13 +96,23 @@ def probe_links(ctx, sizes: Sequence[int] = PROBE_SIZES, reps: int = 5, rccl: bo
                 except Exception as ex:
                     err["ipc"] = f"rank {ctx.rank} -> {peer}: {ex}"[:200]
     rccl_state = "not probed"
-    if rccl and probe is not None:
-        uid = native.rccl_unique_id() if ctx.rank == 0 else None
+    # every rank takes the same branch (a rank whose probe buffers failed must not skip the
+    # collectives its peers make below)
+    have = ctx.allreduce(1.0 if probe is not None else 0.0, "min") > 0
+    if rccl and have:
+        uid = None
+        if ctx.rank == 0:
+            try:
+                uid = native.rccl_unique_id()
+            except Exception as ex:  # broadcast as None: every rank reports the failure
+                err["rccl"] = f"rank 0: {ex}"[:200]
         uid = ctx.broadcast_object(uid, src=0)
         try:
+            if uid is None:
+                raise RuntimeError("no RCCL unique id (rank 0 could not create one)")
             probe.rccl_init(uid, ctx.world_size, ctx.rank)
         except Exception as ex:
-            err["rccl"] = f"rank {ctx.rank}: {ex}"[:200]
+            err["rccl"] = err["rccl"] or f"rank {ctx.rank}: {ex}"[:200]
         rccl_ok = ctx.allreduce(0.0 if err["rccl"] else 1.0, "min") > 0
         if rccl_ok:
             for pairs in rounds:

@@ -227,3 +227,43 @@ def test_explicit_transport_rows_are_timed_even_without_rccl(monkeypatch):
     out = autotune.tune_data_path(s, _OneRankView(), 512, "hip", steps=10, warmup=1, link=link)
     assert not any(str(r.get("skipped", "")).startswith("rccl unavailable") for r in out["table"])
     assert "host" in timed
+
+
+def _probe_worker(rank, world, port, outdir):
+    import json
+    import os
+    import sys
+
+    from .mp_utils import ROOT
+    sys.path.insert(0, ROOT)
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": "0",
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    from grayscott_amd.parallel import dist as gdist
+    from grayscott_amd.parallel.linkprobe import probe_links
+    ctx = gdist.init_from_env("cpu")
+    out = probe_links(ctx, reps=1)
+    with open(os.path.join(outdir, f"rank{rank}.json"), "w") as f:
+        json.dump(out, f)
+    ctx.barrier()
+    ctx.finalize()
+
+
+def test_probe_without_a_device_is_agreed_and_does_not_hang(tmp_path):
+    """Ranks that cannot create the probe's device buffers (no GPU here) still make the same
+    collectives: every rank returns the same record, with the IPC failure and no rates, within
+    seconds -- the failure path a node with a broken device takes before the tuner runs."""
+    import json
+
+    import torch.multiprocessing as mp
+
+    from .mp_utils import free_port
+    pc = mp.start_processes(_probe_worker, args=(2, free_port(), str(tmp_path)), nprocs=2,
+                            join=False, start_method="spawn")
+    import time
+    t0 = time.monotonic()
+    while not pc.join(60):
+        assert time.monotonic() - t0 < 120, "probe ranks hung"
+    outs = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(2)]
+    assert outs[0]["ipc"] == outs[1]["ipc"] and outs[0]["ipc"] != "ok"
+    assert outs[0]["rccl"] == "not probed" and not outs[0]["rccl_failed"]
+    assert outs[0]["summary"] == {} and len(outs[0]["pairs"]) == 1
