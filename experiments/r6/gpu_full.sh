@@ -1,10 +1,10 @@
 # Round 6 re-entry: full GPU test suite, smoke, the driver's bench command x3, K=400
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/${GS_OUT:-r6h}
+O=$R/gpurun_out/${GS_OUT:-r6l}
 mkdir -p $O
 cd $R
-timeout -k 10 900 python -u -m pytest tests -m gpu --maxfail=5 -v --timeout 120 --timeout-method thread > $O/pytest.txt 2>&1 || { tail -30 $O/pytest.txt; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -m gpu --maxfail=5 -v --timeout 300 --timeout-method thread > $O/pytest.txt 2>&1 || { tail -30 $O/pytest.txt; exit 1; }
 tail -3 $O/pytest.txt
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 || exit 1
 for i in 1 2 3; do
