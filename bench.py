@@ -108,6 +108,9 @@ def failure_record(args, status: str, n_gpus: int, **extra) -> dict:
                       "seq_len": args.L, "parallelism": f"spatial-3d ({n_gpus} ranks)"},
            "status": status, "phase": _PROGRESS["phase"],
            "data_path_tuning": list(_PROGRESS["rows"]),
+           # what the ranks measured of their links before the failure (first contact on a
+           # node: the probe runs before any candidate; None if it did not get that far)
+           "link_probe": _PROGRESS.get("link_probe"),
            "wall_s": round(time.perf_counter() - T_START, 2)}
     rec.update(extra)
     return rec
@@ -133,6 +136,18 @@ def _progress_row(row: dict) -> None:
         try:
             with open(path, "a") as f:
                 f.write(json.dumps(row) + "\n")
+        except OSError:
+            pass
+
+
+def _progress_link(link) -> None:
+    """The link probe's result (rank 0) into GS_BENCH_PROGRESS too, so a self-launching parent
+    can report it if the job dies later."""
+    path = os.environ.get("GS_BENCH_PROGRESS")
+    if path and link is not None:
+        try:
+            with open(path, "a") as f:
+                f.write(json.dumps({"link_probe": link}) + "\n")
         except OSError:
             pass
 
@@ -207,7 +222,9 @@ def self_launch(args, argv, ngpus: int) -> int:
         if os.path.exists(prog):
             with open(prog) as f:
                 rows = [json.loads(l) for l in f if l.strip()]
-        _PROGRESS["rows"] = rows
+        links = [r["link_probe"] for r in rows if "link_probe" in r]
+        _PROGRESS["link_probe"] = links[-1] if links else None
+        _PROGRESS["rows"] = [r for r in rows if "link_probe" not in r]
         _PROGRESS["phase"] = "unknown (no line from rank 0)"
         status = "timeout" if info.get("timed_out") else "rank_failed"
         rec = failure_record(args, status, ngpus, failed_rank=info.get("failed_rank"),
@@ -443,6 +460,9 @@ def run(args) -> int:
         from grayscott_amd.parallel.linkprobe import probe_links
         link = probe_links(ctx, log=lambda m: print(f"bench.py: {m}", file=sys.stderr,
                                                      flush=True))
+        _PROGRESS["link_probe"] = link
+        if ctx.rank == 0:
+            _progress_link(link)
         if link and link.get("rccl_failed"):
             # the engines' "auto" transport chain starts after RCCL (agreed: same dict everywhere)
             from grayscott_amd.models import grayscott as _gsm
