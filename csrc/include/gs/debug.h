@@ -28,6 +28,9 @@
 //   gate_mode       0 (default): the gated pass's tuner times carried, one-unit and pairs tables;
 //                   1: one-unit tables packed at the start only; 2: pairs tables only; 3: carried
 //                   one-unit tables only (tests of each kernel path).  Read at tuning.
+//   plan_order      0 (default): a planned window runs its deepest passes first (engine.h
+//                   plan_passes); 1: shallowest first (A/B of the power ramp inside a short
+//                   window).  Read at every advance().
 //   cpu_ftz         1 (default): the CPU solver flushes fp32 denormals in its step region
 //                   (MXCSR FTZ + DAZ; ~100x faster where the reference example's v field
 //                   passes through them); 0: IEEE denormals, the reference's and the GPU's
@@ -48,6 +51,7 @@ struct DebugKnobs {
   int gate_mode = 0;
   int cpu_ftz = 1;
   int gated = 1;
+  int plan_order = 0;
 };
 
 inline DebugKnobs& debug_knobs() {
@@ -68,6 +72,7 @@ inline int debug_set(const char* name, double value) {
   else if (!strcmp(name, "gate_mode")) k.gate_mode = (int)value;
   else if (!strcmp(name, "cpu_ftz")) k.cpu_ftz = value != 0.0 ? 1 : 0;
   else if (!strcmp(name, "gated")) k.gated = value >= 2.0 ? 2 : (value != 0.0 ? 1 : 0);
+  else if (!strcmp(name, "plan_order")) k.plan_order = value != 0.0 ? 1 : 0;
   else return -1;
   return 0;
 }

@@ -500,7 +500,9 @@ class Engine {
     double cost[8] = {0.0};
     const int kmax = cfg_.fuse < 7 ? cfg_.fuse : 7;
     for (int k = 2; k <= kmax; ++k) cost[k] = be_->fused_ms(k);
-    return plan_depths(cost, kmax, nsteps);
+    std::vector<int> plan = plan_depths(cost, kmax, nsteps);
+    if (debug_knobs().plan_order == 1) std::reverse(plan.begin(), plan.end());
+    return plan;
   }
   // planner off (tests, A/B): the greedy min(nsteps, depth) schedule
   void set_plan(bool on) { planner_ = on; }
