@@ -250,3 +250,38 @@ def test_fp64_lds_ring_bitwise_vs_register_ring(L, fuse, sched):
     assert np.isfinite(out[1][0]).all()
     np.testing.assert_array_equal(out[1][0], out[0][0])
     np.testing.assert_array_equal(out[1][1], out[0][1])
+
+
+@pytest.mark.parametrize("prec,fuse,cfg,sched,steps", [
+    ("Float32", 4, "4x12:1sl", 1, 240),    # T=4 LDS ring, unfolded (edge tiles at L=200)
+    ("Float32", 2, "4x12:2sfl", 0, 240),   # T=2 LDS ring, 2-plane prefetch, folded, schedule 0
+    ("Float64", 3, "4x8:1sl", 0, 120)])    # fp64 LDS ring (centre plane in registers)
+def test_lds_ring_soak_bitwise_vs_register_ring(prec, fuse, cfg, sched, steps):
+    """Soak of the LDS ring's hand-counted DMA waits (csrc/hip/fused.hpp lr_wait / pad_store): a
+    long run through an LDS-ring shape equals the register-ring T=3 run bit for bit (every fused
+    depth is bit-identical; the step counts avoid a single-step remainder, whose k_step1 kernel
+    rounds differently).  A wait that lets a DMA piece land late shows up as a mismatch at a
+    segment start (profiles/r6_f64_lr.txt, r6_lr_soak.txt)."""
+    from grayscott_amd.models.grayscott import GrayScott
+    from grayscott_amd.ops import native
+    from grayscott_amd.parallel.decomp import init_domain
+    from grayscott_amd.utils.config import Settings
+    out = []
+    try:
+        for f, c, sc in ((3, "4x12:1s" if prec == "Float32" else "4x8:1s", 2), (fuse, cfg, sched)):
+            native.fused_select(c)
+            native.fused_sched(sc)
+            s = Settings(L=200, precision=prec, F=0.02, k=0.048, dt=1.0, Du=0.2, Dv=0.1,
+                         noise=0.1, backend="AMDGPU", seed=11)
+            sim = GrayScott(s, init_domain(200, 1, 0), fuse=f)
+            try:
+                sim.init_fields()
+                sim.randomize_fields(seed=5)
+                sim.iterate(steps)
+                out.append(sim.get_fields())
+            finally:
+                sim.close()
+    finally:
+        native.fused_unpin()
+    np.testing.assert_array_equal(out[1][0], out[0][0])
+    np.testing.assert_array_equal(out[1][1], out[0][1])
