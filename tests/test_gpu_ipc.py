@@ -136,6 +136,10 @@ def _cfg(L, steps, fuse, prec="Float32", **extra):
     (4, 40, 2, "Float64", dict(decomposition="z", overlap="off")),
     (8, 36, 2, "Float32", dict(decomposition="balanced", overlap="on")),
     (4, 32, 3, "Float32", dict(decomposition="balanced", periodic=True, overlap="auto")),
+    # fuse_steps = 4 with neighbours: H = 4 halos, then the T = 4 LDS-ring pass over the whole
+    # interior (no overlapped / gated T = 4 pass exists: the sequential path)
+    (2, 64, 4, "Float32", dict(decomposition="z", overlap="auto")),
+    (4, 64, 4, "Float32", dict(decomposition="balanced", overlap="off")),
 ])
 def test_ipc_multiprocess_matches_single_rank(world, L, fuse, prec, extra):
     """Several processes on the GPU, neighbours' buffers mapped through IPC handles."""
