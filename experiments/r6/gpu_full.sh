@@ -1,7 +1,7 @@
 # Round 6 re-entry: full GPU test suite, smoke, the driver's bench command x3, K=400
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/${GS_OUT:-r6z}
+O=$R/gpurun_out/${GS_OUT:-r6final}
 mkdir -p $O
 cd $R
 timeout -k 10 900 python -u -m pytest tests -m gpu --maxfail=5 -v --timeout 300 --timeout-method thread > $O/pytest.txt 2>&1 || { tail -30 $O/pytest.txt; exit 1; }
