@@ -289,7 +289,8 @@ def tune_data_path(settings, ctx, L: int, backend: str,
     no_rccl = bool(use_model and link.get("rccl_failed") and link.get("ipc") == "ok" and
                    str(settings.transport).lower() in ("auto", "rccl"))
     if no_rccl:
-        # the IPC rows first (stable: the reference grid's IPC rows lead them)
+        # the IPC rows first, in their own order (the rows after them that fall back to the host
+        # transport are skipped once one IPC row passed)
         cands = ([c for c in cands if len(c) > 4 and c[4] == "ipc"] +
                  [c for c in cands if not (len(c) > 4 and c[4] == "ipc")])
 
