@@ -88,3 +88,19 @@ def test_write_roundtrip(tmp_path):
     p = str(tmp_path / "s.toml")
     write_settings_toml(s, p)
     assert get_settings([p]) == s
+
+
+def test_every_example_config_loads():
+    """examples/*.toml (the reference example and the BASELINE configs' settings) load through the
+    same loader as the CLI, with the reference's keys and the extensions they use."""
+    import glob
+    import os
+
+    from grayscott_amd.utils.config import load_settings
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    files = sorted(glob.glob(os.path.join(root, "examples", "*.toml")))
+    assert len(files) >= 4
+    for f in files:
+        s = load_settings(f)
+        assert s.L > 0 and s.precision in ("Float32", "Float64"), f
+        assert s.backend in ("CPU", "AMDGPU", "HIP", "CUDA"), f
