@@ -517,6 +517,8 @@ def run(args) -> int:
             time.sleep(1e6)
     ctx.barrier()
     sync()
+    # the passes the timed window will run (a host-side query: engine.h plan_passes)
+    timed_plan = sim.engine.plan_passes(args.steps) if hasattr(sim.engine, "plan_passes") else []
     _PROGRESS["phase"] = "timed region"
     t0 = time.perf_counter()
     sim.iterate(args.steps)
@@ -604,7 +606,10 @@ def run(args) -> int:
                                           "ms": round(float(c[2]), 4)}
                                  for n, c in sim.fused_choice().items()},
                 # the timed window's passes (engine.h plan_passes; [] = greedy by fuse_steps)
-                "pass_plan": sim.engine.plan_passes(args.steps),
+                "pass_plan": timed_plan,
+                # one outer-ghost refresh (ms): the planner's price of a depth-parity switch
+                "bc_fill_ms": (round(sim.engine.fill_ms(), 4)
+                               if hasattr(sim.engine, "fill_ms") else None),
                 "transport": sim.transport,
                 "overlap": sim.overlapped,
                 "gated": sim.gated,

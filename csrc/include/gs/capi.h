@@ -40,6 +40,11 @@ int gs_set_plan(gs_engine* e, int32_t on);        // pass-depth planner on (defa
 int gs_plan_passes(gs_engine* e, int64_t nsteps, int32_t* out, int32_t cap);
 // gs::plan_depths for given pass times cost[0..kmax] (cost[k]: depth k; kmax <= 7)
 int gs_plan_depths(const double* cost, int32_t kmax, int64_t nsteps, int32_t* out, int32_t cap);
+// the same with the outer-ghost refresh priced: `fill` per depth-parity switch, pp the parity a
+// first pass needs to avoid one (-1: none)
+int gs_plan_depths_bc(const double* cost, int32_t kmax, int64_t nsteps, double fill, int32_t pp,
+                      int32_t* out, int32_t cap);
+double gs_fill_ms(gs_engine* e);                 // one refresh as timed by prepare (ms)
 int gs_plan_zplanes(gs_engine* e);               // 1 if halos are whole contiguous z planes
 int gs_fused_runs_raw(gs_engine* e, int32_t k, int32_t zlo0, int32_t zlen0, int32_t zlo1,
                       int32_t zlen1, int32_t mask, int32_t leave_room);  // timing (state unchanged)

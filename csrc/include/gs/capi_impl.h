@@ -121,6 +121,14 @@ int gs_plan_depths(const double* cost, int32_t kmax, int64_t nsteps, int32_t* ou
   for (size_t i = 0; i < p.size() && (int32_t)i < cap; ++i) out[i] = p[i];
   return (int)p.size();
 }
+int gs_plan_depths_bc(const double* cost, int32_t kmax, int64_t nsteps, double fill, int32_t pp,
+                      int32_t* out, int32_t cap) {
+  if (kmax < 2 || kmax > 7) return -1;
+  const std::vector<int> p = gs::plan_depths(cost, kmax, nsteps, fill, pp);
+  for (size_t i = 0; i < p.size() && (int32_t)i < cap; ++i) out[i] = p[i];
+  return (int)p.size();
+}
+double gs_fill_ms(gs_engine* e) { return e->eng->fill_ms(); }
 int gs_plan_passes(gs_engine* e, int64_t nsteps, int32_t* out, int32_t cap) {
   try {
     const std::vector<int> p = e->eng->plan_passes(nsteps);

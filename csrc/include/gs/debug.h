@@ -31,6 +31,9 @@
 //   plan_order      0 (default): a planned window runs its deepest passes first (engine.h
 //                   plan_passes); 1: shallowest first (A/B of the power ramp inside a short
 //                   window).  Read at every advance().
+//   plan_fill       1 (default): the planner prices a depth-parity switch at one outer-ghost
+//                   refresh (engine.h plan_depths, Engine::fill_ms); 0: refreshes not counted
+//                   (A/B).  Read at every advance().
 //   cpu_ftz         1 (default): the CPU solver flushes fp32 denormals in its step region
 //                   (MXCSR FTZ + DAZ; ~100x faster where the reference example's v field
 //                   passes through them); 0: IEEE denormals, the reference's and the GPU's
@@ -52,6 +55,7 @@ struct DebugKnobs {
   int cpu_ftz = 1;
   int gated = 1;
   int plan_order = 0;
+  int plan_fill = 1;
 };
 
 inline DebugKnobs& debug_knobs() {
@@ -73,6 +77,7 @@ inline int debug_set(const char* name, double value) {
   else if (!strcmp(name, "cpu_ftz")) k.cpu_ftz = value != 0.0 ? 1 : 0;
   else if (!strcmp(name, "gated")) k.gated = value >= 2.0 ? 2 : (value != 0.0 ? 1 : 0);
   else if (!strcmp(name, "plan_order")) k.plan_order = value != 0.0 ? 1 : 0;
+  else if (!strcmp(name, "plan_fill")) k.plan_fill = value != 0.0 ? 1 : 0;
   else return -1;
   return 0;
 }

@@ -162,18 +162,29 @@ class Backend {
 };
 
 // The cheapest partition of nsteps into passes of depth 2..kmax, given each depth's pass time
-// cost[k] (all > 0, else an empty plan), deepest passes first: an exact dynamic programme over the
-// last kPlanTail steps, before them passes of the depth with the lowest time per step.  nsteps = 1
-// is a lone single step (depth 1).  (Engine::plan_passes; tests/test_planner.py.)
+// cost[k] (all > 0, else an empty plan): an exact dynamic programme over the last kPlanTail
+// steps, before them passes of the depth with the lowest time per step.  nsteps = 1 is a lone
+// single step (depth 1).  (Engine::plan_passes; tests/test_planner.py.)
+//   fill = 0: deepest passes first.  fill > 0 (non-periodic grids): one outer-ghost refresh
+// (Engine::ensure_bc) costs `fill`, and one runs whenever two consecutive passes differ in depth
+// parity -- the buffer read next is then read at the other time parity than when it was last
+// filled; pp is the depth parity a first pass needs to avoid one (-1: no preference).  The plan
+// is then the cheapest of the best all-even, all-odd and mixed partitions with those refreshes
+// counted, its passes grouped by parity (pp's group first), deepest first within a group:
+// 4,4,3,3,3,3 after an even pass, not 3,3,3,3,4,4.
 constexpr int64_t kPlanTail = 240;
-inline std::vector<int> plan_depths(const double* cost, int kmax, int64_t nsteps) {
+namespace plan_detail {
+// the cheapest partition using the depths whose parity bit is in `allow` (bit0 even, bit1 odd);
+// *total = 1e300 if there is none
+inline std::vector<int> solve(const double* cost, int kmax, int64_t nsteps, int allow,
+                              double* total) {
   std::vector<int> out;
-  if (nsteps < 1 || kmax < 2) return out;
+  *total = 1e300;
+  auto ok = [&](int k) { return ((allow >> (k & 1)) & 1) != 0; };
   int dbest = 0;
-  for (int k = 2; k <= kmax; ++k) {
-    if (!(cost[k] > 0.0)) return out;
-    if (dbest == 0 || cost[k] / k < cost[dbest] / dbest) dbest = k;
-  }
+  for (int k = 2; k <= kmax; ++k)
+    if (ok(k) && (dbest == 0 || cost[k] / k < cost[dbest] / dbest)) dbest = k;
+  if (dbest == 0) return out;
   const int64_t head = nsteps > kPlanTail ? (nsteps - kPlanTail) / dbest : 0;
   const int tail = (int)(nsteps - head * dbest);
   std::vector<double> best((size_t)tail + 1, 1e300);
@@ -181,16 +192,60 @@ inline std::vector<int> plan_depths(const double* cost, int kmax, int64_t nsteps
   best[0] = 0.0;
   for (int m = 2; m <= tail; ++m)
     for (int k = kmax; k >= 2; --k)  // ties: the deeper pass (fewer launches)
-      if (k <= m && best[(size_t)(m - k)] + cost[k] < best[(size_t)m] * (1.0 - 1e-12)) {
+      if (ok(k) && k <= m && best[(size_t)(m - k)] < 1e300 &&
+          best[(size_t)(m - k)] + cost[k] < best[(size_t)m] * (1.0 - 1e-12)) {
         best[(size_t)m] = best[(size_t)(m - k)] + cost[k];
         how[(size_t)m] = k;
       }
+  if (tail == 1) {
+    if (!(allow & 2)) return out;  // a lone single step is odd
+  } else if (!(best[(size_t)tail] < 1e300)) {
+    return out;
+  }
   out.assign((size_t)head, dbest);
-  std::vector<int> t;
-  for (int m = tail; m >= 2; m -= how[(size_t)m]) t.push_back(how[(size_t)m]);
-  if (tail == 1) t.push_back(1);
-  std::sort(t.begin(), t.end(), [](int x, int y) { return x > y; });
-  out.insert(out.end(), t.begin(), t.end());
+  for (int m = tail; m >= 2; m -= how[(size_t)m]) out.push_back(how[(size_t)m]);
+  if (tail == 1) out.push_back(1);
+  *total = (double)head * cost[dbest] + (tail == 1 ? 0.0 : best[(size_t)tail]);
+  return out;
+}
+}  // namespace plan_detail
+
+inline std::vector<int> plan_depths(const double* cost, int kmax, int64_t nsteps,
+                                    double fill = 0.0, int pp = -1) {
+  std::vector<int> out;
+  if (nsteps < 1 || kmax < 2) return out;
+  for (int k = 2; k <= kmax; ++k)
+    if (!(cost[k] > 0.0)) return out;
+  double tot = 0.0;
+  if (!(fill > 0.0)) {
+    out = plan_detail::solve(cost, kmax, nsteps, 3, &tot);
+    std::sort(out.begin(), out.end(), [](int x, int y) { return x > y; });
+    return out;
+  }
+  // the refreshes a plan made of these parities needs (grouped, pp's group first)
+  auto refreshes = [&](const std::vector<int>& p) {
+    bool ev = false, od = false;
+    for (int k : p) (k & 1 ? od : ev) = true;
+    if (ev && od) return 1;
+    if (pp < 0 || p.empty()) return 0;
+    return (od ? 1 : 0) != pp ? 1 : 0;
+  };
+  double best = 1e300;
+  for (int allow : {3, 1, 2}) {  // ties: the plain optimum
+    double t = 0.0;
+    std::vector<int> p = plan_detail::solve(cost, kmax, nsteps, allow, &t);
+    if (!(t < 1e300)) continue;
+    t += fill * refreshes(p);
+    if (t < best * (1.0 - 1e-12)) {
+      best = t;
+      out = p;
+    }
+  }
+  const int first = pp >= 0 ? pp : (out.empty() ? 0 : (*std::max_element(out.begin(), out.end()) & 1));
+  std::sort(out.begin(), out.end(), [first](int x, int y) {
+    const int gx = (x & 1) != first, gy = (y & 1) != first;
+    return gx != gy ? gx < gy : x > y;
+  });
   return out;
 }
 
@@ -331,6 +386,23 @@ class Engine {
       // profiles/r2_fuse_small.txt), else the full depth up to T=3 (the untuned T=4 tile is the
       // unfolded one, 10 % under T=3 at L=512: profiles/r6_t4.txt)
       if (best == 0.0) depth_ = (cfg_.g.nx < 160 || cfg_.g.ny < 160) ? 2 : (cfg_.fuse > 3 ? 3 : 0);
+    }
+    // the planner's price of a parity switch: one outer-ghost refresh of the other buffer
+    // (timed on the device's clock; its contents are reset just below)
+    fill_ms_ = 0.0;
+    if (!cfg_.g.periodic && !has_remote_ && planner_ && !plog_.on) {
+      constexpr int kReps = 4;
+      be_->prof_reserve(2);
+      be_->prof_mark(0, -1);
+      for (int r = 0; r < kReps; ++r) {
+        bc_parity_[1 - cur_] = -1;
+        ensure_bc(1 - cur_, t_ + r);
+      }
+      be_->prof_mark(1, -1);
+      be_->host_sync();
+      double us[2] = {0.0, 0.0};
+      be_->prof_times(us, 2);
+      fill_ms_ = us[1] > us[0] ? (us[1] - us[0]) * 1e-3 / kReps : 0.0;
     }
     // the timing runs scribbled over the other buffer: restore the reference's zeroed
     // u_temp/v_temp (ghosts included) so the ghost-parity bookkeeping stays exact
@@ -500,20 +572,30 @@ class Engine {
     double cost[8] = {0.0};
     const int kmax = cfg_.fuse < 7 ? cfg_.fuse : 7;
     for (int k = 2; k <= kmax; ++k) cost[k] = be_->fused_ms(k);
-    std::vector<int> plan = plan_depths(cost, kmax, nsteps);
+    // a first pass of depth parity pp reads the other buffer next at the time parity its outer
+    // ghosts already hold (ensure_bc); unknown ghosts need a refresh whatever the plan
+    const int by = bc_parity_[1 - cur_];
+    const int pp = by >= 0 ? by ^ (int)(t_ & 1) : -1;
+    std::vector<int> plan = plan_depths(cost, kmax, nsteps,
+                                         cfg_.g.periodic || !debug_knobs().plan_fill ? 0.0 : fill_ms_, pp);
     if (debug_knobs().plan_order == 1) std::reverse(plan.begin(), plan.end());
     return plan;
   }
   // planner off (tests, A/B): the greedy min(nsteps, depth) schedule
   void set_plan(bool on) { planner_ = on; }
+  // milliseconds of one outer-ghost refresh as timed by prepare() (0: periodic or not timed)
+  double fill_ms() const { return fill_ms_; }
 
   void advance(int64_t nsteps) {
     const std::vector<int> plan = plan_passes(nsteps);
     if (!plan.empty()) {
       for (int k : plan) advance_depth(k, k);
-      return;
+    } else {
+      advance_depth(nsteps, depth());
     }
-    advance_depth(nsteps, depth());
+    // the state at t_ is whole, outer ghosts included: the refresh its last pass made
+    // necessary belongs to this call, not to the next one (a no-op if the parity holds)
+    if (nsteps > 0) ensure_bc(cur_, t_);
   }
 
  private:
@@ -726,6 +808,7 @@ class Engine {
   bool gate_ = debug_knobs().gated != 0;
   uint32_t gate_depths_ = 0xffffffffu;  // set_gated_depth
   bool planner_ = true;  // plan_passes (set_plan)
+  double fill_ms_ = 0.0;  // prepare(): one ensure_bc refresh (the planner's parity-switch cost)
   enum { kNone, kUnpack, kCallback };
   int xpending_ = kNone;
   int cur_ = 0;

@@ -235,17 +235,27 @@ def gate_plan(g: Geom, nbr27, n: int, xp: int = 0, allpk: bool = False, slots: i
     return units, int(npk.value), dict(zip(keys, list(grid)))
 
 
-def plan_depths(cost: dict, nsteps: int) -> list:
+def plan_depths(cost: dict, nsteps: int, fill: float = 0.0, pp: int = -1) -> list:
     """gs::plan_depths (engine.h): the cheapest partition of ``nsteps`` into fused passes of
-    depth 2..max(cost), given each depth's pass time ``cost[k]``; deepest passes first."""
+    depth 2..max(cost), given each depth's pass time ``cost[k]``; deepest passes first.  With
+    ``fill`` > 0 every depth-parity switch between consecutive passes costs one outer-ghost
+    refresh of ``fill`` (``pp``: the parity a first pass needs to avoid one, -1 none), and the
+    passes come grouped by parity."""
     lib = load("core")
     kmax = max(cost)
     arr = (c_double * 8)(*[float(cost.get(k, 0.0)) for k in range(8)])
-    lib.gs_plan_depths.argtypes = [POINTER(c_double), c_int32, c_int64, POINTER(c_int32), c_int32]
-    lib.gs_plan_depths.restype = c_int
     cap = 1 << 16
     out = (c_int32 * cap)()
-    n = lib.gs_plan_depths(arr, int(kmax), int(nsteps), out, cap)
+    if fill > 0.0 or pp >= 0:
+        lib.gs_plan_depths_bc.argtypes = [POINTER(c_double), c_int32, c_int64, c_double, c_int32,
+                                          POINTER(c_int32), c_int32]
+        lib.gs_plan_depths_bc.restype = c_int
+        n = lib.gs_plan_depths_bc(arr, int(kmax), int(nsteps), float(fill), int(pp), out, cap)
+    else:
+        lib.gs_plan_depths.argtypes = [POINTER(c_double), c_int32, c_int64, POINTER(c_int32),
+                                       c_int32]
+        lib.gs_plan_depths.restype = c_int
+        n = lib.gs_plan_depths(arr, int(kmax), int(nsteps), out, cap)
     if n < 0:
         raise ValueError("plan_depths: depths must be 2..7")
     return [int(out[i]) for i in range(min(n, cap))]
@@ -386,6 +396,12 @@ class Engine:
         self.lib.gs_set_plan.argtypes = [c_void_p, c_int32]
         self.lib.gs_set_plan.restype = c_int
         self._chk(self.lib.gs_set_plan(self.h, 1 if on else 0), "set_plan")
+
+    def fill_ms(self) -> float:
+        """One outer-ghost refresh as timed by prepare() (the planner's parity-switch cost)."""
+        self.lib.gs_fill_ms.argtypes = [c_void_p]
+        self.lib.gs_fill_ms.restype = c_double
+        return float(self.lib.gs_fill_ms(self.h))
 
     def plan_passes(self, nsteps: int) -> list:
         """The pass depths advance(nsteps) runs ([] = the greedy min(nsteps, depth) schedule:

@@ -20,7 +20,7 @@ def debug_knob():
     from grayscott_amd.ops import native
     defaults = {"overlap_chain": 1, "philox_generic": 0, "ipc_emulate_us": 0,
                 "ipc_system_stores": 0, "cpu_ftz": 1, "gated": 1, "gate_stamps": 0,
-                "ipc_pair_same_dir": 0, "gate_mode": 0, "plan_order": 0}
+                "ipc_pair_same_dir": 0, "gate_mode": 0, "plan_order": 0, "plan_fill": 1}
     touched = []
 
     def _set(name, value, which="hip"):

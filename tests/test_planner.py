@@ -84,3 +84,54 @@ def test_engine_without_timed_depths_keeps_the_greedy_schedule():
         assert sim.engine.plan_passes(20) == []
     finally:
         sim.close()
+
+
+def _refreshes(plan, pp):
+    """Outer-ghost refreshes a plan needs: one per depth-parity switch between consecutive
+    passes, plus one if the first pass's parity is not ``pp`` (engine.h ensure_bc)."""
+    n = sum(1 for a, b in zip(plan, plan[1:]) if (a & 1) != (b & 1))
+    if plan and pp >= 0 and (plan[0] & 1) != pp:
+        n += 1
+    return n
+
+
+def test_parity_switches_are_priced():
+    c = {2: 0.4625, 3: 0.5137, 4: 0.6905}  # 4,4,3,3,3,3 = 3.4358 vs 5 x 4 = 3.4525
+    # no refresh cost: the plain optimum, deepest first
+    assert native.plan_depths(c, 20, 0.0, -1) == [4, 4, 3, 3, 3, 3]
+    # after an even pass (pp = 0) the mixed plan needs one refresh; at 16 us it still wins
+    assert native.plan_depths(c, 20, 0.016, 0) == [4, 4, 3, 3, 3, 3]
+    # after an odd pass the odd group goes first (one refresh, not two)
+    assert native.plan_depths(c, 20, 0.016, 1) == [3, 3, 3, 3, 4, 4]
+    # a dearer refresh: the all-even plan needs none after an even pass
+    assert native.plan_depths(c, 20, 0.030, 0) == [4, 4, 4, 4, 4]
+
+
+def test_parity_aware_plans_are_optimal():
+    rng = random.Random(11)
+    for _ in range(40):
+        kmax = rng.choice([3, 4, 5])
+        cost = {k: rng.uniform(0.3, 1.0) * k ** rng.uniform(0.6, 1.1) for k in range(2, kmax + 1)}
+        fill = rng.uniform(0.0, 0.3)
+        for pp in (-1, 0, 1):
+            for n in [2, 3, 5, 7, 10, 20, 23]:
+                p = native.plan_depths(cost, n, fill, pp)
+                assert sum(p) == n and all(2 <= k <= kmax for k in p)
+                got = _cost(p, cost) + fill * _refreshes(p, pp)
+                # brute force over every multiset, arranged with the fewest refreshes
+                best = 1e300
+
+                def walk(m, kmin, acc):
+                    nonlocal best
+                    if m == 0:
+                        ev = any(k % 2 == 0 for k in acc)
+                        od = any(k % 2 for k in acc)
+                        r = 1 if ev and od else (1 if pp >= 0 and (1 if od else 0) != pp else 0)
+                        best = min(best, _cost(acc, cost) + fill * r)
+                        return
+                    for k in range(kmin, kmax + 1):
+                        if k <= m:
+                            walk(m - k, k, acc + [k])
+
+                walk(n, 2, [])
+                assert got == pytest.approx(best, rel=1e-9, abs=1e-12)
