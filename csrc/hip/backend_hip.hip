@@ -321,6 +321,7 @@ class HipBackend final : public gs::Backend {
   }
 
   bool has_comm_stream() const override { return comm_stream_ != nullptr; }
+  hipStream_t main_stream() const { return stream_; }
   void comm_fork() override {
     HIP_CHECK(hipEventRecord(ev_fork_, stream_));
     HIP_CHECK(hipStreamWaitEvent(comm_stream_, ev_fork_, 0));
@@ -1445,6 +1446,51 @@ int gs_rccl_unique_id(char* out, int32_t cap) {
 int gs_rccl_info(gs_engine* e, int32_t dtype, int32_t* out3) {
   try {
     with_hip_backend(e, dtype, [&](auto* b) { b->comm_info(out3); });
+    return 0;
+  } catch (const std::exception& ex) {
+    g_gs_err = ex.what();
+    return -1;
+  }
+}
+
+// Timing experiment (experiments/r6/graph_probe_engine.py): microseconds per step of `reps` x
+// advance(nsteps) enqueued as usual (out2[0]) and of the same advance(nsteps) captured once into a
+// hipGraph and replayed `reps` times (out2[1]).  The replays repeat the captured time step, so the
+// state afterwards is NOT a valid simulation state: timing only.
+int gs_graph_probe(gs_engine* e, int32_t dtype, int64_t nsteps, int32_t reps, double* out2) {
+  try {
+    hipStream_t st = nullptr;
+    with_hip_backend(e, dtype, [&](auto* b) { st = b->main_stream(); });
+    hipEvent_t a, z;
+    HIP_CHECK(hipEventCreate(&a));
+    HIP_CHECK(hipEventCreate(&z));
+    e->eng->advance(nsteps);  // warm
+    HIP_CHECK(hipStreamSynchronize(st));
+    HIP_CHECK(hipEventRecord(a, st));
+    for (int r = 0; r < reps; ++r) e->eng->advance(nsteps);
+    HIP_CHECK(hipEventRecord(z, st));
+    HIP_CHECK(hipEventSynchronize(z));
+    float ms = 0.f;
+    HIP_CHECK(hipEventElapsedTime(&ms, a, z));
+    out2[0] = 1e3 * ms / ((double)reps * nsteps);
+    hipGraph_t g = nullptr;
+    hipGraphExec_t ge = nullptr;
+    HIP_CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+    e->eng->advance(nsteps);
+    HIP_CHECK(hipStreamEndCapture(st, &g));
+    HIP_CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    HIP_CHECK(hipGraphLaunch(ge, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    HIP_CHECK(hipEventRecord(a, st));
+    for (int r = 0; r < reps; ++r) HIP_CHECK(hipGraphLaunch(ge, st));
+    HIP_CHECK(hipEventRecord(z, st));
+    HIP_CHECK(hipEventSynchronize(z));
+    HIP_CHECK(hipEventElapsedTime(&ms, a, z));
+    out2[1] = 1e3 * ms / ((double)reps * nsteps);
+    (void)hipGraphExecDestroy(ge);
+    (void)hipGraphDestroy(g);
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(z);
     return 0;
   } catch (const std::exception& ex) {
     g_gs_err = ex.what();
